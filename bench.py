@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident SST block decode throughput (BASELINE.json).
+
+One "step" = one batched ReadBlockWithStat over the whole per-GPU workload
+(okv_decode_blocks: count + scan + copy kernels), inputs already resident in
+HBM.  Default workload = BASELINE.json configs[2] (C3): 65 536 x 64 KiB
+blocks, Zipf key 8-256 B / value 0-4096 B, full decode (keys and values
+materialised into packed arenas + SoA row index: Go's fresh-copy semantics).
+
+Multi-GPU (launched by torch.distributed.run): one process per GPU, each
+decodes its own segment (seed 3 + rank) -- blocks/segments are independent,
+so there is no data-path collective (weak scaling).  Timing: barrier +
+synchronize on both sides of K steps, max over ranks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2]
+                    [--mode full|index] [--no-cpu] [--e2e]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident SST block decode + M rows/s, at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+CONFIGS = {
+    # name: (synth kind, seed, nblocks, threshold, block size, description)
+    "c3": (1, 3, 65536, 57344, 65536,
+           "C3: 65536 x 64 KiB blocks, Zipf key 8-256 B / value 0-4096 B"),
+    "c2": (0, 1, 256, 3584, 4096, "C2: 256 x 4 KiB blocks, fixed 16 B key / 64 B value"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--mode", default="full", choices=["full", "index"])
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--e2e", action="store_true", help="also time the host-buffer path")
+    args = ap.parse_args()
+
+    import torch
+
+    import objectkv_amd as okv
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local)
+
+    kind, seed0, nblk, th, bs, desc = CONFIGS[args.config]
+    seed = seed0 + rank
+    t0 = time.time()
+    w = okv.synth_segment(kind, seed, nblocks=nblk, threshold=th, block_size=bs)
+    seg = w.data_view()
+    descs = w.descs()[:nblk]
+    log(f"[rank {rank}] generated {seg.nbytes / 2**30:.2f} GiB segment "
+        f"({nblk} blocks) in {time.time() - t0:.1f}s")
+    in_bytes = int(descs[:, 1].sum())  # sum BlockSize (headline GiB/s numerator)
+    orig_bytes = int(descs[:, 2].sum())
+
+    # ---- device-resident inputs ---------------------------------------------
+    stream = torch.cuda.current_stream(dev)
+    dec = okv.Decoder(local, stream=stream.cuda_stream)
+    seg_t = torch.empty(seg.nbytes + 64, dtype=torch.uint8, device=dev)
+    seg_t[:seg.nbytes].copy_(torch.from_numpy(seg))
+    d_t = torch.from_numpy(descs.view(np.int64).copy()).to(dev)
+    index_only = args.mode == "index"
+    rows, kb, vb = dec.plan_device(seg_t, seg.nbytes, d_t, nblk, index_only=index_only)
+    out = dict(row_start=torch.empty(nblk + 1, dtype=torch.int64, device=dev),
+               key_base=torch.empty(nblk, dtype=torch.int64, device=dev),
+               val_base=torch.empty(nblk, dtype=torch.int64, device=dev),
+               status=torch.empty(nblk, dtype=torch.int32, device=dev),
+               key_off=torch.empty(rows, dtype=torch.int64, device=dev),
+               key_len=torch.empty(rows, dtype=torch.int16, device=dev),
+               val_off=torch.empty(rows, dtype=torch.int64, device=dev),
+               val_len=torch.empty(rows, dtype=torch.int32, device=dev),
+               key_arena=torch.empty(max(kb, 16), dtype=torch.uint8, device=dev),
+               val_arena=torch.empty(max(vb, 16), dtype=torch.uint8, device=dev))
+    payload = int(kb + vb)  # padded arena bytes written
+
+    def step(sync=False):
+        return dec.decode_device(seg_t, seg.nbytes, d_t, nblk, out, index_only=index_only,
+                                 sync=sync)
+
+    # correctness guard on the bench path itself (totals + statuses)
+    o = step(sync=True)
+    assert o.n_rows == rows and o.n_bad_blocks == 0, (o.n_rows, rows, o.n_bad_blocks)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    # ---- timed region ----------------------------------------------------------
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dec.profile(True)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    t_elapsed = time.perf_counter() - t_start
+    if dist:
+        dist.barrier()
+    kern_ms, calls = dec.profile_read()
+    dec.profile(False)
+    t_max = t_elapsed
+    if dist:
+        tt = torch.tensor([t_elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+    ms_per_step = 1e3 * t_max / args.steps
+
+    # ---- roofline for the dominant kernel (pass 3) ------------------------------
+    copy_ms = kern_ms["copy"] / max(calls, 1)
+    count_ms = kern_ms["count"] / max(calls, 1)
+    scan_ms = kern_ms["scan"] / max(calls, 1)
+    if index_only:
+        # index mode reads only the record headers: 6 B per row (+ the descs)
+        alg = rows * 6 + rows * 22 + nblk * 12
+    else:
+        # read OriginalSize per block; write payload (padded arenas) + 22 B/row
+        # SoA (u64 key_off, u16 key_len, u64 val_off, u32 val_len) + 28 B/block
+        alg = orig_bytes + payload + rows * 22 + nblk * 28
+    achieved = alg / (copy_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}_{args.mode}.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            traffic = json.load(f).get("copy_kernel_hbm_bytes_per_launch")
+
+    # ---- CPU baseline (rank 0, N = 1 only) ---------------------------------------
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle import coracle
+        threads = min(16, os.cpu_count() or 1)
+        cd = coracle.descs_array([tuple(int(x) for x in d) for d in descs])
+        res = {}
+        for nth in (1, threads):
+            # bounded sample: whole passes over the first blocks until the budget is spent
+            sample = nblk if args.config != "c3" else 4096 * nth
+            sample = min(sample, nblk)
+            n_pass, t_cpu, nrows_cpu = 0, 0.0, 0
+            budget = args.cpu_seconds / 2
+            while t_cpu < budget:
+                t1 = time.perf_counter()
+                r_, _pay = coracle.decode_go(seg, cd[:sample], 0, nth)
+                t_cpu += time.perf_counter() - t1
+                n_pass += 1
+                nrows_cpu += r_
+            sbytes = int(descs[:sample, 1].sum()) * n_pass
+            res[nth] = (sbytes / t_cpu / 2**30, nrows_cpu / t_cpu, sample, n_pass, t_cpu)
+        v1, vN = res[1], res[threads]
+        cpu = {"value": round(vN[0], 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+               "rows_per_s": round(vN[1]), "single_thread_value": round(v1[0], 4),
+               "single_thread_rows_per_s": round(v1[1]),
+               "sample": (f"{vN[2]} of {nblk} blocks x {vN[3]} passes ({vN[4]:.1f}s) on "
+                          f"{threads} threads; 1 thread: {v1[2]} blocks x {v1[3]} passes "
+                          f"({v1[4]:.1f}s); C restatement of Go ReadBlockWithStat with Go "
+                          f"allocation semantics (Go toolchain unavailable); host CPU: "
+                          f"{cpu_model()}, nproc={os.cpu_count()}")}
+
+    # ---- optional end-to-end (host buffers, PCIe both ways) -----------------------
+    e2e = None
+    if args.e2e and rank == 0:
+        t1 = time.perf_counter()
+        n_e2e = 3
+        for _ in range(n_e2e):
+            got = dec.decode(seg, descs, index_only=index_only)
+        t_e2e = (time.perf_counter() - t1) / n_e2e
+        e2e = {"GiB_s": round(in_bytes / t_e2e / 2**30, 3), "ms": round(t_e2e * 1e3, 2),
+               "note": "pageable host buffers, H2D + plan + decode + D2H, synchronous"}
+        del got
+
+    total_in = in_bytes * world
+    total_rows = rows * world
+    value = total_in / (t_max / args.steps) / 2**30
+    line = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": desc + (", full decode (arenas + SoA)" if not index_only
+                                       else ", index-only spans"),
+                   "blocks_per_gpu": nblk, "segment_bytes_per_gpu": int(seg.nbytes),
+                   "block_bytes_per_gpu": in_bytes, "original_bytes_per_gpu": orig_bytes,
+                   "rows_per_gpu": int(rows), "mode": args.mode,
+                   "parallelism": f"{world} independent segments (no collective)"},
+        "rows_per_s": round(total_rows / (t_max / args.steps)),
+        "mrows_per_s": round(total_rows / (t_max / args.steps) / 1e6, 3),
+        "original_GiB_s": round(orig_bytes * world / (t_max / args.steps) / 2**30, 3),
+        "kernel_ms": {"count": round(count_ms, 4), "scan": round(scan_ms, 4),
+                      "copy": round(copy_ms, 4)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel": "okv_copy_kernel" if not index_only
+                     else "okv_index_kernel", "algorithmic_bytes_per_launch": int(alg)},
+        "cpu_baseline": cpu,
+    }
+    if e2e:
+        line["e2e"] = e2e
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    dec.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

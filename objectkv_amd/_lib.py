@@ -1,0 +1,116 @@
+"""ctypes binding of libokv_sst.so (include/okv_sst.h, include/okv_host.h).
+
+The product path: every decode goes through the HIP kernels in this library.
+There is no CPU fallback -- if the library is missing or no GPU is present,
+the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libokv_sst.so")
+
+# ---- constants (include/okv_sst.h) -------------------------------------------
+OKV_OK, OKV_E_ARG, OKV_E_HIP, OKV_E_CAPACITY, OKV_E_NOMEM, OKV_E_NODEV = 0, -1, -2, -3, -4, -5
+BLK_OK, BLK_EOF, BLK_SHORT, BLK_PANIC, BLK_UNSUPPORTED, BLK_CAPACITY = 0, 1, 2, 3, 4, 5
+COMP_NONE, COMP_ZSTD, COMP_LZ4 = 0, 1, 2
+F_DEVICE_PTRS, F_INDEX_ONLY, F_ASYNC = 1, 2, 4
+SYNTH_FIXED, SYNTH_ZIPF = 0, 1
+
+# exported symbols declared by include/*.h (checked by tests/test_abi.py)
+SYMBOLS = [
+    "okv_open", "okv_open_on_stream", "okv_close", "okv_last_error", "okv_stream", "okv_sync",
+    "okv_abi_version", "okv_decode_plan", "okv_decode_blocks", "okv_decode_totals",
+    "okv_xxh64", "okv_hash_blocks", "okv_device_alloc", "okv_device_free", "okv_host_alloc",
+    "okv_host_free", "okv_memcpy", "okv_profile", "okv_profile_read",
+    "okv_writer_new", "okv_writer_write_row", "okv_writer_close", "okv_writer_data",
+    "okv_writer_meta", "okv_writer_num_blocks", "okv_writer_block", "okv_writer_free",
+    "okv_meta_fetch", "okv_meta_parse", "okv_meta_num_blocks", "okv_meta_compression",
+    "okv_meta_descs", "okv_meta_first_key", "okv_meta_last_key", "okv_meta_block",
+    "okv_meta_free", "okv_synth_segment",
+]
+
+
+class BlockDesc(C.Structure):
+    _fields_ = [("offset", C.c_uint64), ("block_size", C.c_uint64),
+                ("original_size", C.c_uint64), ("compressed_size", C.c_uint64)]
+
+
+class DecodeOut(C.Structure):
+    _fields_ = [("row_start", C.c_void_p), ("key_base", C.c_void_p), ("val_base", C.c_void_p),
+                ("blk_status", C.c_void_p), ("key_off", C.c_void_p), ("key_len", C.c_void_p),
+                ("val_off", C.c_void_p), ("val_len", C.c_void_p), ("key_arena", C.c_void_p),
+                ("val_arena", C.c_void_p), ("row_cap", C.c_uint64), ("key_cap", C.c_uint64),
+                ("val_cap", C.c_uint64), ("n_rows", C.c_uint64), ("key_bytes", C.c_uint64),
+                ("val_bytes", C.c_uint64), ("n_bad_blocks", C.c_uint64)]
+
+
+_lib = None
+
+
+def build():
+    """Compile libokv_sst.so for gfx950 (hipcc) in-tree."""
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(_HERE, "csrc")], check=True)
+
+
+def lib():
+    """Load libokv_sst.so (raises if it is missing: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run objectkv_amd._lib.build() "
+                          "(or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    p, u64, i32, u32 = C.c_void_p, C.c_uint64, C.c_int, C.c_uint32
+    sig = {
+        "okv_open": (p, [i32]),
+        "okv_open_on_stream": (p, [i32, p]),
+        "okv_close": (None, [p]),
+        "okv_last_error": (C.c_char_p, [p]),
+        "okv_stream": (p, [p]),
+        "okv_sync": (i32, [p]),
+        "okv_abi_version": (i32, []),
+        "okv_decode_plan": (i32, [p, p, u64, p, u32, i32, u32, C.POINTER(u64), C.POINTER(u64),
+                                  C.POINTER(u64)]),
+        "okv_decode_blocks": (i32, [p, p, u64, p, u32, i32, C.POINTER(DecodeOut), u32]),
+        "okv_decode_totals": (i32, [p, C.POINTER(DecodeOut)]),
+        "okv_xxh64": (u64, [p, C.c_size_t, u64]),
+        "okv_hash_blocks": (i32, [p, p, u64, p, u32, p, u32]),
+        "okv_device_alloc": (p, [p, C.c_size_t]),
+        "okv_device_free": (None, [p, p]),
+        "okv_host_alloc": (p, [C.c_size_t]),
+        "okv_host_free": (None, [p]),
+        "okv_memcpy": (i32, [p, p, p, C.c_size_t, i32]),
+        "okv_profile": (i32, [p, i32]),
+        "okv_profile_read": (i32, [p, C.POINTER(C.c_double), C.POINTER(u64)]),
+        "okv_writer_new": (p, [u64, u64, i32, i32]),
+        "okv_writer_write_row": (i32, [p, p, C.c_size_t, p, C.c_size_t]),
+        "okv_writer_close": (i32, [p, i32, C.POINTER(u64), C.POINTER(u64)]),
+        "okv_writer_data": (p, [p, C.POINTER(u64)]),
+        "okv_writer_meta": (p, [p, C.POINTER(u64)]),
+        "okv_writer_num_blocks": (u64, [p]),
+        "okv_writer_block": (i32, [p, u64, C.POINTER(BlockDesc), C.POINTER(u64),
+                                   C.POINTER(p), C.POINTER(u64)]),
+        "okv_writer_free": (None, [p]),
+        "okv_meta_fetch": (i32, [p, u64, C.c_int64, C.POINTER(p)]),
+        "okv_meta_parse": (i32, [p, u64, C.POINTER(p)]),
+        "okv_meta_num_blocks": (u64, [p]),
+        "okv_meta_compression": (i32, [p]),
+        "okv_meta_descs": (p, [p]),
+        "okv_meta_first_key": (p, [p, C.POINTER(u64)]),
+        "okv_meta_last_key": (p, [p, C.POINTER(u64)]),
+        "okv_meta_block": (i32, [p, u64, C.POINTER(BlockDesc), C.POINTER(u64), C.POINTER(p),
+                                 C.POINTER(u64)]),
+        "okv_meta_free": (None, [p]),
+        "okv_synth_segment": (p, [i32, u64, u64, u64, u64, u64]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L

@@ -1,0 +1,981 @@
+// okv_decode.hip -- MI355X (gfx950) batched SST data-block decode.
+//
+// Replaces the record loop of sst.SegmentReader.ReadBlockWithStat
+// (/root/reference/sst/segment_reader.go:295-355) for many blocks at once.
+// Three launches per call (DESIGN.md "Kernels"):
+//   1. okv_count_kernel  -- one lane per block walks the record headers in
+//      HBM, validating exactly what the Go loop validates, and produces per
+//      block (status, rows, key bytes, value bytes, end position); each
+//      256-block tile is exclusive-scanned in the workgroup.
+//   2. okv_scan_kernel   -- one workgroup scans the tile totals.
+//   3. okv_copy_kernel   -- one workgroup per block stages the block's bytes
+//      into LDS with coalesced 16-byte loads, re-walks the headers in LDS to
+//      build a row table, writes the SoA row index, and scatters key/value
+//      bytes into packed 16-byte-aligned arenas with dwordx4 stores
+//      (Go's fresh-copy semantics, mustReadBytes :489-512).
+//   (okv_index_kernel replaces 3 for OKV_F_INDEX_ONLY: spans into seg.)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "okv_kernels.hpp"
+#include "okv_sst.h"
+
+namespace okv {
+
+// ---------------------------------------------------------------------------
+// Pass 1: header walk in HBM, one lane per block.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void okv_count_kernel(
+    const uint8_t* __restrict__ seg, uint64_t seg_bytes, const Desc* __restrict__ descs,
+    uint32_t nblk, int comp, BlockCount* __restrict__ cnt, Prefix* __restrict__ lp,
+    Prefix* __restrict__ tile_tot) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t b = blockIdx.x * kTile + tid;
+  uint64_t rows = 0, kb = 0, vb = 0, p = 0;
+  int32_t st = OKV_BLK_OK;
+  if (b < nblk) {
+    const Desc d = descs[b];
+    if (int64_t(d.offset) < 0 || d.offset >= seg_bytes) {
+      st = OKV_BLK_EOF;  // Seek error / bytes.Reader io.EOF (:303-313)
+    } else if (seg_bytes - d.offset < d.block_size) {
+      st = OKV_BLK_SHORT;  // ErrUnexpectedBytesRead (:314-316)
+    } else if (comp == OKV_COMP_ZSTD) {
+      st = OKV_BLK_UNSUPPORTED;  // :320-330 (device zstd: SURVEY §8f)
+    } else {
+      const uint64_t len = (comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
+      const uint64_t orig = d.original_size;
+      while (p < orig) {  // :340
+        if (len - p < 6) { st = OKV_BLK_PANIC; break; }  // u16/u32 reads (:342-345)
+        uint32_t kl, vl;
+        header_global(seg, d.offset + p, kl, vl);
+        const uint64_t room = len - p - 6;
+        if (kl > room || vl > room - kl) {  // zero-length reads always succeed (:490-493)
+          st = OKV_BLK_PANIC;                // key/value reads (:346-349)
+          break;
+        }
+        rows++;
+        kb += kl;
+        vb += vl;
+        p += 6 + uint64_t(kl) + uint64_t(vl);
+      }
+    }
+    if (st != OKV_BLK_OK) rows = kb = vb = 0;
+    BlockCount c;
+    c.rows = rows;
+    c.kbytes = kb;
+    c.vbytes = vb;
+    c.pend = p;
+    c.status = st;
+    c.pad = 0;
+    cnt[b] = c;
+  }
+  // workgroup exclusive scan of (rows, padded kb, padded vb, bad)
+  __shared__ uint64_t s_w[4][kThreads / 64];
+  const int lane = tid & 63, wave = tid >> 6;
+  uint64_t v[4] = {rows, round16(kb), round16(vb), uint64_t(b < nblk && st != OKV_BLK_OK)};
+  uint64_t inc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    inc[k] = wave_incl_scan(v[k], lane);
+    if (lane == 63) s_w[k][wave] = inc[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint64_t off = 0;
+    for (int w = 0; w < wave; ++w) off += s_w[k][w];
+    inc[k] += off - v[k];  // exclusive
+  }
+  if (b < nblk) {
+    Prefix e;
+    e.rows = inc[0];
+    e.kb = inc[1];
+    e.vb = inc[2];
+    e.bad = inc[3];
+    lp[b] = e;
+  }
+  if (tid == kThreads - 1) {
+    Prefix t;
+    t.rows = inc[0] + v[0];
+    t.kb = inc[1] + v[1];
+    t.vb = inc[2] + v[2];
+    t.bad = inc[3] + v[3];
+    tile_tot[blockIdx.x] = t;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 2: exclusive scan of the tile totals (single workgroup, carried loop).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void okv_scan_kernel(const Prefix* __restrict__ tile_tot,
+                                                        uint32_t ntiles,
+                                                        Prefix* __restrict__ tile_pre,
+                                                        Totals* __restrict__ tot,
+                                                        uint64_t* __restrict__ row_start,
+                                                        uint32_t nblk) {
+  __shared__ uint64_t s_w[4][16];
+  __shared__ uint64_t s_carry[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 4) s_carry[tid] = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < ntiles; base += 1024) {
+    const uint32_t i = base + tid;
+    Prefix t = {0, 0, 0, 0};
+    if (i < ntiles) t = tile_tot[i];
+    uint64_t v[4] = {t.rows, t.kb, t.vb, t.bad};
+    uint64_t inc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      inc[k] = wave_incl_scan(v[k], lane);
+      if (lane == 63) s_w[k][wave] = inc[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint64_t off = s_carry[k];
+      for (int w = 0; w < wave; ++w) off += s_w[k][w];
+      inc[k] += off - v[k];
+    }
+    if (i < ntiles) {
+      Prefix e;
+      e.rows = inc[0];
+      e.kb = inc[1];
+      e.vb = inc[2];
+      e.bad = inc[3];
+      tile_pre[i] = e;
+    }
+    __syncthreads();
+    if (tid == 1023) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s_carry[k] = inc[k] + v[k];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    Totals T;
+    T.rows = s_carry[0];
+    T.kb = s_carry[1];
+    T.vb = s_carry[2];
+    T.bad = s_carry[3];
+    *tot = T;
+    if (row_start) row_start[nblk] = T.rows;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 3: per-block materialisation.
+// ---------------------------------------------------------------------------
+struct CopyParams {
+  const uint8_t* seg;
+  uint64_t seg_bytes;
+  const Desc* descs;
+  uint32_t nblk;
+  int comp;
+  const BlockCount* cnt;
+  const Prefix* lp;
+  const Prefix* tile_pre;
+  uint64_t* row_start;
+  uint64_t* key_base;
+  uint64_t* val_base;
+  int32_t* blk_status;
+  uint64_t* key_off;
+  uint16_t* key_len;
+  uint64_t* val_off;
+  uint32_t* val_len;
+  uint8_t* key_arena;
+  uint8_t* val_arena;
+  uint64_t row_cap, key_cap, val_cap;
+};
+
+struct __align__(16) CopySmem {
+  uint4 stage[(kStage + kStagePad) / 16];  // [16 B guard][block image][guard]
+  uint64_t rec[kRowBatch];                 // record position within the block
+  uint64_t kpre[kRowBatch + 1];            // key-byte prefix within the block
+  uint64_t vpre[kRowBatch + 1];            // value-byte prefix within the block
+  uint32_t klen[kRowBatch];
+  uint32_t vlen[kRowBatch];
+};
+
+// Byte source: the LDS image of the block (byte index = 16 + shift + pos).
+struct LdsSrc {
+  const uint32_t* sw;
+  uint32_t bias;
+  __device__ __forceinline__ void header(uint64_t pos, uint32_t& kl, uint32_t& vl) const {
+    header_lds(sw, bias + uint32_t(pos), kl, vl);
+  }
+  __device__ __forceinline__ uint4 load16(int64_t pos) const {
+    return load16_lds(sw, uint32_t(int64_t(bias) + pos));
+  }
+};
+
+// Byte source: the block in HBM (blocks too large to stage).
+struct GlobalSrc {
+  const uint8_t* seg;
+  uint64_t seg_bytes;
+  uint64_t off;
+  __device__ __forceinline__ void header(uint64_t pos, uint32_t& kl, uint32_t& vl) const {
+    header_global(seg, off + pos, kl, vl);
+  }
+  __device__ __forceinline__ uint4 load16(int64_t pos) const {
+    return load16_global(seg, seg_bytes, int64_t(off) + pos);
+  }
+};
+
+// Lanes per row for a region whose rows average `avg` bytes.
+__device__ __forceinline__ uint32_t group_size(uint64_t avg) {
+  const uint64_t chunks = avg / 16 + 2;
+  uint32_t g = 1;
+  while (g < 64 && g < chunks) g <<= 1;
+  return g;
+}
+
+// Copy rows [0, nb) of one region (keys or values) into `arena`:
+//   row i bytes = src[spos_i, spos_i + len_i) -> arena[dbase + pre_i, ...).
+// Lane groups of G lanes own one row; each lane writes 16-byte aligned
+// destination chunks (dwordx4), masked head/tail chunks with narrow stores.
+template <class Src>
+__device__ __forceinline__ void copy_region(const Src& src, uint8_t* __restrict__ arena,
+                                            uint64_t dbase, const uint64_t* pre,
+                                            const uint64_t* rec, const uint32_t* klen,
+                                            const uint32_t* len, bool is_val, int nb,
+                                            uint32_t G) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t grp = tid / G, sub = tid % G, ngrp = kThreads / G;
+  for (uint32_t i = grp; i < uint32_t(nb); i += ngrp) {
+    const uint64_t L = len[i];
+    if (L == 0) continue;
+    const uint64_t d0 = dbase + pre[i];
+    const int64_t s0 = int64_t(rec[i] + 6 + (is_val ? klen[i] : 0));
+    const uint64_t c0 = d0 & ~uint64_t(15), c1 = (d0 + L + 15) & ~uint64_t(15);
+    for (uint64_t ca = c0 + 16ull * sub; ca < c1; ca += 16ull * G) {
+      const int64_t rel = int64_t(ca) - int64_t(d0);
+      const uint4 v = src.load16(s0 + rel);
+      const uint32_t lo = ca < d0 ? uint32_t(d0 - ca) : 0u;
+      const uint64_t end = d0 + L - ca;
+      const uint32_t hi = end < 16 ? uint32_t(end) : 16u;
+      if (lo == 0 && hi == 16) {
+        *reinterpret_cast<uint4*>(arena + ca) = v;
+      } else {
+        store_partial(arena + ca, v, lo, hi);
+      }
+    }
+  }
+}
+
+template <class Src>
+__device__ __forceinline__ void materialise(const Src& src, const CopyParams& P,
+                                           CopySmem& sm, uint64_t rows, uint64_t kbytes,
+                                           uint64_t vbytes, uint64_t row0, uint64_t kb0,
+                                           uint64_t vb0) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t Gk = group_size(kbytes / rows), Gv = group_size(vbytes / rows);
+  uint64_t p = 0, kacc = 0, vacc = 0;  // chase state (lane 0)
+  for (uint64_t r0 = 0; r0 < rows; r0 += kRowBatch) {
+    const int nb = int(rows - r0 < kRowBatch ? rows - r0 : kRowBatch);
+    if (tid == 0) {
+      // serial header chase: record i+1 starts at rec_i + 6 + klen_i + vlen_i
+      for (int i = 0; i < nb; ++i) {
+        uint32_t kl, vl;
+        src.header(p, kl, vl);
+        sm.rec[i] = p;
+        sm.klen[i] = kl;
+        sm.vlen[i] = vl;
+        sm.kpre[i] = kacc;
+        sm.vpre[i] = vacc;
+        kacc += kl;
+        vacc += vl;
+        p += 6 + uint64_t(kl) + uint64_t(vl);
+      }
+      sm.kpre[nb] = kacc;
+      sm.vpre[nb] = vacc;
+    }
+    __syncthreads();
+    // SoA row index (coalesced over rows)
+    for (int i = tid; i < nb; i += kThreads) {
+      const uint64_t g = row0 + r0 + i;
+      P.key_off[g] = kb0 + sm.kpre[i];
+      P.key_len[g] = uint16_t(sm.klen[i]);
+      P.val_off[g] = vb0 + sm.vpre[i];
+      P.val_len[g] = sm.vlen[i];
+    }
+    copy_region(src, P.key_arena, kb0, sm.kpre, sm.rec, sm.klen, sm.klen, false, nb, Gk);
+    copy_region(src, P.val_arena, vb0, sm.vpre, sm.rec, sm.klen, sm.vlen, true, nb, Gv);
+    __syncthreads();
+  }
+  // zero the 16-byte padding tail of each arena region
+  if (tid == 0) {
+    const uint64_t ke = kb0 + kbytes, ve = vb0 + vbytes;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    if (ke & 15) store_partial(P.key_arena + (ke & ~uint64_t(15)), z, uint32_t(ke & 15), 16);
+    if (ve & 15) store_partial(P.val_arena + (ve & ~uint64_t(15)), z, uint32_t(ve & 15), 16);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void okv_copy_kernel(CopyParams P) {
+  __shared__ CopySmem sm;
+  const uint32_t b = blockIdx.x;
+  const uint32_t tid = threadIdx.x;
+  const BlockCount c = P.cnt[b];
+  const Prefix l = P.lp[b];
+  const Prefix t = P.tile_pre[b / kTile];
+  const uint64_t row0 = t.rows + l.rows, kb0 = t.kb + l.kb, vb0 = t.vb + l.vb;
+  int32_t st = c.status;
+  if (st == OKV_BLK_OK && (row0 + c.rows > P.row_cap || kb0 + round16(c.kbytes) > P.key_cap ||
+                           vb0 + round16(c.vbytes) > P.val_cap))
+    st = OKV_BLK_CAPACITY;
+  if (tid == 0) {
+    P.row_start[b] = row0;
+    if (P.key_base) P.key_base[b] = kb0;
+    if (P.val_base) P.val_base[b] = vb0;
+    P.blk_status[b] = st;
+  }
+  if (st != OKV_BLK_OK || c.rows == 0) return;
+  const Desc d = P.descs[b];
+  if (c.pend <= uint64_t(kStage)) {
+    // stage [offset - shift, offset + pend) with aligned 16-byte loads
+    const uint32_t shift = uint32_t(d.offset & 15);
+    const uint32_t nch = uint32_t((shift + c.pend + 15) / 16);
+    const uint4* g = reinterpret_cast<const uint4*>(P.seg + (d.offset - shift));
+    constexpr int kPer = kStage / 16 / kThreads;  // 16 chunks per lane at 64 KiB
+    const uint32_t rounds = (nch + kThreads - 1) / kThreads;  // workgroup-uniform
+    uint4 v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      if (k < int(rounds)) {  // uniform branch; lanes past nch re-load the last chunk
+        const uint32_t ci = tid + k * kThreads;
+        v[k] = load_nt16(g + (ci < nch ? ci : nch - 1));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t ci = tid + k * kThreads;
+      if (k < int(rounds) && ci < nch) sm.stage[1 + ci] = v[k];
+    }
+    __syncthreads();
+    LdsSrc src{reinterpret_cast<const uint32_t*>(sm.stage), 16u + shift};
+    materialise(src, P, sm, c.rows, c.kbytes, c.vbytes, row0, kb0, vb0);
+  } else {
+    GlobalSrc src{P.seg, P.seg_bytes, d.offset};
+    materialise(src, P, sm, c.rows, c.kbytes, c.vbytes, row0, kb0, vb0);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 3 (OKV_F_INDEX_ONLY): spans into seg; one lane per block re-walks the
+// headers in HBM and writes its rows' SoA entries.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void okv_index_kernel(CopyParams P) {
+  const uint32_t b = blockIdx.x * kThreads + threadIdx.x;
+  if (b >= P.nblk) return;
+  const BlockCount c = P.cnt[b];
+  const Prefix l = P.lp[b];
+  const Prefix t = P.tile_pre[b / kTile];
+  const uint64_t row0 = t.rows + l.rows;
+  int32_t st = c.status;
+  if (st == OKV_BLK_OK && row0 + c.rows > P.row_cap) st = OKV_BLK_CAPACITY;
+  P.row_start[b] = row0;
+  P.blk_status[b] = st;
+  if (st != OKV_BLK_OK) return;
+  const uint64_t off = P.descs[b].offset;
+  uint64_t p = 0;
+  for (uint64_t r = 0; r < c.rows; ++r) {
+    uint32_t kl, vl;
+    header_global(P.seg, off + p, kl, vl);
+    const uint64_t g = row0 + r;
+    P.key_off[g] = off + p + 6;
+    P.key_len[g] = uint16_t(kl);
+    P.val_off[g] = off + p + 6 + kl;
+    P.val_len[g] = vl;
+    p += 6 + uint64_t(kl) + uint64_t(vl);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// XXH64 of each block's BlockSize bytes (BlockStat.Hash, segment_writer.go:185).
+// XXH64 has four independent accumulators, so four lanes share one block
+// (lane q owns stripe word q); the merge and tail run on lane q == 0.
+// ---------------------------------------------------------------------------
+__device__ constexpr uint64_t XP1 = 11400714785074694791ULL, XP2 = 14029467366897019727ULL,
+                              XP3 = 1609587929392839161ULL, XP4 = 9650029242287828579ULL,
+                              XP5 = 2870177450012600261ULL;
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
+  return (x << r) | (x >> (64 - r));
+}
+__device__ __forceinline__ uint64_t xround(uint64_t acc, uint64_t in) {
+  acc += in * XP2;
+  acc = rotl64(acc, 31);
+  return acc * XP1;
+}
+__device__ __forceinline__ uint64_t ld64u(const uint8_t* p) {  // unaligned LE load
+  uint64_t v = 0;
+#pragma unroll
+  for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+  return v;
+}
+
+__global__ __launch_bounds__(kThreads) void okv_hash_kernel(const uint8_t* __restrict__ seg,
+                                                            uint64_t seg_bytes,
+                                                            const Desc* __restrict__ descs,
+                                                            uint32_t nblk,
+                                                            uint64_t* __restrict__ out) {
+  const uint32_t gid = blockIdx.x * kThreads + threadIdx.x;
+  const uint32_t b = gid >> 2, q = gid & 3;
+  const bool live = b < nblk;
+  Desc d = {0, 0, 0, 0};
+  if (live) d = descs[b];
+  const bool ok = live && d.offset < seg_bytes && seg_bytes - d.offset >= d.block_size;
+  const uint8_t* p = seg + (ok ? d.offset : 0);
+  const uint64_t len = ok ? d.block_size : 0;
+  const uint64_t nstripe = len / 32;
+  const uint64_t seed = 0;
+  uint64_t acc = (q == 0) ? seed + XP1 + XP2 : (q == 1) ? seed + XP2 : (q == 2) ? seed : seed - XP1;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(p)) & 7) == 0;
+  for (uint64_t s = 0; s < nstripe; ++s) {
+    const uint8_t* w = p + s * 32 + q * 8;
+    const uint64_t x = aligned ? *reinterpret_cast<const uint64_t*>(w) : ld64u(w);
+    acc = xround(acc, x);
+  }
+  // gather the four accumulators onto lane q == 0 of the quad
+  const int lane = threadIdx.x & 63;
+  const uint64_t a1 = __shfl(acc, (lane & ~3) + 1, 64);
+  const uint64_t a2 = __shfl(acc, (lane & ~3) + 2, 64);
+  const uint64_t a3 = __shfl(acc, (lane & ~3) + 3, 64);
+  if (!live || q != 0) return;
+  if (!ok) {
+    out[b] = 0;
+    return;
+  }
+  uint64_t h;
+  if (len >= 32) {
+    const uint64_t v1 = acc, v2 = a1, v3 = a2, v4 = a3;
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h = (h ^ xround(0, v1)) * XP1 + XP4;
+    h = (h ^ xround(0, v2)) * XP1 + XP4;
+    h = (h ^ xround(0, v3)) * XP1 + XP4;
+    h = (h ^ xround(0, v4)) * XP1 + XP4;
+  } else {
+    h = seed + XP5;
+  }
+  h += len;
+  const uint8_t* t = p + nstripe * 32;
+  const uint8_t* end = p + len;
+  while (t + 8 <= end) {
+    h ^= xround(0, ld64u(t));
+    h = rotl64(h, 27) * XP1 + XP4;
+    t += 8;
+  }
+  if (t + 4 <= end) {
+    const uint32_t v = uint32_t(t[0]) | (uint32_t(t[1]) << 8) | (uint32_t(t[2]) << 16) |
+                       (uint32_t(t[3]) << 24);
+    h ^= uint64_t(v) * XP1;
+    h = rotl64(h, 23) * XP2 + XP3;
+    t += 4;
+  }
+  while (t < end) {
+    h ^= uint64_t(*t) * XP5;
+    h = rotl64(h, 11) * XP1;
+    ++t;
+  }
+  h ^= h >> 33;
+  h *= XP2;
+  h ^= h >> 29;
+  h *= XP3;
+  h ^= h >> 32;
+  out[b] = h;
+}
+
+}  // namespace okv
+
+// ===========================================================================
+// C-ABI (include/okv_sst.h)
+// ===========================================================================
+using namespace okv;
+
+struct okv_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+  // pass-1/2 scratch
+  BlockCount* d_cnt = nullptr;
+  Prefix* d_lp = nullptr;
+  Prefix* d_tile_tot = nullptr;
+  Prefix* d_tile_pre = nullptr;
+  size_t cap_blocks = 0;
+  Totals* d_tot = nullptr;
+  Totals* h_tot = nullptr;  // pinned
+  // host-mode staging buffers (device side)
+  uint8_t* d_seg = nullptr;
+  size_t cap_seg = 0;
+  Desc* d_desc = nullptr;
+  size_t cap_desc = 0;
+  void* d_out = nullptr;
+  size_t cap_out = 0;
+  uint64_t* d_hash = nullptr;
+  size_t cap_hash = 0;
+  // per-pass event timing (okv_profile)
+  bool prof = false;
+  std::vector<hipEvent_t> ev;  // 4 per timed call
+  size_t ev_used = 0;
+  double prof_ms[3] = {0, 0, 0};
+  uint64_t prof_calls = 0;
+};
+
+namespace {
+
+int set_err(okv_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
+  if (c) {
+    c->err = what;
+    if (e != hipSuccess) {
+      c->err += ": ";
+      c->err += hipGetErrorString(e);
+    }
+  }
+  return code;
+}
+
+#define OKV_HIP(call)                                             \
+  do {                                                            \
+    hipError_t e_ = (call);                                       \
+    if (e_ != hipSuccess) return set_err(ctx, OKV_E_HIP, #call, e_); \
+  } while (0)
+
+int grow(okv_ctx* ctx, void** p, size_t* cap, size_t need) {
+  if (need <= *cap && *p) return OKV_OK;
+  if (*p) {
+    OKV_HIP(hipStreamSynchronize(ctx->stream));
+    OKV_HIP(hipFree(*p));
+    *p = nullptr;
+  }
+  size_t c = std::max<size_t>(need, 4096);
+  c = (c + 4095) & ~size_t(4095);
+  OKV_HIP(hipMalloc(p, c));
+  *cap = c;
+  return OKV_OK;
+}
+
+int ensure_blocks(okv_ctx* ctx, uint32_t nblk) {
+  const size_t n = std::max<size_t>(nblk, 1);
+  if (n <= ctx->cap_blocks && ctx->d_cnt) return OKV_OK;
+  const size_t ntiles = (n + kTile - 1) / kTile;
+  if (ctx->d_cnt) {
+    OKV_HIP(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(ctx->d_cnt);
+    (void)hipFree(ctx->d_lp);
+    (void)hipFree(ctx->d_tile_tot);
+    (void)hipFree(ctx->d_tile_pre);
+  }
+  OKV_HIP(hipMalloc(&ctx->d_cnt, n * sizeof(BlockCount)));
+  OKV_HIP(hipMalloc(&ctx->d_lp, n * sizeof(Prefix)));
+  OKV_HIP(hipMalloc(&ctx->d_tile_tot, (ntiles + 1) * sizeof(Prefix)));
+  OKV_HIP(hipMalloc(&ctx->d_tile_pre, (ntiles + 1) * sizeof(Prefix)));
+  ctx->cap_blocks = n;
+  return OKV_OK;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// Event slot k (0..3) of the current timed call, or nullptr when not profiling.
+hipEvent_t prof_event(okv_ctx* ctx, int k) {
+  if (!ctx->prof) return nullptr;
+  const size_t need = ctx->ev_used + 4;
+  while (ctx->ev.size() < need) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    ctx->ev.push_back(e);
+  }
+  return ctx->ev[ctx->ev_used + k];
+}
+
+void prof_mark(okv_ctx* ctx, int k) {
+  hipEvent_t e = prof_event(ctx, k);
+  if (e) (void)hipEventRecord(e, ctx->stream);
+  if (e && k == 3) ctx->ev_used += 4;
+}
+
+// Launch passes 1 and 2 on device inputs.
+int launch_plan(okv_ctx* ctx, const uint8_t* d_seg, uint64_t seg_bytes, const Desc* d_desc,
+                uint32_t nblk, int comp, uint64_t* d_row_start, bool timed = false) {
+  int rc = ensure_blocks(ctx, nblk);
+  if (rc) return rc;
+  const uint32_t ntiles = (nblk + kTile - 1) / kTile;
+  if (timed) prof_mark(ctx, 0);
+  if (ntiles)
+    hipLaunchKernelGGL(okv_count_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, d_seg,
+                       seg_bytes, d_desc, nblk, comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot);
+  if (timed) prof_mark(ctx, 1);
+  hipLaunchKernelGGL(okv_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_tile_tot,
+                     ntiles, ctx->d_tile_pre, ctx->d_tot, d_row_start, nblk);
+  if (timed) prof_mark(ctx, 2);
+  OKV_HIP(hipGetLastError());
+  return OKV_OK;
+}
+
+int read_totals(okv_ctx* ctx, Totals* out) {
+  OKV_HIP(hipMemcpyAsync(ctx->h_tot, ctx->d_tot, sizeof(Totals), hipMemcpyDeviceToHost,
+                         ctx->stream));
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  *out = *ctx->h_tot;
+  return OKV_OK;
+}
+
+int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
+                  uint32_t nblk, int comp, okv_decode_out* o, uint32_t flags) {
+  const bool index_only = flags & OKV_F_INDEX_ONLY;
+  if (!o->row_start || !o->blk_status) return set_err(ctx, OKV_E_ARG, "row_start/blk_status");
+  if (!aligned16(seg)) return set_err(ctx, OKV_E_ARG, "device seg must be 16-byte aligned");
+  if (!index_only && (!aligned16(o->key_arena) || !aligned16(o->val_arena)))
+    return set_err(ctx, OKV_E_ARG, "device arenas must be 16-byte aligned");
+  int rc = launch_plan(ctx, seg, seg_bytes, descs, nblk, comp, o->row_start, true);
+  if (rc) return rc;
+  CopyParams P;
+  P.seg = seg;
+  P.seg_bytes = seg_bytes;
+  P.descs = descs;
+  P.nblk = nblk;
+  P.comp = comp;
+  P.cnt = ctx->d_cnt;
+  P.lp = ctx->d_lp;
+  P.tile_pre = ctx->d_tile_pre;
+  P.row_start = o->row_start;
+  P.key_base = o->key_base;
+  P.val_base = o->val_base;
+  P.blk_status = o->blk_status;
+  P.key_off = o->key_off;
+  P.key_len = o->key_len;
+  P.val_off = o->val_off;
+  P.val_len = o->val_len;
+  P.key_arena = o->key_arena;
+  P.val_arena = o->val_arena;
+  P.row_cap = o->row_cap;
+  P.key_cap = index_only ? 0 : o->key_cap;
+  P.val_cap = index_only ? 0 : o->val_cap;
+  if (nblk) {
+    if (index_only)
+      hipLaunchKernelGGL(okv_index_kernel, dim3((nblk + kThreads - 1) / kThreads),
+                         dim3(kThreads), 0, ctx->stream, P);
+    else
+      hipLaunchKernelGGL(okv_copy_kernel, dim3(nblk), dim3(kThreads), 0, ctx->stream, P);
+    OKV_HIP(hipGetLastError());
+  }
+  prof_mark(ctx, 3);
+  if (flags & OKV_F_ASYNC) return OKV_OK;
+  Totals T;
+  rc = read_totals(ctx, &T);
+  if (rc) return rc;
+  o->n_rows = T.rows;
+  o->key_bytes = index_only ? 0 : T.kb;
+  o->val_bytes = index_only ? 0 : T.vb;
+  o->n_bad_blocks = T.bad;
+  if (T.rows > o->row_cap || (!index_only && (T.kb > o->key_cap || T.vb > o->val_cap)))
+    return set_err(ctx, OKV_E_CAPACITY, "output capacity too small (totals set)");
+  return OKV_OK;
+}
+
+// Host pointers: stage inputs to device scratch, decode, copy results back.
+int decode_host(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv_block_desc* descs,
+                uint32_t nblk, int comp, okv_decode_out* o, uint32_t flags) {
+  const bool index_only = flags & OKV_F_INDEX_ONLY;
+  int rc = grow(ctx, reinterpret_cast<void**>(&ctx->d_seg), &ctx->cap_seg, seg_bytes + 64);
+  if (rc) return rc;
+  rc = grow(ctx, reinterpret_cast<void**>(&ctx->d_desc), &ctx->cap_desc,
+            size_t(nblk) * sizeof(Desc) + 64);
+  if (rc) return rc;
+  if (seg_bytes)
+    OKV_HIP(hipMemcpyAsync(ctx->d_seg, seg, seg_bytes, hipMemcpyHostToDevice, ctx->stream));
+  if (nblk)
+    OKV_HIP(hipMemcpyAsync(ctx->d_desc, descs, size_t(nblk) * sizeof(Desc),
+                           hipMemcpyHostToDevice, ctx->stream));
+  // size the device outputs from the plan
+  rc = ensure_blocks(ctx, nblk);
+  if (rc) return rc;
+  // device output layout inside one scratch allocation
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  // provisional: row_start needed by the plan launch
+  const size_t n1 = size_t(nblk) + 1;
+  size_t off_rs = 0, off_kb = al(off_rs + n1 * 8), off_vb = al(off_kb + n1 * 8),
+         off_st = al(off_vb + n1 * 8), off_rows = al(off_st + n1 * 4);
+  rc = grow(ctx, &ctx->d_out, &ctx->cap_out, off_rows + 256);
+  if (rc) return rc;
+  uint8_t* base = static_cast<uint8_t*>(ctx->d_out);
+  rc = launch_plan(ctx, ctx->d_seg, seg_bytes, ctx->d_desc, nblk, comp,
+                   reinterpret_cast<uint64_t*>(base + off_rs));
+  if (rc) return rc;
+  Totals T;
+  rc = read_totals(ctx, &T);
+  if (rc) return rc;
+  o->n_rows = T.rows;
+  o->key_bytes = index_only ? 0 : T.kb;
+  o->val_bytes = index_only ? 0 : T.vb;
+  o->n_bad_blocks = T.bad;
+  if (T.rows > o->row_cap || (!index_only && (T.kb > o->key_cap || T.vb > o->val_cap)))
+    return set_err(ctx, OKV_E_CAPACITY, "output capacity too small (totals set)");
+  const size_t R = T.rows;
+  size_t off_ko = al(off_rows), off_kl = al(off_ko + R * 8), off_vo = al(off_kl + R * 2),
+         off_vl = al(off_vo + R * 8), off_ka = al(off_vl + R * 4),
+         off_va = al(off_ka + (index_only ? 0 : T.kb)),
+         total = al(off_va + (index_only ? 0 : T.vb)) + 256;
+  if (total > ctx->cap_out) {
+    // grow (keeps nothing: plan results live in ctx scratch, row_start[nblk] is rewritten)
+    rc = grow(ctx, &ctx->d_out, &ctx->cap_out, total);
+    if (rc) return rc;
+    base = static_cast<uint8_t*>(ctx->d_out);
+  }
+  okv_decode_out d = *o;
+  d.row_start = reinterpret_cast<uint64_t*>(base + off_rs);
+  d.key_base = reinterpret_cast<uint64_t*>(base + off_kb);
+  d.val_base = reinterpret_cast<uint64_t*>(base + off_vb);
+  d.blk_status = reinterpret_cast<int32_t*>(base + off_st);
+  d.key_off = reinterpret_cast<uint64_t*>(base + off_ko);
+  d.key_len = reinterpret_cast<uint16_t*>(base + off_kl);
+  d.val_off = reinterpret_cast<uint64_t*>(base + off_vo);
+  d.val_len = reinterpret_cast<uint32_t*>(base + off_vl);
+  d.key_arena = index_only ? nullptr : base + off_ka;
+  d.val_arena = index_only ? nullptr : base + off_va;
+  d.row_cap = R;
+  d.key_cap = T.kb;
+  d.val_cap = T.vb;
+  rc = decode_device(ctx, ctx->d_seg, seg_bytes, ctx->d_desc, nblk, comp, &d,
+                     (flags & ~OKV_F_ASYNC) | OKV_F_DEVICE_PTRS);
+  if (rc) return rc;
+  auto d2h = [&](void* dst, const void* src, size_t n) -> int {
+    if (dst && n) OKV_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, ctx->stream));
+    return OKV_OK;
+  };
+  if ((rc = d2h(o->row_start, d.row_start, n1 * 8))) return rc;
+  if ((rc = d2h(o->blk_status, d.blk_status, size_t(nblk) * 4))) return rc;
+  if (!index_only) {
+    if ((rc = d2h(o->key_base, d.key_base, size_t(nblk) * 8))) return rc;
+    if ((rc = d2h(o->val_base, d.val_base, size_t(nblk) * 8))) return rc;
+    if ((rc = d2h(o->key_arena, d.key_arena, T.kb))) return rc;
+    if ((rc = d2h(o->val_arena, d.val_arena, T.vb))) return rc;
+  }
+  if ((rc = d2h(o->key_off, d.key_off, R * 8))) return rc;
+  if ((rc = d2h(o->key_len, d.key_len, R * 2))) return rc;
+  if ((rc = d2h(o->val_off, d.val_off, R * 8))) return rc;
+  if ((rc = d2h(o->val_len, d.val_len, R * 4))) return rc;
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  return OKV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int okv_abi_version(void) { return OKV_ABI_VERSION; }
+
+okv_ctx* okv_open_on_stream(int device, void* stream) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  okv_ctx* ctx = new okv_ctx();
+  ctx->device = device;
+  if (stream) {
+    ctx->stream = static_cast<hipStream_t>(stream);
+  } else {
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete ctx;
+      return nullptr;
+    }
+    ctx->own_stream = true;
+  }
+  if (hipMalloc(&ctx->d_tot, sizeof(Totals)) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&ctx->h_tot), sizeof(Totals), 0) != hipSuccess) {
+    okv_close(ctx);
+    return nullptr;
+  }
+  return ctx;
+}
+
+okv_ctx* okv_open(int device) { return okv_open_on_stream(device, nullptr); }
+
+void okv_close(okv_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  (void)hipFree(ctx->d_cnt);
+  (void)hipFree(ctx->d_lp);
+  (void)hipFree(ctx->d_tile_tot);
+  (void)hipFree(ctx->d_tile_pre);
+  (void)hipFree(ctx->d_tot);
+  if (ctx->h_tot) (void)hipHostFree(ctx->h_tot);
+  (void)hipFree(ctx->d_seg);
+  (void)hipFree(ctx->d_desc);
+  (void)hipFree(ctx->d_out);
+  (void)hipFree(ctx->d_hash);
+  if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* okv_last_error(const okv_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+void* okv_stream(const okv_ctx* ctx) { return ctx ? ctx->stream : nullptr; }
+
+int okv_sync(okv_ctx* ctx) {
+  if (!ctx) return OKV_E_ARG;
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  return OKV_OK;
+}
+
+int okv_decode_plan(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes,
+                    const okv_block_desc* descs, uint32_t nblk, int compression, uint32_t flags,
+                    uint64_t* n_rows, uint64_t* key_bytes, uint64_t* val_bytes) {
+  if (!ctx || (!seg && seg_bytes) || (!descs && nblk)) return set_err(ctx, OKV_E_ARG, "args");
+  OKV_HIP(hipSetDevice(ctx->device));
+  const uint8_t* d_seg = seg;
+  const Desc* d_desc = reinterpret_cast<const Desc*>(descs);
+  int rc;
+  if (!(flags & OKV_F_DEVICE_PTRS)) {
+    if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->d_seg), &ctx->cap_seg, seg_bytes + 64)))
+      return rc;
+    if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->d_desc), &ctx->cap_desc,
+                   size_t(nblk) * sizeof(Desc) + 64)))
+      return rc;
+    if (seg_bytes)
+      OKV_HIP(hipMemcpyAsync(ctx->d_seg, seg, seg_bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (nblk)
+      OKV_HIP(hipMemcpyAsync(ctx->d_desc, descs, size_t(nblk) * sizeof(Desc),
+                             hipMemcpyHostToDevice, ctx->stream));
+    d_seg = ctx->d_seg;
+    d_desc = ctx->d_desc;
+  } else if (!aligned16(seg)) {
+    return set_err(ctx, OKV_E_ARG, "device seg must be 16-byte aligned");
+  }
+  if ((rc = launch_plan(ctx, d_seg, seg_bytes, d_desc, nblk, compression, nullptr))) return rc;
+  Totals T;
+  if ((rc = read_totals(ctx, &T))) return rc;
+  if (n_rows) *n_rows = T.rows;
+  if (key_bytes) *key_bytes = (flags & OKV_F_INDEX_ONLY) ? 0 : T.kb;
+  if (val_bytes) *val_bytes = (flags & OKV_F_INDEX_ONLY) ? 0 : T.vb;
+  return OKV_OK;
+}
+
+int okv_decode_blocks(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes,
+                      const okv_block_desc* descs, uint32_t nblk, int compression,
+                      okv_decode_out* out, uint32_t flags) {
+  if (!ctx || !out || (!seg && seg_bytes) || (!descs && nblk))
+    return set_err(ctx, OKV_E_ARG, "null argument");
+  if (compression < 0 || compression > 2) return set_err(ctx, OKV_E_ARG, "compression");
+  OKV_HIP(hipSetDevice(ctx->device));
+  if (flags & OKV_F_DEVICE_PTRS)
+    return decode_device(ctx, seg, seg_bytes, reinterpret_cast<const Desc*>(descs), nblk,
+                         compression, out, flags);
+  return decode_host(ctx, seg, seg_bytes, descs, nblk, compression, out, flags);
+}
+
+int okv_decode_totals(okv_ctx* ctx, okv_decode_out* out) {
+  if (!ctx || !out) return OKV_E_ARG;
+  Totals T;
+  int rc = read_totals(ctx, &T);
+  if (rc) return rc;
+  out->n_rows = T.rows;
+  out->key_bytes = T.kb;
+  out->val_bytes = T.vb;
+  out->n_bad_blocks = T.bad;
+  if (T.rows > out->row_cap || T.kb > out->key_cap || T.vb > out->val_cap)
+    return OKV_E_CAPACITY;
+  return OKV_OK;
+}
+
+int okv_hash_blocks(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes,
+                    const okv_block_desc* descs, uint32_t nblk, uint64_t* hashes,
+                    uint32_t flags) {
+  if (!ctx || !hashes || (!seg && seg_bytes) || (!descs && nblk)) return OKV_E_ARG;
+  OKV_HIP(hipSetDevice(ctx->device));
+  const uint8_t* d_seg = seg;
+  const Desc* d_desc = reinterpret_cast<const Desc*>(descs);
+  uint64_t* d_h = hashes;
+  int rc;
+  if (!(flags & OKV_F_DEVICE_PTRS)) {
+    if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->d_seg), &ctx->cap_seg, seg_bytes + 64)))
+      return rc;
+    if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->d_desc), &ctx->cap_desc,
+                   size_t(nblk) * sizeof(Desc) + 64)))
+      return rc;
+    if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->d_hash), &ctx->cap_hash,
+                   size_t(nblk) * 8 + 64)))
+      return rc;
+    if (seg_bytes)
+      OKV_HIP(hipMemcpyAsync(ctx->d_seg, seg, seg_bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (nblk)
+      OKV_HIP(hipMemcpyAsync(ctx->d_desc, descs, size_t(nblk) * sizeof(Desc),
+                             hipMemcpyHostToDevice, ctx->stream));
+    d_seg = ctx->d_seg;
+    d_desc = ctx->d_desc;
+    d_h = ctx->d_hash;
+  }
+  if (nblk) {
+    const uint64_t threads = uint64_t(nblk) * 4;
+    hipLaunchKernelGGL(okv_hash_kernel, dim3(uint32_t((threads + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, ctx->stream, d_seg, seg_bytes, d_desc, nblk, d_h);
+    OKV_HIP(hipGetLastError());
+  }
+  if (!(flags & OKV_F_DEVICE_PTRS)) {
+    if (nblk)
+      OKV_HIP(hipMemcpyAsync(hashes, d_h, size_t(nblk) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  if (!(flags & OKV_F_ASYNC)) OKV_HIP(hipStreamSynchronize(ctx->stream));
+  return OKV_OK;
+}
+
+int okv_profile(okv_ctx* ctx, int enable) {
+  if (!ctx) return OKV_E_ARG;
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  ctx->prof = enable != 0;
+  ctx->ev_used = 0;
+  ctx->prof_ms[0] = ctx->prof_ms[1] = ctx->prof_ms[2] = 0;
+  ctx->prof_calls = 0;
+  return OKV_OK;
+}
+
+int okv_profile_read(okv_ctx* ctx, double* ms, uint64_t* calls) {
+  if (!ctx) return OKV_E_ARG;
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  for (size_t i = 0; i + 4 <= ctx->ev_used; i += 4) {
+    for (int k = 0; k < 3; ++k) {
+      float t = 0.f;
+      OKV_HIP(hipEventElapsedTime(&t, ctx->ev[i + k], ctx->ev[i + k + 1]));
+      ctx->prof_ms[k] += t;
+    }
+    ctx->prof_calls++;
+  }
+  ctx->ev_used = 0;
+  if (ms)
+    for (int k = 0; k < 3; ++k) ms[k] = ctx->prof_ms[k];
+  if (calls) *calls = ctx->prof_calls;
+  return OKV_OK;
+}
+
+void* okv_device_alloc(okv_ctx* ctx, size_t bytes) {
+  void* p = nullptr;
+  if (ctx) hipSetDevice(ctx->device);
+  if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) return nullptr;
+  return p;
+}
+void okv_device_free(okv_ctx* ctx, void* p) {
+  if (ctx) hipSetDevice(ctx->device);
+  if (p) (void)hipFree(p);
+}
+void* okv_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, 0) != hipSuccess) return nullptr;
+  return p;
+}
+void okv_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+int okv_memcpy(okv_ctx* ctx, void* dst, const void* src, size_t bytes, int kind) {
+  if (!ctx) return OKV_E_ARG;
+  hipMemcpyKind k = kind == 0   ? hipMemcpyHostToDevice
+                    : kind == 1 ? hipMemcpyDeviceToHost
+                                : hipMemcpyDeviceToDevice;
+  OKV_HIP(hipMemcpyAsync(dst, src, bytes, k, ctx->stream));
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  return OKV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+// okv_kernels.hpp -- device-side building blocks for the SST block decode
+// (gfx950 / CDNA4, wave64).  Byte and index work only: no MFMA.
+//
+// Record format restated from the reference writer/reader:
+//   [u16 LE klen][u32 LE vlen][key][value]      segment_writer.go:121-125
+// decode loop `for consumed < OriginalSize`     segment_reader.go:338-352
+// each read must be satisfied in full or Go panics (mustReadBytes :506-512);
+// zero-length reads read nothing and yield nil (readBytes :490-493).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace okv {
+
+constexpr int kThreads = 256;      // 4 waves per workgroup
+constexpr int kTile = 256;         // blocks per pass-1 workgroup (one lane each)
+constexpr int kRowBatch = 256;     // rows materialised per LDS row-table batch
+constexpr int kStage = 65536;      // LDS staging capacity for one block (bytes)
+constexpr int kStagePad = 64;      // guard bytes around the staged image
+
+struct BlockCount {   // pass-1 result per block
+  uint64_t rows;      // records decoded
+  uint64_t kbytes;    // sum of key lengths
+  uint64_t vbytes;    // sum of value lengths
+  uint64_t pend;      // final walk position (>= OriginalSize; <= buffer length)
+  int32_t status;     // OKV_BLK_*
+  int32_t pad;
+};
+
+struct Prefix {       // exclusive prefixes (rows, padded key bytes, padded value bytes)
+  uint64_t rows, kb, vb, bad;
+};
+
+struct Totals {
+  uint64_t rows, kb, vb, bad;
+};
+
+struct Desc {         // == okv_block_desc
+  uint64_t offset, block_size, original_size, compressed_size;
+};
+
+__device__ __forceinline__ uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+
+// Bytes [pos, pos+4) from two consecutive aligned dwords.
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+// Read the 6-byte record header at absolute segment position pos (the caller
+// has checked pos + 6 <= buffer end <= seg_bytes).  Only dwords containing a
+// needed byte are loaded, so no load leaves the segment's last dword.
+__device__ __forceinline__ void header_global(const uint8_t* __restrict__ seg, uint64_t pos,
+                                              uint32_t& klen, uint32_t& vlen) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(seg + (pos & ~uint64_t(3)));
+  const uint32_t sh = uint32_t(pos & 3);
+  const uint32_t w0 = w[0];
+  const uint32_t w1 = w[1];
+  const uint32_t w2 = (sh == 3) ? w[2] : 0u;
+  const uint32_t a = funnel(w1, w0, sh);  // bytes pos..pos+3
+  const uint32_t b = funnel(w2, w1, sh);  // bytes pos+4..pos+7
+  klen = a & 0xffffu;
+  vlen = (a >> 16) | (b << 16);
+}
+
+// Same, from an LDS byte image (word-addressed, byte index bi).
+__device__ __forceinline__ void header_lds(const uint32_t* sw, uint32_t bi, uint32_t& klen,
+                                           uint32_t& vlen) {
+  const uint32_t* w = sw + (bi >> 2);
+  const uint32_t sh = bi & 3;
+  const uint32_t a = funnel(w[1], w[0], sh);
+  const uint32_t b = funnel(w[2], w[1], sh);
+  klen = a & 0xffffu;
+  vlen = (a >> 16) | (b << 16);
+}
+
+// 16 bytes starting at LDS byte index bi (any alignment): 5 dword reads + funnels.
+__device__ __forceinline__ uint4 load16_lds(const uint32_t* sw, uint32_t bi) {
+  const uint32_t* w = sw + (bi >> 2);
+  const uint32_t sh = bi & 3;
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+  return make_uint4(funnel(w1, w0, sh), funnel(w2, w1, sh), funnel(w3, w2, sh),
+                    funnel(w4, w3, sh));
+}
+
+// 16 bytes starting at absolute segment position pos (may be < 0 or run past
+// the end for masked head/tail chunks): dwords wholly outside [0, seg_bytes)
+// are not loaded.
+__device__ __forceinline__ uint4 load16_global(const uint8_t* __restrict__ seg, uint64_t seg_bytes,
+                                               int64_t pos) {
+  const int64_t a = pos & ~int64_t(3);
+  const uint32_t sh = uint32_t(pos & 3);
+  uint32_t w[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int64_t at = a + 4 * i;
+    w[i] = (at >= 0 && uint64_t(at) < seg_bytes)
+               ? *reinterpret_cast<const uint32_t*>(seg + at)
+               : 0u;
+  }
+  return make_uint4(funnel(w[1], w[0], sh), funnel(w[2], w[1], sh), funnel(w[3], w[2], sh),
+                    funnel(w[4], w[3], sh));
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte streaming load (nontemporal: the block is read once).
+__device__ __forceinline__ uint4 load_nt16(const uint4* p) {
+  const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(t.x, t.y, t.z, t.w);
+}
+
+// Dword of v starting at byte o (0..15) without runtime-indexed arrays.
+__device__ __forceinline__ uint32_t dword_at(const uint4& v, uint32_t o) {
+  const uint32_t wi = o >> 2, sh = o & 3;
+  const uint32_t a = wi == 0 ? v.x : wi == 1 ? v.y : wi == 2 ? v.z : v.w;
+  const uint32_t b = wi == 0 ? v.y : wi == 1 ? v.z : wi == 2 ? v.w : 0u;
+  return funnel(b, a, sh);
+}
+
+// Store bytes [lo, hi) of the 16-byte vector v to the 16-byte aligned dst,
+// using the widest naturally aligned stores (no read-modify-write: bytes
+// outside [lo, hi) belong to a neighbouring row and are not touched).
+__device__ __forceinline__ void store_partial(uint8_t* dst, const uint4& v, uint32_t lo,
+                                              uint32_t hi) {
+  uint32_t o = lo;
+  while (o < hi) {
+    if ((o & 7) == 0 && o + 8 <= hi) {
+      const uint64_t q = uint64_t(dword_at(v, o)) | (uint64_t(dword_at(v, o + 4)) << 32);
+      *reinterpret_cast<uint64_t*>(dst + o) = q;
+      o += 8;
+    } else if ((o & 3) == 0 && o + 4 <= hi) {
+      *reinterpret_cast<uint32_t*>(dst + o) = dword_at(v, o);
+      o += 4;
+    } else if ((o & 1) == 0 && o + 2 <= hi) {
+      *reinterpret_cast<uint16_t*>(dst + o) = uint16_t(dword_at(v, o));
+      o += 2;
+    } else {
+      dst[o] = uint8_t(dword_at(v, o));
+      o += 1;
+    }
+  }
+}
+
+// Wave64 inclusive scan of a 64-bit value (DPP-free shuffle form).
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+}  // namespace okv

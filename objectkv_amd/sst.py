@@ -1,0 +1,334 @@
+"""Python host side of the MI355X SST decode path.
+
+Mirrors the Go ``sst`` API surface the hot path sits under
+(/root/reference/sst): ``SegmentWriter`` (segment_writer.go:35-328),
+metadata loading (segment_reader.go:91-238) and the batched
+``ReadBlockWithStat`` (segment_reader.go:295-355) executed by the HIP kernels
+in libokv_sst.so.  ``objectkv_amd.reader`` builds ``SegmentReader`` /
+``RowIter`` on top of this.
+
+Descriptor arrays are numpy ``uint64`` arrays of shape (nblk, 4):
+``(Offset, BlockSize, OriginalSize, CompressedSize)`` == ``okv_block_desc``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import (BLK_OK, COMP_LZ4, COMP_NONE, COMP_ZSTD, F_ASYNC, F_DEVICE_PTRS,  # noqa: F401
+                   F_INDEX_ONLY, OKV_E_CAPACITY, OKV_OK, SYNTH_FIXED, SYNTH_ZIPF, BlockDesc,
+                   DecodeOut, lib)
+
+
+class OkvError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__(f"okv error {code}: {msg}")
+        self.code = code
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data if a.size else None
+    return a.data_ptr()  # torch tensor
+
+
+def _bytes_array(b) -> np.ndarray:
+    if isinstance(b, np.ndarray):
+        return b
+    return np.frombuffer(bytes(b), np.uint8)
+
+
+def xxh64(data, seed: int = 0) -> int:
+    a = _bytes_array(data)
+    return lib().okv_xxh64(_ptr(a), a.size, seed)
+
+
+# ---- SegmentWriter -------------------------------------------------------------
+
+
+class SegmentWriter:
+    """Host C++ SegmentWriter (okv_writer_*); raises OkvError with the Go
+    sentinel codes of include/okv_host.h."""
+
+    def __init__(self, threshold=3584, block_size=4096, zstd_level=0, lz4=False, _handle=None):
+        L = lib()
+        self._h = _handle or L.okv_writer_new(threshold, block_size, zstd_level, int(lz4))
+        if not self._h:
+            raise OkvError(-1, "okv_writer_new")
+
+    def WriteRow(self, key: bytes, val: bytes):
+        rc = lib().okv_writer_write_row(self._h, key, len(key), val, len(val))
+        if rc:
+            raise OkvError(rc, "WriteRow")
+
+    def Close(self, strict_go=True):
+        fl, ml = C.c_uint64(), C.c_uint64()
+        rc = lib().okv_writer_close(self._h, int(strict_go), C.byref(fl), C.byref(ml))
+        if rc:
+            raise OkvError(rc, "Close")
+        return fl.value, self.meta()
+
+    def data_view(self) -> np.ndarray:
+        """Zero-copy view of the segment bytes (valid while the writer lives)."""
+        n = C.c_uint64()
+        p = lib().okv_writer_data(self._h, C.byref(n))
+        if not n.value:
+            return np.zeros(0, np.uint8)
+        return np.ctypeslib.as_array((C.c_uint8 * n.value).from_address(p))
+
+    def data(self) -> np.ndarray:
+        n = C.c_uint64()
+        p = lib().okv_writer_data(self._h, C.byref(n))
+        if not n.value:
+            return np.zeros(0, np.uint8)
+        return np.ctypeslib.as_array((C.c_uint8 * n.value).from_address(p)).copy()
+
+    def meta(self) -> bytes:
+        n = C.c_uint64()
+        p = lib().okv_writer_meta(self._h, C.byref(n))
+        return C.string_at(p, n.value) if n.value else b""
+
+    def num_blocks(self) -> int:
+        return lib().okv_writer_num_blocks(self._h)
+
+    def blocks(self):
+        """[(first_key, (offset, block_size, original_size, compressed_size), hash)]"""
+        out = []
+        d, h, fk, fl = BlockDesc(), C.c_uint64(), C.c_void_p(), C.c_uint64()
+        for i in range(self.num_blocks()):
+            lib().okv_writer_block(self._h, i, C.byref(d), C.byref(h), C.byref(fk), C.byref(fl))
+            key = C.string_at(fk, fl.value) if fl.value else b""
+            out.append((key, (d.offset, d.block_size, d.original_size, d.compressed_size),
+                        h.value))
+        return out
+
+    def descs(self) -> np.ndarray:
+        return np.array([b[1] for b in self.blocks()], np.uint64).reshape(-1, 4)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().okv_writer_free(h)
+            self._h = None
+
+
+def synth_segment(kind: int, seed: int, nrows: int = 0, nblocks: int = 0,
+                  threshold: int = 3584, block_size: int = 4096) -> SegmentWriter:
+    """Deterministic synthetic segment, closed."""
+    h = lib().okv_synth_segment(kind, seed, nrows, nblocks, threshold, block_size)
+    if not h:
+        raise OkvError(-1, "okv_synth_segment")
+    return SegmentWriter(_handle=h)
+
+
+# ---- metadata ------------------------------------------------------------------
+
+
+@dataclass
+class Metadata:
+    """SegmentMetadata (segment_reader.go:43-55) plus the index in file order."""
+
+    first_key: bytes
+    last_key: bytes
+    compression: int
+    first_keys: list  # per index entry, file order
+    descs: np.ndarray  # (n, 4) uint64, file order
+    hashes: np.ndarray  # (n,) uint64
+
+
+def _meta_from_handle(h) -> Metadata:
+    L = lib()
+    try:
+        n = L.okv_meta_num_blocks(h)
+        ln = C.c_uint64()
+        p = L.okv_meta_first_key(h, C.byref(ln))
+        fk = C.string_at(p, ln.value) if ln.value else b""
+        p = L.okv_meta_last_key(h, C.byref(ln))
+        lk = C.string_at(p, ln.value) if ln.value else b""
+        descs = np.zeros((n, 4), np.uint64)
+        hashes = np.zeros(n, np.uint64)
+        keys = []
+        d, hh, kp, kl = BlockDesc(), C.c_uint64(), C.c_void_p(), C.c_uint64()
+        for i in range(n):
+            L.okv_meta_block(h, i, C.byref(d), C.byref(hh), C.byref(kp), C.byref(kl))
+            descs[i] = (d.offset, d.block_size, d.original_size, d.compressed_size)
+            hashes[i] = hh.value
+            keys.append(C.string_at(kp, kl.value) if kl.value else b"")
+        return Metadata(fk, lk, L.okv_meta_compression(h), keys, descs, hashes)
+    finally:
+        L.okv_meta_free(h)
+
+
+def bytes_to_metadata(meta: bytes) -> Metadata:
+    """BytesToMetadata (segment_reader.go:147-181)."""
+    h = C.c_void_p()
+    buf = C.create_string_buffer(bytes(meta), len(meta))
+    rc = lib().okv_meta_parse(buf, len(meta), C.byref(h))
+    if rc:
+        raise OkvError(rc, "BytesToMetadata")
+    return _meta_from_handle(h)
+
+
+def fetch_metadata(data, file_bytes: int) -> Metadata:
+    """FetchAndLoadMetadata (segment_reader.go:91-141)."""
+    a = _bytes_array(data)
+    h = C.c_void_p()
+    rc = lib().okv_meta_fetch(_ptr(a), a.size, file_bytes, C.byref(h))
+    if rc:
+        raise OkvError(rc, "FetchAndLoadMetadata")
+    return _meta_from_handle(h)
+
+
+# ---- batched decode ------------------------------------------------------------
+
+
+@dataclass
+class Decoded:
+    """Host copy of an okv_decode_out (see include/okv_sst.h)."""
+
+    status: np.ndarray
+    row_start: np.ndarray
+    key_base: np.ndarray | None
+    val_base: np.ndarray | None
+    key_off: np.ndarray
+    key_len: np.ndarray
+    val_off: np.ndarray
+    val_len: np.ndarray
+    key_arena: np.ndarray | None
+    val_arena: np.ndarray | None
+    index_only: bool
+    seg: np.ndarray | None = None
+
+    def block_rows(self, b):
+        """Rows of block b as [(key|None, value|None)] (None = Go nil, Q4)."""
+        src_k = self.seg if self.index_only else self.key_arena
+        src_v = self.seg if self.index_only else self.val_arena
+        out = []
+        for g in range(int(self.row_start[b]), int(self.row_start[b + 1])):
+            kl, vl = int(self.key_len[g]), int(self.val_len[g])
+            ko, vo = int(self.key_off[g]), int(self.val_off[g])
+            out.append((src_k[ko:ko + kl].tobytes() if kl else None,
+                        src_v[vo:vo + vl].tobytes() if vl else None))
+        return out
+
+
+class Decoder:
+    """One okv_ctx bound to a GPU (HIP device ordinal)."""
+
+    def __init__(self, device: int = 0, stream=None):
+        L = lib()
+        self._ctx = (L.okv_open_on_stream(device, stream) if stream is not None
+                     else L.okv_open(device))
+        if not self._ctx:
+            raise OkvError(_lib.OKV_E_NODEV, f"okv_open({device}) failed (no GPU?)")
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            lib().okv_close(self._ctx)
+            self._ctx = None
+
+    __del__ = close
+
+    def error(self) -> str:
+        return (lib().okv_last_error(self._ctx) or b"").decode()
+
+    def _check(self, rc, what):
+        if rc:
+            raise OkvError(rc, f"{what}: {self.error()}")
+
+    @property
+    def stream(self):
+        return lib().okv_stream(self._ctx)
+
+    def sync(self):
+        self._check(lib().okv_sync(self._ctx), "okv_sync")
+
+    def profile(self, enable=True):
+        """Per-pass HIP-event timing on the context stream (okv_profile)."""
+        self._check(lib().okv_profile(self._ctx, int(enable)), "okv_profile")
+
+    def profile_read(self):
+        """-> ({'count': ms, 'scan': ms, 'copy': ms} summed, number of calls)"""
+        ms = (C.c_double * 3)()
+        n = C.c_uint64()
+        self._check(lib().okv_profile_read(self._ctx, ms, C.byref(n)), "okv_profile_read")
+        return {"count": ms[0], "scan": ms[1], "copy": ms[2]}, n.value
+
+    # -- host-pointer API ------------------------------------------------------
+    def plan(self, seg, descs: np.ndarray, compression=COMP_NONE, index_only=False):
+        s = _bytes_array(seg)
+        d = np.ascontiguousarray(descs, np.uint64).reshape(-1, 4)
+        r, k, v = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        flags = F_INDEX_ONLY if index_only else 0
+        self._check(lib().okv_decode_plan(self._ctx, _ptr(s), s.size, _ptr(d), d.shape[0],
+                                          compression, flags, C.byref(r), C.byref(k),
+                                          C.byref(v)), "okv_decode_plan")
+        return r.value, k.value, v.value
+
+    def decode(self, seg, descs: np.ndarray, compression=COMP_NONE,
+               index_only=False) -> Decoded:
+        """Batched ReadBlockWithStat over host buffers (H2D, kernels, D2H)."""
+        s = _bytes_array(seg)
+        d = np.ascontiguousarray(descs, np.uint64).reshape(-1, 4)
+        n = d.shape[0]
+        rows, kb, vb = self.plan(s, d, compression, index_only)
+        o = dict(status=np.zeros(n, np.int32), row_start=np.zeros(n + 1, np.uint64),
+                 key_base=None if index_only else np.zeros(n, np.uint64),
+                 val_base=None if index_only else np.zeros(n, np.uint64),
+                 key_off=np.zeros(rows, np.uint64), key_len=np.zeros(rows, np.uint16),
+                 val_off=np.zeros(rows, np.uint64), val_len=np.zeros(rows, np.uint32),
+                 key_arena=None if index_only else np.zeros(kb, np.uint8),
+                 val_arena=None if index_only else np.zeros(vb, np.uint8))
+        out = DecodeOut(_ptr(o["row_start"]), _ptr(o["key_base"]), _ptr(o["val_base"]),
+                        _ptr(o["status"]), _ptr(o["key_off"]), _ptr(o["key_len"]),
+                        _ptr(o["val_off"]), _ptr(o["val_len"]), _ptr(o["key_arena"]),
+                        _ptr(o["val_arena"]), rows, kb, vb, 0, 0, 0, 0)
+        flags = F_INDEX_ONLY if index_only else 0
+        self._check(lib().okv_decode_blocks(self._ctx, _ptr(s), s.size, _ptr(d), n, compression,
+                                            C.byref(out), flags), "okv_decode_blocks")
+        return Decoded(index_only=index_only, seg=s if index_only else None, **o)
+
+    def hash_blocks(self, seg, descs: np.ndarray) -> np.ndarray:
+        s = _bytes_array(seg)
+        d = np.ascontiguousarray(descs, np.uint64).reshape(-1, 4)
+        h = np.zeros(d.shape[0], np.uint64)
+        self._check(lib().okv_hash_blocks(self._ctx, _ptr(s), s.size, _ptr(d), d.shape[0],
+                                          _ptr(h), 0), "okv_hash_blocks")
+        return h
+
+    # -- device-pointer API (torch tensors on this device) ---------------------
+    def decode_device(self, seg_t, seg_bytes, descs_t, nblk, out: dict, compression=COMP_NONE,
+                      index_only=False, sync=True) -> DecodeOut:
+        """Device-resident decode into caller-allocated torch tensors.
+
+        ``out`` keys: row_start, key_base, val_base, status, key_off, key_len,
+        val_off, val_len, key_arena, val_arena (arenas/bases unused when
+        index_only).  With sync=False the call only enqueues (OKV_F_ASYNC).
+        """
+        g = out.get
+        o = DecodeOut(_ptr(g("row_start")), _ptr(g("key_base")), _ptr(g("val_base")),
+                      _ptr(g("status")), _ptr(g("key_off")), _ptr(g("key_len")),
+                      _ptr(g("val_off")), _ptr(g("val_len")), _ptr(g("key_arena")),
+                      _ptr(g("val_arena")), g("key_off").numel(),
+                      0 if index_only else g("key_arena").numel(),
+                      0 if index_only else g("val_arena").numel(), 0, 0, 0, 0)
+        flags = F_DEVICE_PTRS | (F_INDEX_ONLY if index_only else 0) | (0 if sync else F_ASYNC)
+        rc = lib().okv_decode_blocks(self._ctx, _ptr(seg_t), seg_bytes, _ptr(descs_t), nblk,
+                                     compression, C.byref(o), flags)
+        self._check(rc, "okv_decode_blocks(device)")
+        return o
+
+    def plan_device(self, seg_t, seg_bytes, descs_t, nblk, compression=COMP_NONE,
+                    index_only=False):
+        r, k, v = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        flags = F_DEVICE_PTRS | (F_INDEX_ONLY if index_only else 0)
+        self._check(lib().okv_decode_plan(self._ctx, _ptr(seg_t), seg_bytes, _ptr(descs_t), nblk,
+                                          compression, flags, C.byref(r), C.byref(k),
+                                          C.byref(v)), "okv_decode_plan(device)")
+        return r.value, k.value, v.value

@@ -1,0 +1,223 @@
+"""GPU parity: the HIP decode (libokv_sst.so through the C-ABI) against the
+CPU oracle (oracle/) and the committed golden vectors.  Integer/byte work:
+every comparison is bit-exact."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+import objectkv_amd as okv
+from objectkv_amd import _lib
+from oracle import coracle as CO
+from tests.conftest import descs_of, rowval, unpack
+
+pytestmark = pytest.mark.gpu
+
+SOA = ("row_start", "key_off", "key_len", "val_off", "val_len")
+
+
+def _assert_same_as_oracle(got: okv.Decoded, seg, descs, comp, index_only):
+    ref = CO.decode_soa(seg, CO.descs_array([tuple(int(x) for x in d) for d in descs]), comp,
+                        index_only)
+    assert np.array_equal(got.status, ref["status"])
+    for k in SOA:
+        assert np.array_equal(getattr(got, k), ref[k]), k
+    if not index_only:
+        assert np.array_equal(got.key_base, ref["key_base"])
+        assert np.array_equal(got.val_base, ref["val_base"])
+        assert got.key_arena.tobytes() == ref["key_arena"].tobytes()
+        assert got.val_arena.tobytes() == ref["val_arena"].tobytes()
+    return ref
+
+
+@pytest.mark.parametrize("index_only", [False, True])
+def test_golden_writer_cases(decoder, golden, index_only):
+    """Reference test segments (segment_reader_test.go inputs) decode to the
+    golden rows, including the nil value of TestReadBlankRecordUncompressed."""
+    for name, case in golden.items():
+        if case["kind"] != "writer":
+            continue
+        seg = np.frombuffer(unpack(case["segment_z"]), np.uint8)
+        d = descs_of(case)
+        got = decoder.decode(seg, d, case["compression"], index_only=index_only)
+        for b, blk in enumerate(case["blocks"]):
+            assert got.status[b] == blk["status"], (name, b)
+            rows = got.block_rows(b)
+            assert [[rowval(k), rowval(v)] for k, v in rows] == blk["rows"], (name, b)
+        _assert_same_as_oracle(got, seg, d, case["compression"], index_only)
+
+
+def test_reference_known_answers_on_gpu(decoder, golden):
+    """TestReadUncompressed's asserted rows, straight from the HIP decode."""
+    case = golden["ref_read_uncompressed_200"]
+    got = decoder.decode(unpack(case["segment_z"]), descs_of(case))
+    r0, r1 = got.block_rows(0), got.block_rows(1)
+    assert len(r0) + len(r1) == 200
+    assert r0[0] == (b"key000", b"value000") and r1[0] == (b"key180", b"value180")
+    assert r1[-1] == (b"key199", b"value199")
+    blank = golden["ref_blank_value"]
+    got = decoder.decode(unpack(blank["segment_z"]), descs_of(blank))
+    assert got.block_rows(1)[-1] == (b"key200", None)  # nil value (Q4)
+
+
+@pytest.mark.parametrize("comp", [_lib.COMP_NONE, _lib.COMP_LZ4])
+@pytest.mark.parametrize("index_only", [False, True])
+def test_crafted_edges(decoder, golden, comp, index_only):
+    """Overrun panics, short reads, EOF, OriginalSize 0, records past
+    OriginalSize, nil keys/values, u16-max key, >64 KiB block (HBM path),
+    600-row block (several row-table batches), unaligned offset, LZ4 flag."""
+    case = golden["crafted_edges"]
+    seg = unpack(case["segment_z"])
+    d = descs_of(case)
+    got = decoder.decode(seg, d, comp, index_only=index_only)
+    for b, blk in enumerate(case["blocks"]):
+        want_st = blk["status"] if comp == _lib.COMP_NONE else blk["status_lz4"]
+        want_rows = blk["rows"] if comp == _lib.COMP_NONE else blk["rows_lz4"]
+        assert got.status[b] == want_st, (b, blk["note"])
+        assert [[rowval(k), rowval(v)] for k, v in got.block_rows(b)] == want_rows, blk["note"]
+    _assert_same_as_oracle(got, seg, d, comp, index_only)
+
+
+def _digests(got: okv.Decoded, index_only):
+    dig = {"row_start": got.row_start, "status": got.status, "key_off": got.key_off,
+           "key_len": got.key_len, "val_off": got.val_off, "val_len": got.val_len}
+    if not index_only:
+        dig.update(key_base=got.key_base, val_base=got.val_base, key_arena=got.key_arena,
+                   val_arena=got.val_arena)
+    return {k: hashlib.sha256(v.tobytes()).hexdigest() for k, v in dig.items()}
+
+
+@pytest.mark.parametrize("name", ["c2_fixed_256x4k", "c3_zipf_8x64k"])
+@pytest.mark.parametrize("index_only", [False, True])
+def test_golden_synthetic_configs(decoder, golden, name, index_only):
+    """C2 (256 x 4 KiB, 16/64) and a C3-shaped sample (8 x 64 KiB Zipf):
+    SHA-256 of every output array equals the golden digest."""
+    c = golden[name]
+    kind = okv.sst.SYNTH_FIXED if c["gen"] == "fixed" else okv.sst.SYNTH_ZIPF
+    w = okv.synth_segment(kind, c["seed"], nblocks=c["nblocks"], threshold=c["threshold"],
+                          block_size=c["block_size"])
+    seg = w.data()
+    assert hashlib.sha256(seg.tobytes()).hexdigest() == c["segment_sha256"]
+    d = w.descs()[:c["decode_blocks"]]
+    got = decoder.decode(seg, d, index_only=index_only)
+    want = c["index" if index_only else "full"]
+    dig = _digests(got, index_only)
+    for k, v in dig.items():
+        assert v == want[k], k
+    assert int(got.row_start[-1]) == want["n_rows"]
+
+
+def test_c3_scale_against_c_oracle(decoder):
+    """A larger C3-shaped segment (512 x 64 KiB) against the C oracle,
+    plus size-independent properties."""
+    w = okv.synth_segment(okv.sst.SYNTH_ZIPF, 3, nblocks=512, threshold=57344, block_size=65536)
+    seg = w.data()
+    d = w.descs()[:512]
+    got = decoder.decode(seg, d)
+    ref = _assert_same_as_oracle(got, seg, d, 0, False)
+    n = int(got.row_start[-1])
+    assert n == int(ref["row_start"][-1]) and n > 512 * 20
+    # property: re-encoding the decoded rows reproduces the segment bytes
+    w2 = okv.SegmentWriter(57344, 65536)
+    for b in range(512):
+        for k, v in got.block_rows(b):
+            w2.WriteRow(k or b"", v or b"")
+    w2.Close(strict_go=False)
+    assert w2.data().tobytes()[:int(d[-1][0] + d[-1][1])] == \
+        seg.tobytes()[:int(d[-1][0] + d[-1][1])]
+
+
+def test_hash_blocks_matches_writer(decoder, golden):
+    """Device XXH64 of each block == BlockStat.Hash written by the writer
+    (segment_writer.go:185)."""
+    for name in ("ref_read_uncompressed_200", "ref_larger_than_block"):
+        case = golden[name]
+        h = decoder.hash_blocks(unpack(case["segment_z"]), descs_of(case))
+        assert h.tolist() == [b["hash"] for b in case["blocks"]]
+    w = okv.synth_segment(okv.sst.SYNTH_ZIPF, 3, nblocks=64, threshold=57344, block_size=65536)
+    h = decoder.hash_blocks(w.data(), w.descs())
+    assert h.tolist() == [b[2] for b in w.blocks()]
+
+
+def test_capacity_error_reports_totals(decoder, golden):
+    case = golden["ref_read_uncompressed_200"]
+    seg = np.frombuffer(unpack(case["segment_z"]), np.uint8)
+    d = descs_of(case)
+    rows, kb, vb = decoder.plan(seg, d)
+    # keys 6 B, values 8 B; per-block regions padded to 16 B: 1080->1088 + 120->128, 1440 + 160
+    assert (rows, kb, vb) == (200, 1216, 1600)
+    o = {k: np.zeros(n, t) for k, n, t in [("row_start", 3, np.uint64),
+                                           ("status", 2, np.int32)]}
+    small = _lib.DecodeOut(o["row_start"].ctypes.data, None, None, o["status"].ctypes.data,
+                           None, None, None, None, None, None, 0, 0, 0, 0, 0, 0, 0)
+    import ctypes as C
+    rc = _lib.lib().okv_decode_blocks(decoder._ctx, seg.ctypes.data, seg.size, d.ctypes.data,
+                                      2, 0, C.byref(small), 0)
+    assert rc == _lib.OKV_E_CAPACITY and small.n_rows == 200
+
+
+def test_device_pointer_api_torch(decoder):
+    """Device-resident mode (the bench path): torch tensors in HBM, async
+    enqueue, totals after sync."""
+    torch = pytest.importorskip("torch")
+    w = okv.synth_segment(okv.sst.SYNTH_ZIPF, 3, nblocks=32, threshold=57344, block_size=65536)
+    seg = w.data()
+    d = w.descs()[:32]
+    dev = torch.device("cuda", 0)
+    seg_t = torch.from_numpy(seg).to(dev)
+    d_t = torch.from_numpy(d.view(np.int64)).to(dev)
+    rows, kb, vb = decoder.plan_device(seg_t, seg.size, d_t, 32)
+    out = dict(row_start=torch.zeros(33, dtype=torch.int64, device=dev),
+               key_base=torch.zeros(32, dtype=torch.int64, device=dev),
+               val_base=torch.zeros(32, dtype=torch.int64, device=dev),
+               status=torch.zeros(32, dtype=torch.int32, device=dev),
+               key_off=torch.zeros(rows, dtype=torch.int64, device=dev),
+               key_len=torch.zeros(rows, dtype=torch.int16, device=dev),
+               val_off=torch.zeros(rows, dtype=torch.int64, device=dev),
+               val_len=torch.zeros(rows, dtype=torch.int32, device=dev),
+               key_arena=torch.zeros(kb, dtype=torch.uint8, device=dev),
+               val_arena=torch.zeros(vb, dtype=torch.uint8, device=dev))
+    decoder.decode_device(seg_t, seg.size, d_t, 32, out, sync=False)
+    decoder.sync()
+    host = decoder.decode(seg, d)
+    assert np.array_equal(out["row_start"].cpu().numpy().view(np.uint64), host.row_start)
+    assert np.array_equal(out["val_len"].cpu().numpy().view(np.uint32), host.val_len)
+    assert out["val_arena"].cpu().numpy().tobytes() == host.val_arena.tobytes()
+    assert out["key_arena"].cpu().numpy().tobytes() == host.key_arena.tobytes()
+
+
+def test_random_fuzz_against_c_oracle(decoder):
+    """Random record streams with truncation/corruption/odd offsets."""
+    rng = np.random.default_rng(2024)
+    for trial in range(25):
+        seg = bytearray()
+        descs = []
+        for b in range(int(rng.integers(1, 40))):
+            body = bytearray()
+            for _ in range(int(rng.integers(0, 30))):
+                kl = int(rng.choice([0, 1, 5, 16, 100, 300]))
+                vl = int(rng.choice([0, 1, 7, 64, 500, 3000]))
+                body += kl.to_bytes(2, "little") + vl.to_bytes(4, "little")
+                body += rng.integers(0, 256, kl + vl, dtype=np.uint8).tobytes()
+            orig = len(body)
+            if rng.random() < 0.3 and body:
+                orig = int(rng.integers(0, len(body) + 1))
+            if rng.random() < 0.2 and len(body) > 3:
+                body[int(rng.integers(0, len(body)))] = int(rng.integers(0, 256))
+            bsize = len(body) + int(rng.choice([0, 1, 5, 64, 4096]))
+            off = len(seg) + int(rng.choice([0, 0, 1, 3, 8]))
+            seg += bytes(off - len(seg))
+            seg += body + bytes(bsize - len(body))
+            descs.append((off, bsize, orig, 0))
+        d = np.array(descs, np.uint64).reshape(-1, 4)
+        comp = int(rng.choice([0, 0, 2]))
+        for index_only in (False, True):
+            got = decoder.decode(bytes(seg), d, comp, index_only=index_only)
+            _assert_same_as_oracle(got, bytes(seg), d, comp, index_only)
+
+
+def test_empty_batch(decoder):
+    got = decoder.decode(b"\x00" * 32, np.zeros((0, 4), np.uint64))
+    assert got.row_start.tolist() == [0]

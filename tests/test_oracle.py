@@ -1,0 +1,409 @@
+"""Pin the CPU oracle (oracle/) before trusting it.
+
+1. Every known answer the reference's own Go tests assert
+   (/root/reference/sst/segment_reader_test.go, segment_row_iter_test.go,
+   segment_writer_test.go) is re-asserted against the Python restatement and,
+   where it applies, the C restatement.
+2. XXH64 against the specification value and the `xxhash` 3.8.1 package.
+3. The two independent restatements (C and Python) agree byte for byte.
+4. The committed golden vectors regenerate identically.
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import coracle as CO
+from oracle import pyoracle as P
+from tests.conftest import GOLDEN, unpack
+
+R200 = [(b"key%03d" % i, b"value%03d" % i) for i in range(200)]
+
+
+def write(rows, **kw):
+    w = P.SegmentWriter(P.SegmentWriterOptions(**kw))
+    for k, v in rows:
+        w.WriteRow(k, v)
+    flen, meta = w.Close()
+    return bytes(w.external), flen, meta
+
+
+# ---- XXH64 -------------------------------------------------------------------
+
+
+def test_xxh64_spec_and_implementations():
+    assert P.xxh64(b"") == 0xEF46DB3751D8E999 == 17241709254077376921
+    assert P.xxh64_py(b"") == CO.xxh64(b"") == 0xEF46DB3751D8E999
+    rng = random.Random(7)
+    for n in list(range(0, 70)) + [100, 1000, 4096, 65536]:
+        d = bytes(rng.getrandbits(8) for _ in range(n))
+        seed = rng.choice([0, 1, 2 ** 64 - 1, 12345])
+        assert P.xxh64(d, seed) == P.xxh64_py(d, seed) == CO.xxh64(d, seed)
+
+
+# ---- reference known answers (segment_reader_test.go) ----------------------
+
+
+def test_reference_known_answers_uncompressed():
+    """TestReadUncompressed, segment_reader_test.go:12-269."""
+    seg, flen, meta = write(R200)
+    r = P.SegmentReader(seg, flen)
+    md = r.BytesToMetadata(meta)
+    r.LoadCachedMetadata(md)
+    assert md.FirstKey == b"key000" and md.LastKey == b"key199"  # :61-66
+    assert md.BlockIndex.Len() == 2  # :77
+    b0, ok = md.BlockIndex.Get(b"key000")
+    assert ok and b0.FirstKey == b"key000" and b0.OriginalSize == 3600  # :81-86
+    assert b0.CompressedSize == 0 and b0.Offset == 0  # :87-92
+    b1, ok = md.BlockIndex.Get(b"key180")
+    assert ok and b1.OriginalSize == 400 and b1.CompressedSize == 0  # :94-102
+    assert b1.Offset == 4096  # :103
+    rows = r.ReadBlockWithStat(b0)
+    assert rows[0].Key == b"key000" and rows[0].Value == b"value000"  # :116-121
+    rows2 = r.ReadBlockWithStat(b1)
+    assert len(rows) + len(rows2) == 200  # :131
+    assert rows2[0].Key == b"key180" and rows2[0].Value == b"value180"  # :135-140
+    assert rows2[-1].Key == b"key199" and rows2[-1].Value == b"value199"  # :142-147
+    assert r.GetRow(b"key000").Value == b"value000"  # :150-159
+    with pytest.raises(P.GoError) as e:
+        r.GetRow(b"fuhguiregui")  # :161-164
+    assert e.value.kind == P.ErrNoRows
+    assert r.GetRow(b"key101").Value == b"value101"  # :166-179
+    assert r.GetRow(b"key199").Value == b"value199"  # :181-190
+    g = r.GetRange(b"key000", b"key180")  # :193-212
+    assert len(g) == 180 and g[0].Key == b"key000" and g[-1].Key == b"key179"
+    assert g[-1].Value == b"value179"
+    assert len(r.GetRange(b"", b"key180")) == 180  # :215-222
+    g = r.GetRange(b"key180", b"\xff")  # :224-244
+    assert len(g) == 20 and g[0].Key == b"key180" and g[-1].Key == b"key199"
+    g = r.GetRange(b"key199", b"\xff")  # :246-259
+    assert len(g) == 1 and g[0].Key == b"key199" and g[0].Value == b"value199"
+    r.Close()  # :261-268
+    with pytest.raises(P.GoError) as e:
+        r.Close()
+    assert e.value.kind == P.ErrAlreadyClosed
+    # the C restatement derives the same bytes and index
+    w = CO.Writer()
+    for k, v in R200:
+        assert w.write_row(k, v) == 0
+    rc, cseg, cmeta = w.close()
+    assert rc == 0 and cseg == seg and cmeta == meta
+    rc, cm = CO.parse_meta(meta)
+    assert rc == 0 and [(e["first_key"], e["offset"], e["original_size"], e["compressed_size"])
+                        for e in cm["entries"]] == [(b"key000", 0, 3600, 0),
+                                                   (b"key180", 4096, 400, 0)]
+
+
+def test_reference_known_answers_blank_value():
+    """TestReadBlankRecordUncompressed, segment_reader_test.go:271-326."""
+    seg, flen, meta = write(R200 + [(b"key200", b"")])
+    r = P.SegmentReader(seg, flen)
+    r.LoadCachedMetadata(r.BytesToMetadata(meta))
+    row = r.GetRow(b"key200")
+    assert row.Key == b"key200" and P._b(row.Value) == b""  # :316-325
+    assert row.Value is None  # Q4: readBytes(0) returns nil (segment_reader.go:490-493)
+
+
+def test_reference_known_answers_single_row():
+    """TestReadSingleRecordUncompressed, segment_reader_test.go:328-511."""
+    seg, flen, meta = write(R200[:1])
+    r = P.SegmentReader(seg, flen)
+    md = r.BytesToMetadata(meta)
+    r.LoadCachedMetadata(md)
+    assert md.FirstKey == b"key000" and md.LastKey == b"key000"
+    assert md.BlockIndex.Len() == 1  # :388
+    b0, _ = md.BlockIndex.Get(b"key000")
+    assert b0.OriginalSize == 20 and b0.CompressedSize == 0 and b0.Offset == 0  # :392-403
+    rows = r.ReadBlockWithStat(b0)
+    assert rows[0].Key == b"key000" and rows[-1].Value == b"value000"
+    assert r.GetRow(b"key000").Value == b"value000"
+    with pytest.raises(P.GoError):
+        r.GetRow(b"fuhguiregui")
+    assert len(r.GetRange(b"key000", b"key000")) == 0  # :457-464
+    assert len(r.GetRange(b"", b"key000")) == 0  # :466-473
+    g = r.GetRange(b"", b"\xff")  # :476-495
+    assert len(g) == 1 and g[0].Key == b"key000"
+    assert len(r.GetRange(b"key000", b"\xff")) == 1  # :497-510
+
+
+def test_reference_zstd_known_answers_are_parity_unpinned():
+    """TestReadCompressionZSTD (segment_reader_test.go:513-723) pins
+    CompressedSize 298 and Hash 7503979350938866005, which depend on the
+    klauspost/compress v1.17.9 encoder -- not runnable offline.  The restated
+    writer refuses zstd rather than guess."""
+    with pytest.raises(NotImplementedError):
+        P.SegmentWriter(P.SegmentWriterOptions(ZSTDCompressionLevel=1)).WriteRow(b"k", b"v")
+    assert CO.Writer(zstd_level=1).write_row(b"k", b"v") == -106
+
+
+def test_reference_corrupt_file_end():
+    """TestReadCorruptFileEnd, segment_reader_test.go:727-776 (10 trailing
+    random bytes; crypto/rand replaced by a seeded generator)."""
+    seg, flen, meta = write(R200)
+    rnd = bytes(random.Random(1).getrandbits(8) for _ in range(10))
+    r = P.SegmentReader(seg + rnd, flen)
+    with pytest.raises(P.GoError) as e:
+        r.FetchAndLoadMetadata()
+    assert e.value.kind == P.ErrInvalidMagicNumber and e.value.kind in P.FATAL
+    rc, _ = CO.fetch_meta(seg + rnd, flen)
+    assert rc == -201
+
+
+def test_reference_corrupt_file_middle():
+    """TestReadCorruptFileMiddle, segment_reader_test.go:778-830: 10 bytes
+    written straight into the sink after row 101 shift every offset."""
+    w = P.SegmentWriter(P.SegmentWriterOptions())
+    for i, (k, v) in enumerate(R200):
+        w.WriteRow(k, v)
+        if i == 101:
+            w.external += bytes(random.Random(2).getrandbits(8) for _ in range(10))
+    flen, meta = w.Close()
+    data = bytes(w.external)
+    r = P.SegmentReader(data, flen)
+    with pytest.raises(P.GoError) as e:
+        r.FetchAndLoadMetadata()
+    assert e.value.kind == P.ErrMismatchedMetaBlockHash and e.value.kind in P.FATAL
+    rc, _ = CO.fetch_meta(data, flen)
+    assert rc == -203
+    # and the intact file loads
+    seg, flen2, meta2 = write(R200)
+    rc, m = CO.fetch_meta(seg, flen2)
+    assert rc == 0 and m["first_key"] == b"key000" and len(m["entries"]) == 2
+
+
+def test_reference_writer_errors():
+    """TestEmptyKey segment_writer_test.go:114-127 and the WriteRow checks
+    (segment_writer.go:81-92)."""
+    w = P.SegmentWriter(P.SegmentWriterOptions())
+    for bad, kind in [((b"", b""), P.ErrInvalidKey), ((b"k" * 65536, b""), P.ErrKeyTooLarge)]:
+        with pytest.raises(P.GoError) as e:
+            w.WriteRow(*bad)
+        assert e.value.kind == kind
+    cw = CO.Writer()
+    assert cw.write_row(b"", b"") == -104
+    assert cw.write_row(b"k" * 65536, b"") == -101
+    # Q1: Close with no pending row panics (defer on a nil interface, :212)
+    with pytest.raises(P.GoPanic):
+        P.SegmentWriter(P.SegmentWriterOptions()).Close()
+    assert CO.Writer().close()[0] == -105
+    w = P.SegmentWriter(P.SegmentWriterOptions())
+    w.WriteRow(b"a", b"b")
+    w.Close()
+    with pytest.raises(P.GoError) as e:
+        w.WriteRow(b"a", b"b")
+    assert e.value.kind == P.ErrWriterClosed
+
+
+def test_reference_larger_than_block():
+    """TestSegmentWriterLargerThanBlock segment_writer_test.go:73-112: a 10 511 B
+    row pads to 12 288 (Q2 rule: (len/DBS+1)*DBS)."""
+    rows = [(b"a" * 511, b"b" * 10000)] + [(b"key%d" % i, b"value%d" % i) for i in range(200)]
+    seg, flen, meta = write(rows)
+    md = P.bytes_to_metadata(meta)
+    assert [st.desc()[:3] for st in md.entries] == [(0, 12288, 10517), (12288, 4096, 3600),
+                                                    (16384, 4096, 180)]
+    total = sum(len(P.read_block(seg, st.desc(), 0)[1]) for st in md.entries)
+    assert total == 201
+
+
+# ---- RowIter (segment_row_iter_test.go) ----------------------------------------
+
+
+def _iter_reader():
+    seg, flen, meta = write(R200)
+    r = P.SegmentReader(seg, flen)
+    return r
+
+
+def test_reference_rowiter_next():
+    """TestRowIterNext segment_row_iter_test.go:12-134."""
+    r = _iter_reader()
+    it = r.RowIter(P.DirectionAscending)
+    assert it.Next().Key == b"key000"
+    assert it.Next().Key == b"key001"
+    for _ in range(198):
+        row = it.Next()
+    assert row.Key == b"key199" and row.Value == b"value199"
+    with pytest.raises(P.GoError) as e:
+        it.Next()
+    assert e.value.kind == P.EOF
+    it = r.RowIter(P.DirectionDescending)
+    assert it.Next().Key == b"key199"
+    assert it.Next().Key == b"key198"
+    for _ in range(197):
+        row = it.Next()
+    assert row.Key == b"key001" and row.Value == b"value001"
+
+
+def _eof(it):
+    with pytest.raises(P.GoError) as e:
+        it.Next()
+    assert e.value.kind == P.EOF
+
+
+def test_reference_rowiter_seek():
+    """TestRowIterSeek segment_row_iter_test.go:136-378."""
+    r = _iter_reader()
+    it = r.RowIter(P.DirectionAscending)
+    it.Seek(b"key010")
+    assert it.Next().Key == b"key010" and it.Next().Key == b"key011"
+    it.Seek(P.UnboundStart)
+    assert it.Next().Key == b"key000"
+    it.Seek(b"key200")
+    _eof(it)
+    it.Seek(P.UnboundEnd)
+    _eof(it)
+    it = r.RowIter(P.DirectionDescending)
+    it.Seek(b"key010")
+    assert it.Next().Key == b"key010" and it.Next().Key == b"key009"
+    it.Seek(P.UnboundStart)
+    _eof(it)
+    it.Seek(P.UnboundEnd)
+    assert it.Next().Key == b"key199"
+    it.Seek(b"key200")
+    assert it.Next().Key == b"key199"
+    it.Seek(b"key")
+    _eof(it)
+    it.Seek(P.UnboundEnd)
+    assert it.Next().Key == b"key199"
+    it.Seek(b"key000")
+    assert it.Next().Key == b"key000"
+    _eof(it)
+
+
+def test_reference_rollover_descending_seek():
+    """TestRollover segment_row_iter_test.go:380-450 (run with BloomFilter=nil:
+    the bloom only feeds GetRow, not RowIter)."""
+    rows = [(b"key%03d" % i, b"value%03d-I-SHOULD-NOT-SHOW" % i) for i in range(1, 200, 2)]
+    seg, flen, meta = write(rows + [(b"key900", b"value900")])
+    r = P.SegmentReader(seg, flen)
+    it = r.RowIter(P.DirectionDescending)
+    it.Seek(b"key006")
+    got = [it.Next().Key for _ in range(3)]
+    assert got == [b"key005", b"key003", b"key001"]
+    _eof(it)
+
+
+# ---- the two restatements agree ---------------------------------------------
+
+
+def _cmp_soa(seg, descs, comp):
+    for index_only in (False, True):
+        py = P.decode_soa(seg, [tuple(int(x) for x in d) for d in descs], comp, index_only)
+        c = CO.decode_soa(seg, CO.descs_array([tuple(int(x) for x in d) for d in descs]), comp,
+                          index_only)
+        assert list(c["status"]) == py["status"]
+        assert [int(x) for x in c["row_start"]] == py["row_start"]
+        for k in ("key_off", "key_len", "val_off", "val_len"):
+            assert [int(x) for x in c[k]] == py[k], k
+        if not index_only:
+            assert [int(x) for x in c["key_base"]] == py["key_base"]
+            assert [int(x) for x in c["val_base"]] == py["val_base"]
+            assert c["key_arena"].tobytes() == py["key_arena"]
+            assert c["val_arena"].tobytes() == py["val_arena"]
+
+
+def test_c_and_python_restatements_agree(golden):
+    for name in ("ref_read_uncompressed_200", "ref_larger_than_block", "lz4_flag_200"):
+        case = golden[name]
+        seg = unpack(case["segment_z"])
+        descs = [b["desc"] for b in case["blocks"]]
+        _cmp_soa(seg, descs, case["compression"])
+    case = golden["crafted_edges"]
+    seg = unpack(case["segment_z"])
+    for comp in (P.COMP_NONE, P.COMP_LZ4):
+        _cmp_soa(seg, [b["desc"] for b in case["blocks"]], comp)
+    # synthetic segments: C writer == Python writer, and decodes agree
+    for gen, nb, th, bs in (("fixed", 12, 3584, 4096), ("zipf", 3, 57344, 65536)):
+        src = P.rows_fixed(10 ** 12, 1) if gen == "fixed" else P.rows_zipf(3)
+        pw = P.SegmentWriter(P.SegmentWriterOptions(th, bs))
+        cw = CO.Writer(th, bs)
+        for k, v in src:
+            if len(pw.index) >= nb and pw.block_open:
+                break
+            pw.WriteRow(k, v)
+            assert cw.write_row(k, v) == 0
+        flen, meta = pw.Close()
+        rc, cseg, cmeta = cw.close()
+        assert rc == 0 and cseg == bytes(pw.external) and cmeta == meta
+        _cmp_soa(cseg, [st.desc() for st in P.bytes_to_metadata(meta).entries], 0)
+
+
+def test_random_blocks_restatements_agree():
+    """Fuzz: random record streams with random truncation/corruption."""
+    rng = random.Random(11)
+    for trial in range(40):
+        seg = bytearray()
+        descs = []
+        for b in range(rng.randint(1, 6)):
+            body = bytearray()
+            for _ in range(rng.randint(0, 8)):
+                k = bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 3, 16, 40])))
+                v = bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 1, 7, 64, 300])))
+                body += len(k).to_bytes(2, "little") + len(v).to_bytes(4, "little") + k + v
+            orig = len(body)
+            if rng.random() < 0.3 and body:
+                orig = rng.randint(0, len(body))
+            if rng.random() < 0.2 and len(body) > 3:
+                pos = rng.randrange(len(body) - 1)
+                body[pos] = rng.getrandbits(8)
+            bsize = len(body) + rng.choice([0, 1, 5, 64])
+            off = len(seg) + rng.choice([0, 0, 1, 3])
+            seg += bytes(off - len(seg))
+            seg += body + bytes(bsize - len(body))
+            descs.append((off, bsize, orig, 0))
+        if rng.random() < 0.2:
+            descs.append((len(seg) + 5, 8, 8, 0))
+        _cmp_soa(bytes(seg), descs, rng.choice([0, 0, 2]))
+
+
+# ---- golden vectors regenerate -------------------------------------------------
+
+
+def test_golden_vectors_regenerate(tmp_path):
+    """make_golden.py (the committed generator) reproduces golden.json."""
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    out_path = tmp_path / "golden.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "golden", "make_golden.py"),
+                        str(out_path)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    with open(GOLDEN) as f:
+        committed = json.load(f)
+    with open(out_path) as f:
+        fresh = json.load(f)
+    assert fresh == committed
+
+
+def test_golden_writer_cases_match_oracles(golden):
+    for name, case in golden.items():
+        if case["kind"] != "writer":
+            continue
+        seg = unpack(case["segment_z"])
+        assert len(seg) == case["file_len"]
+        md = P.bytes_to_metadata(bytes.fromhex(case["meta"]))
+        assert [list(st.desc()) for st in md.entries] == [b["desc"] for b in case["blocks"]]
+        assert [st.Hash for st in md.entries] == [b["hash"] for b in case["blocks"]]
+        for st, b in zip(md.entries, case["blocks"]):
+            assert P.xxh64(seg[st.Offset:st.Offset + st.BlockSize]) == b["hash"]
+
+
+def test_golden_synth_cases_match_oracle(golden):
+    import hashlib
+    for name in ("c2_fixed_256x4k", "c3_zipf_8x64k"):
+        c = golden[name]
+        rows = P.rows_fixed(10 ** 12, c["seed"]) if c["gen"] == "fixed" else P.rows_zipf(c["seed"])
+        seg, meta, w = P.build_segment(rows, nblocks_target=c["nblocks"],
+                                       threshold=c["threshold"], block_size=c["block_size"])
+        assert hashlib.sha256(seg).hexdigest() == c["segment_sha256"]
+        descs = CO.descs_array([st.desc() for st in P.bytes_to_metadata(meta).entries]
+                               [:c["nblocks"]])
+        o = CO.decode_soa(seg, descs, 0, False)
+        for k in ("row_start", "key_off", "key_len", "val_off", "val_len", "key_arena",
+                  "val_arena", "key_base", "val_base", "status"):
+            assert hashlib.sha256(o[k].tobytes()).hexdigest() == c["full"][k], (name, k)

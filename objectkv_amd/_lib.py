@@ -64,6 +64,15 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built: run objectkv_amd._lib.build() "
                           "(or __graft_entry__.build())")
+    # PyTorch-ROCm ships its own libamdhip64.so with the same soname
+    # (libamdhip64.so.7) as /opt/rocm's.  Loading torch first makes our
+    # DT_NEEDED resolve to the copy already in the process, so one HIP runtime
+    # serves both (torch tensors and our kernels); loading ours first would put
+    # two runtimes in the process and torch would then see no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     p, u64, i32, u32 = C.c_void_p, C.c_uint64, C.c_int, C.c_uint32
     sig = {

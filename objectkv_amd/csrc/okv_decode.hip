@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -267,7 +268,7 @@ __device__ __forceinline__ void copy_region(const Src& src, uint8_t* __restrict_
   }
 }
 
-template <class Src>
+template <int V, class Src>
 __device__ __forceinline__ void materialise(const Src& src, const CopyParams& P,
                                            CopySmem& sm, uint64_t rows, uint64_t kbytes,
                                            uint64_t vbytes, uint64_t row0, uint64_t kb0,
@@ -295,6 +296,7 @@ __device__ __forceinline__ void materialise(const Src& src, const CopyParams& P,
       sm.vpre[nb] = vacc;
     }
     __syncthreads();
+    if (V < 2) continue;  // diagnostic ablation (okv_copy_kernel<V>)
     // SoA row index (coalesced over rows)
     for (int i = tid; i < nb; i += kThreads) {
       const uint64_t g = row0 + r0 + i;
@@ -303,6 +305,7 @@ __device__ __forceinline__ void materialise(const Src& src, const CopyParams& P,
       P.val_off[g] = vb0 + sm.vpre[i];
       P.val_len[g] = sm.vlen[i];
     }
+    if (V < 3) continue;
     copy_region(src, P.key_arena, kb0, sm.kpre, sm.rec, sm.klen, sm.klen, false, nb, Gk);
     copy_region(src, P.val_arena, vb0, sm.vpre, sm.rec, sm.klen, sm.vlen, true, nb, Gv);
     __syncthreads();
@@ -316,6 +319,10 @@ __device__ __forceinline__ void materialise(const Src& src, const CopyParams& P,
   }
 }
 
+// V selects a diagnostic ablation (tools/ablate.py): 0 stage only, 1 + header
+// chase, 2 + SoA index, 3 = the full kernel (the only variant the API uses
+// unless OKV_COPY_VARIANT is set).
+template <int V>
 __global__ __launch_bounds__(kThreads) void okv_copy_kernel(CopyParams P) {
   __shared__ CopySmem sm;
   const uint32_t b = blockIdx.x;
@@ -357,11 +364,15 @@ __global__ __launch_bounds__(kThreads) void okv_copy_kernel(CopyParams P) {
       if (k < int(rounds) && ci < nch) sm.stage[1 + ci] = v[k];
     }
     __syncthreads();
+    if (V == 0) {
+      if (tid == 0 && sm.stage[1 + (c.pend & 1023)].x == 0x12345678u) P.blk_status[b] = 99;
+      return;
+    }
     LdsSrc src{reinterpret_cast<const uint32_t*>(sm.stage), 16u + shift};
-    materialise(src, P, sm, c.rows, c.kbytes, c.vbytes, row0, kb0, vb0);
+    materialise<V>(src, P, sm, c.rows, c.kbytes, c.vbytes, row0, kb0, vb0);
   } else {
     GlobalSrc src{P.seg, P.seg_bytes, d.offset};
-    materialise(src, P, sm, c.rows, c.kbytes, c.vbytes, row0, kb0, vb0);
+    materialise<V>(src, P, sm, c.rows, c.kbytes, c.vbytes, row0, kb0, vb0);
   }
 }
 
@@ -519,6 +530,7 @@ struct okv_ctx {
   uint64_t* d_hash = nullptr;
   size_t cap_hash = 0;
   // per-pass event timing (okv_profile)
+  int variant = 3;  // diagnostic ablation selector (OKV_COPY_VARIANT)
   bool prof = false;
   std::vector<hipEvent_t> ev;  // 4 per timed call
   size_t ev_used = 0;
@@ -660,7 +672,12 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       hipLaunchKernelGGL(okv_index_kernel, dim3((nblk + kThreads - 1) / kThreads),
                          dim3(kThreads), 0, ctx->stream, P);
     else
-      hipLaunchKernelGGL(okv_copy_kernel, dim3(nblk), dim3(kThreads), 0, ctx->stream, P);
+      switch (ctx->variant) {
+        case 0: hipLaunchKernelGGL(okv_copy_kernel<0>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
+        case 1: hipLaunchKernelGGL(okv_copy_kernel<1>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
+        case 2: hipLaunchKernelGGL(okv_copy_kernel<2>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
+        default: hipLaunchKernelGGL(okv_copy_kernel<3>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P);
+      }
     OKV_HIP(hipGetLastError());
   }
   prof_mark(ctx, 3);
@@ -775,6 +792,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   if (hipSetDevice(device) != hipSuccess) return nullptr;
   okv_ctx* ctx = new okv_ctx();
   ctx->device = device;
+  if (const char* v = getenv("OKV_COPY_VARIANT")) ctx->variant = atoi(v);
   if (stream) {
     ctx->stream = static_cast<hipStream_t>(stream);
   } else {

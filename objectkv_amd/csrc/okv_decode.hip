@@ -193,13 +193,24 @@ struct CopyParams {
   uint64_t row_cap, key_cap, val_cap;
 };
 
-struct __align__(16) CopySmem {
-  uint4 stage[(kStage + kStagePad) / 16];  // [16 B guard][block image][guard]
-  uint64_t rec[kRowBatch];                 // record position within the block
-  uint64_t kpre[kRowBatch + 1];            // key-byte prefix within the block
-  uint64_t vpre[kRowBatch + 1];            // value-byte prefix within the block
+struct SlowRows {               // general path: 64-bit positions, batched rows
+  uint64_t rec[kRowBatch];        // record position within the block
+  uint64_t kpre[kRowBatch + 1];   // key-byte prefix within the block
+  uint64_t vpre[kRowBatch + 1];   // value-byte prefix within the block
   uint32_t klen[kRowBatch];
   uint32_t vlen[kRowBatch];
+};
+struct FastRows {               // fast path: block staged in LDS, <= kFastRows rows
+  uint32_t rec[kFastRows + 1];    // record position; rec[rows] = end of the walk
+  uint32_t kpre[kFastRows + 1];   // exclusive prefix of key lengths
+  uint32_t vpre[kFastRows + 1];   // exclusive prefix of value lengths
+};
+struct __align__(16) CopySmem {
+  uint4 stage[(kStage + kStagePad) / 16];  // [16 B guard][block image][guard]
+  union {
+    SlowRows s;
+    FastRows f;
+  };
 };
 
 // Byte source: the LDS image of the block (byte index = 16 + shift + pos).
@@ -239,7 +250,7 @@ __device__ __forceinline__ uint32_t group_size(uint64_t avg) {
 //   row i bytes = src[spos_i, spos_i + len_i) -> arena[dbase + pre_i, ...).
 // Lane groups of G lanes own one row; each lane writes 16-byte aligned
 // destination chunks (dwordx4), masked head/tail chunks with narrow stores.
-template <class Src>
+template <int V, class Src>
 __device__ __forceinline__ void copy_region(const Src& src, uint8_t* __restrict__ arena,
                                             uint64_t dbase, const uint64_t* pre,
                                             const uint64_t* rec, const uint32_t* klen,
@@ -255,13 +266,13 @@ __device__ __forceinline__ void copy_region(const Src& src, uint8_t* __restrict_
     const uint64_t c0 = d0 & ~uint64_t(15), c1 = (d0 + L + 15) & ~uint64_t(15);
     for (uint64_t ca = c0 + 16ull * sub; ca < c1; ca += 16ull * G) {
       const int64_t rel = int64_t(ca) - int64_t(d0);
-      const uint4 v = src.load16(s0 + rel);
+      const uint4 v = (V == 5) ? make_uint4(uint32_t(ca), 0, 0, 0) : src.load16(s0 + rel);
       const uint32_t lo = ca < d0 ? uint32_t(d0 - ca) : 0u;
       const uint64_t end = d0 + L - ca;
       const uint32_t hi = end < 16 ? uint32_t(end) : 16u;
       if (lo == 0 && hi == 16) {
         *reinterpret_cast<uint4*>(arena + ca) = v;
-      } else {
+      } else if (V != 4) {
         store_partial(arena + ca, v, lo, hi);
       }
     }
@@ -283,31 +294,29 @@ __device__ __forceinline__ void materialise(const Src& src, const CopyParams& P,
       for (int i = 0; i < nb; ++i) {
         uint32_t kl, vl;
         src.header(p, kl, vl);
-        sm.rec[i] = p;
-        sm.klen[i] = kl;
-        sm.vlen[i] = vl;
-        sm.kpre[i] = kacc;
-        sm.vpre[i] = vacc;
+        sm.s.rec[i] = p;
+        sm.s.klen[i] = kl;
+        sm.s.vlen[i] = vl;
+        sm.s.kpre[i] = kacc;
+        sm.s.vpre[i] = vacc;
         kacc += kl;
         vacc += vl;
         p += 6 + uint64_t(kl) + uint64_t(vl);
       }
-      sm.kpre[nb] = kacc;
-      sm.vpre[nb] = vacc;
+      sm.s.kpre[nb] = kacc;
+      sm.s.vpre[nb] = vacc;
     }
     __syncthreads();
-    if (V < 2) continue;  // diagnostic ablation (okv_copy_kernel<V>)
     // SoA row index (coalesced over rows)
     for (int i = tid; i < nb; i += kThreads) {
       const uint64_t g = row0 + r0 + i;
-      P.key_off[g] = kb0 + sm.kpre[i];
-      P.key_len[g] = uint16_t(sm.klen[i]);
-      P.val_off[g] = vb0 + sm.vpre[i];
-      P.val_len[g] = sm.vlen[i];
+      P.key_off[g] = kb0 + sm.s.kpre[i];
+      P.key_len[g] = uint16_t(sm.s.klen[i]);
+      P.val_off[g] = vb0 + sm.s.vpre[i];
+      P.val_len[g] = sm.s.vlen[i];
     }
-    if (V < 3) continue;
-    copy_region(src, P.key_arena, kb0, sm.kpre, sm.rec, sm.klen, sm.klen, false, nb, Gk);
-    copy_region(src, P.val_arena, vb0, sm.vpre, sm.rec, sm.klen, sm.vlen, true, nb, Gv);
+    copy_region<V>(src, P.key_arena, kb0, sm.s.kpre, sm.s.rec, sm.s.klen, sm.s.klen, false, nb, Gk);
+    copy_region<V>(src, P.val_arena, vb0, sm.s.vpre, sm.s.rec, sm.s.klen, sm.s.vlen, true, nb, Gv);
     __syncthreads();
   }
   // zero the 16-byte padding tail of each arena region
@@ -317,6 +326,82 @@ __device__ __forceinline__ void materialise(const Src& src, const CopyParams& P,
     if (ke & 15) store_partial(P.key_arena + (ke & ~uint64_t(15)), z, uint32_t(ke & 15), 16);
     if (ve & 15) store_partial(P.val_arena + (ve & ~uint64_t(15)), z, uint32_t(ve & 15), 16);
   }
+}
+
+// ---- fast path: the block is staged in LDS and has <= kFastRows rows ------
+// Every arena store is a full, aligned 16-byte chunk.  A chunk is owned by
+// the row containing its first byte; its owner lane assembles it in
+// registers, merging bytes of the following rows when the chunk spills past
+// its row (no partial stores, so neighbouring chunks never race).  The last
+// chunk of a region is zero-filled past the region end (16-byte padding).
+template <bool kVal>
+__device__ __forceinline__ void copy_region_fast(const uint4* __restrict__ s4, uint32_t bias,
+                                                 uint8_t* __restrict__ arena, uint64_t dbase,
+                                                 const FastRows& t, int rows, uint32_t G) {
+  const uint32_t* pre = kVal ? t.vpre : t.kpre;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t grp = tid / G, sub = tid % G, ngrp = kThreads / G;
+  for (uint32_t i = grp; i < uint32_t(rows); i += ngrp) {
+    const uint32_t p0 = pre[i], p1 = pre[i + 1];
+    if (p1 == p0) continue;
+    const uint32_t cfirst = (p0 + 15) >> 4, clast = (p1 - 1) >> 4;
+    const uint32_t si = bias + t.rec[i] + 6 + (kVal ? t.kpre[i + 1] - t.kpre[i] : 0u);
+    for (uint32_t c = cfirst + sub; c <= clast; c += G) {
+      const uint32_t cs = c << 4, ce = cs + 16;
+      uint4 out = load16_lds_b128(s4, si + (cs - p0));
+      if (ce > p1) {  // spills past row i: keep [0, p1-cs), gather the rest
+        out = merge_bytes(make_uint4(0, 0, 0, 0), out, 0, int32_t(p1 - cs));
+        for (uint32_t j = i + 1; j < uint32_t(rows) && pre[j] < ce; ++j) {
+          const uint32_t q0 = pre[j], q1 = pre[j + 1];
+          if (q1 == q0) continue;
+          const uint32_t sj = bias + t.rec[j] + 6 + (kVal ? t.kpre[j + 1] - t.kpre[j] : 0u);
+          const uint4 v = load16_lds_b128(s4, sj - (q0 - cs));
+          out = merge_bytes(out, v, int32_t(q0 - cs), int32_t((q1 < ce ? q1 : ce) - cs));
+        }
+      }
+      *reinterpret_cast<uint4*>(arena + dbase + cs) = out;
+    }
+  }
+}
+
+template <int V>
+__device__ __forceinline__ void materialise_fast(const CopyParams& P, CopySmem& sm,
+                                                uint32_t bias, int rows, uint64_t kbytes,
+                                                uint64_t vbytes, uint64_t row0, uint64_t kb0,
+                                                uint64_t vb0) {
+  const uint32_t tid = threadIdx.x;
+  FastRows& t = sm.f;
+  if (tid == 0) {
+    // serial header chase in LDS: record i+1 starts at rec_i + 6 + klen_i + vlen_i
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(sm.stage);
+    uint32_t p = 0, ka = 0, va = 0;
+    for (int i = 0; i < rows; ++i) {
+      uint32_t kl, vl;
+      header_lds(sw, bias + p, kl, vl);
+      t.rec[i] = p;
+      t.kpre[i] = ka;
+      t.vpre[i] = va;
+      ka += kl;
+      va += vl;
+      p += 6 + kl + vl;
+    }
+    t.rec[rows] = p;
+    t.kpre[rows] = ka;
+    t.vpre[rows] = va;
+  }
+  __syncthreads();
+  if (V < 2) return;  // diagnostic ablation (okv_copy_kernel<V>)
+  for (int i = tid; i < rows; i += kThreads) {
+    const uint64_t g = row0 + i;
+    P.key_off[g] = kb0 + t.kpre[i];
+    P.key_len[g] = uint16_t(t.kpre[i + 1] - t.kpre[i]);
+    P.val_off[g] = vb0 + t.vpre[i];
+    P.val_len[g] = t.vpre[i + 1] - t.vpre[i];
+  }
+  if (V < 3) return;
+  const uint32_t Gk = group_size(kbytes / rows), Gv = group_size(vbytes / rows);
+  copy_region_fast<false>(sm.stage, bias, P.key_arena, kb0, t, rows, Gk);
+  copy_region_fast<true>(sm.stage, bias, P.val_arena, vb0, t, rows, Gv);
 }
 
 // V selects a diagnostic ablation (tools/ablate.py): 0 stage only, 1 + header
@@ -368,8 +453,12 @@ __global__ __launch_bounds__(kThreads) void okv_copy_kernel(CopyParams P) {
       if (tid == 0 && sm.stage[1 + (c.pend & 1023)].x == 0x12345678u) P.blk_status[b] = 99;
       return;
     }
-    LdsSrc src{reinterpret_cast<const uint32_t*>(sm.stage), 16u + shift};
-    materialise<V>(src, P, sm, c.rows, c.kbytes, c.vbytes, row0, kb0, vb0);
+    if (c.rows <= uint64_t(kFastRows)) {
+      materialise_fast<V>(P, sm, 16u + shift, int(c.rows), c.kbytes, c.vbytes, row0, kb0, vb0);
+    } else {
+      LdsSrc src{reinterpret_cast<const uint32_t*>(sm.stage), 16u + shift};
+      materialise<V>(src, P, sm, c.rows, c.kbytes, c.vbytes, row0, kb0, vb0);
+    }
   } else {
     GlobalSrc src{P.seg, P.seg_bytes, d.offset};
     materialise<V>(src, P, sm, c.rows, c.kbytes, c.vbytes, row0, kb0, vb0);
@@ -676,6 +765,8 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
         case 0: hipLaunchKernelGGL(okv_copy_kernel<0>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
         case 1: hipLaunchKernelGGL(okv_copy_kernel<1>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
         case 2: hipLaunchKernelGGL(okv_copy_kernel<2>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
+        case 4: hipLaunchKernelGGL(okv_copy_kernel<4>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
+        case 5: hipLaunchKernelGGL(okv_copy_kernel<5>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
         default: hipLaunchKernelGGL(okv_copy_kernel<3>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P);
       }
     OKV_HIP(hipGetLastError());

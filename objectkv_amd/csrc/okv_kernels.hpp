@@ -14,7 +14,8 @@ namespace okv {
 
 constexpr int kThreads = 256;      // 4 waves per workgroup
 constexpr int kTile = 256;         // blocks per pass-1 workgroup (one lane each)
-constexpr int kRowBatch = 256;     // rows materialised per LDS row-table batch
+constexpr int kRowBatch = 256;     // rows per LDS row-table batch (general path)
+constexpr int kFastRows = 1024;    // max rows of a block on the fast path
 constexpr int kStage = 65536;      // LDS staging capacity for one block (bytes)
 constexpr int kStagePad = 64;      // guard bytes around the staged image
 
@@ -80,6 +81,38 @@ __device__ __forceinline__ uint4 load16_lds(const uint32_t* sw, uint32_t bi) {
   const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
   return make_uint4(funnel(w1, w0, sh), funnel(w2, w1, sh), funnel(w3, w2, sh),
                     funnel(w4, w3, sh));
+}
+
+// 16 bytes starting at LDS byte index bi from two aligned ds_read_b128 (lanes
+// reading consecutive chunks are bank-conflict free) and a byte funnel.
+__device__ __forceinline__ uint4 load16_lds_b128(const uint4* s4, uint32_t bi) {
+  const uint4 x = s4[bi >> 4];
+  const uint4 y = s4[(bi >> 4) + 1];
+  const uint32_t q = (bi >> 2) & 3, r = bi & 3;
+  const uint32_t d0 = q == 0 ? x.x : q == 1 ? x.y : q == 2 ? x.z : x.w;
+  const uint32_t d1 = q == 0 ? x.y : q == 1 ? x.z : q == 2 ? x.w : y.x;
+  const uint32_t d2 = q == 0 ? x.z : q == 1 ? x.w : q == 2 ? y.x : y.y;
+  const uint32_t d3 = q == 0 ? x.w : q == 1 ? y.x : q == 2 ? y.y : y.z;
+  const uint32_t d4 = q == 0 ? y.x : q == 1 ? y.y : q == 2 ? y.z : y.w;
+  return make_uint4(funnel(d1, d0, r), funnel(d2, d1, r), funnel(d3, d2, r), funnel(d4, d3, r));
+}
+
+// Mask of bytes [a, b) (0 <= a <= b <= 16) that fall in dword k of a chunk.
+__device__ __forceinline__ uint32_t byte_mask(int32_t a, int32_t b, int k) {
+  const int32_t lo = min(max(a - 4 * k, 0), 4), hi = min(max(b - 4 * k, 0), 4);
+  const uint32_t mh = hi >= 4 ? 0xffffffffu : ((1u << (8 * hi)) - 1u);
+  const uint32_t ml = lo >= 4 ? 0xffffffffu : ((1u << (8 * lo)) - 1u);
+  return mh & ~ml;
+}
+
+// out with bytes [a, b) replaced by those of v.
+__device__ __forceinline__ uint4 merge_bytes(uint4 out, const uint4& v, int32_t a, int32_t b) {
+  uint32_t m;
+  m = byte_mask(a, b, 0); out.x = (out.x & ~m) | (v.x & m);
+  m = byte_mask(a, b, 1); out.y = (out.y & ~m) | (v.y & m);
+  m = byte_mask(a, b, 2); out.z = (out.z & ~m) | (v.z & m);
+  m = byte_mask(a, b, 3); out.w = (out.w & ~m) | (v.w & m);
+  return out;
 }
 
 // 16 bytes starting at absolute segment position pos (may be < 0 or run past

@@ -144,6 +144,9 @@ def crafted_case():
     # 8: many tiny records (more rows than one row-table batch)
     b = b"".join(rec(bytes([i % 251 + 1]), b"") for i in range(600))
     add(b, 8192, len(b), "600 tiny records")
+    # 8b: more rows than the fast path holds (> 1024): general batched path
+    b = b"".join(rec(bytes([i % 7 + 1]) * (i % 3), bytes([i % 5]) * (i % 4)) for i in range(1500))
+    add(b, 16384, len(b), "1500 records (> fast-path rows)")
     # 9: unaligned block offset (offset % 16 == 3)
     seg.extend(b"\xAA" * 3)
     b = rec(b"unaligned", b"offset!") + rec(b"k2", b"v" * 37)

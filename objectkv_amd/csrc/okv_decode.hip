@@ -2,18 +2,23 @@
 //
 // Replaces the record loop of sst.SegmentReader.ReadBlockWithStat
 // (/root/reference/sst/segment_reader.go:295-355) for many blocks at once.
-// Three launches per call (DESIGN.md "Kernels"):
+// Launches per call (DESIGN.md "Kernels"):
 //   1. okv_count_kernel  -- one lane per block walks the record headers in
-//      HBM, validating exactly what the Go loop validates, and produces per
-//      block (status, rows, key bytes, value bytes, end position); each
-//      256-block tile is exclusive-scanned in the workgroup.
+//      HBM, validating exactly what the Go loop validates; per block it emits
+//      (status, rows, key bytes, value bytes, end position), the positions of
+//      its first kRCap records, and a 256-block exclusive scan.  Blocks with
+//      more rows go on the "big block" list.
 //   2. okv_scan_kernel   -- one workgroup scans the tile totals.
-//   3. okv_copy_kernel   -- one workgroup per block stages the block's bytes
-//      into LDS with coalesced 16-byte loads, re-walks the headers in LDS to
-//      build a row table, writes the SoA row index, and scatters key/value
-//      bytes into packed 16-byte-aligned arenas with dwordx4 stores
-//      (Go's fresh-copy semantics, mustReadBytes :489-512).
-//   (okv_index_kernel replaces 3 for OKV_F_INDEX_ONLY: spans into seg.)
+//   3. okv_gather_kernel -- one workgroup per block: one wave rebuilds the row
+//      table in parallel (recorded positions + header reads + wave scan),
+//      writes the SoA row index, then every lane gathers 16-byte destination
+//      chunks of the packed key/value arenas straight from HBM (two aligned
+//      16-byte loads + byte funnel) and stores them whole (dwordx4).  Chunks
+//      spanning a row boundary are assembled lane-per-row.  Tiny LDS, so
+//      occupancy is set by registers, not by block size.
+//   4. okv_copy_kernel   -- persistent, over the big-block list only: stages
+//      the block in LDS and chases its headers there (rare: > kRCap rows).
+// OKV_F_INDEX_ONLY writes spans into seg instead of arenas (3 + okv_index_kernel).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,7 +39,8 @@ namespace okv {
 __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     const uint8_t* __restrict__ seg, uint64_t seg_bytes, const Desc* __restrict__ descs,
     uint32_t nblk, int comp, BlockCount* __restrict__ cnt, Prefix* __restrict__ lp,
-    Prefix* __restrict__ tile_tot) {
+    Prefix* __restrict__ tile_tot, uint32_t* __restrict__ rec_s, uint32_t* __restrict__ big_list,
+    uint32_t* __restrict__ big_count) {
   const uint32_t tid = threadIdx.x;
   const uint32_t b = blockIdx.x * kTile + tid;
   uint64_t rows = 0, kb = 0, vb = 0, p = 0;
@@ -50,6 +56,7 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     } else {
       const uint64_t len = (comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
       const uint64_t orig = d.original_size;
+      uint32_t* rec = rec_s + uint64_t(b) * kRCap;
       while (p < orig) {  // :340
         if (len - p < 6) { st = OKV_BLK_PANIC; break; }  // u16/u32 reads (:342-345)
         uint32_t kl, vl;
@@ -59,6 +66,7 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
           st = OKV_BLK_PANIC;                // key/value reads (:346-349)
           break;
         }
+        if (rows < kRCap) rec[rows] = uint32_t(p);
         rows++;
         kb += kl;
         vb += vl;
@@ -66,6 +74,8 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
       }
     }
     if (st != OKV_BLK_OK) rows = kb = vb = 0;
+    if (st == OKV_BLK_OK && (rows > kRCap || p >= (uint64_t(1) << 32)))
+      big_list[atomicAdd(big_count, 1u)] = b;  // staged path (okv_copy_kernel)
     BlockCount c;
     c.rows = rows;
     c.kbytes = kb;
@@ -177,9 +187,13 @@ struct CopyParams {
   const Desc* descs;
   uint32_t nblk;
   int comp;
+  int index_only;
   const BlockCount* cnt;
   const Prefix* lp;
   const Prefix* tile_pre;
+  const uint32_t* rec_s;      // [nblk][kRCap] record positions from pass 1
+  const uint32_t* big_list;   // blocks with > kRCap rows (or >= 4 GiB walks)
+  const uint32_t* big_count;
   uint64_t* row_start;
   uint64_t* key_base;
   uint64_t* val_base;
@@ -193,6 +207,164 @@ struct CopyParams {
   uint64_t row_cap, key_cap, val_cap;
 };
 
+// Global row / arena bases of block b and its final status (capacity check).
+struct BlockBase {
+  uint64_t row0, kb0, vb0;
+  int32_t st;
+};
+__device__ __forceinline__ BlockBase block_base(const CopyParams& P, uint32_t b,
+                                                const BlockCount& c) {
+  const Prefix l = P.lp[b];
+  const Prefix t = P.tile_pre[b / kTile];
+  BlockBase r;
+  r.row0 = t.rows + l.rows;
+  r.kb0 = t.kb + l.kb;
+  r.vb0 = t.vb + l.vb;
+  r.st = c.status;
+  if (r.st == OKV_BLK_OK &&
+      (r.row0 + c.rows > P.row_cap ||
+       (!P.index_only && (r.kb0 + round16(c.kbytes) > P.key_cap ||
+                          r.vb0 + round16(c.vbytes) > P.val_cap))))
+    r.st = OKV_BLK_CAPACITY;
+  return r;
+}
+
+// Lanes per row for a region whose rows average `avg` bytes.
+__device__ __forceinline__ uint32_t group_size(uint64_t avg) {
+  const uint64_t chunks = avg / 16 + 2;
+  uint32_t g = 1;
+  while (g < 64 && g < chunks) g <<= 1;
+  return g;
+}
+
+struct GatherSmem {
+  uint32_t rec[kRCap + 1];   // record position within the block
+  uint32_t kpre[kRCap + 1];  // exclusive prefix of key lengths
+  uint32_t vpre[kRCap + 1];  // exclusive prefix of value lengths
+};
+
+// Source position (absolute, may be < 0 for masked bytes) of region byte 0 of
+// row i: region byte x of row i lives at src_base + x.
+template <bool kVal>
+__device__ __forceinline__ int64_t src_base(const GatherSmem& sm, uint64_t off, uint32_t i) {
+  const uint32_t pre = kVal ? sm.vpre[i] : sm.kpre[i];
+  const uint32_t skip = kVal ? sm.kpre[i + 1] - sm.kpre[i] : 0u;
+  return int64_t(off + sm.rec[i] + 6 + skip) - int64_t(pre);
+}
+
+// Chunks lying wholly inside one row: lane groups of G lanes per row.
+template <bool kVal>
+__device__ __forceinline__ void gather_main(const CopyParams& P, const GatherSmem& sm, int rows,
+                                            uint64_t off, uint8_t* __restrict__ arena,
+                                            uint64_t dbase, uint32_t G) {
+  const uint32_t* pre = kVal ? sm.vpre : sm.kpre;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t grp = tid / G, sub = tid % G, ngrp = kThreads / G;
+  for (uint32_t i = grp; i < uint32_t(rows); i += ngrp) {
+    const uint32_t p0 = pre[i], p1 = pre[i + 1];
+    const uint32_t cf = (p0 + 15) >> 4, cl = p1 >> 4;  // 16c >= p0 and 16c + 16 <= p1
+    if (cf >= cl) continue;
+    const int64_t sb = src_base<kVal>(sm, off, i);
+    for (uint32_t c = cf + sub; c < cl; c += G) {
+      const uint4 v = window16(P.seg, P.seg_bytes, sb + int64_t(c) * 16);
+      *reinterpret_cast<uint4*>(arena + dbase + uint64_t(c) * 16) = v;
+    }
+  }
+}
+
+// The chunk holding row i's end when it starts inside row i and spills past
+// it: assembled from rows i, i+1, ... (zero past the region end = padding).
+template <bool kVal>
+__device__ __forceinline__ void gather_tail(const CopyParams& P, const GatherSmem& sm, int rows,
+                                            uint64_t off, uint8_t* __restrict__ arena,
+                                            uint64_t dbase, uint32_t i) {
+  const uint32_t* pre = kVal ? sm.vpre : sm.kpre;
+  const uint32_t p0 = pre[i], p1 = pre[i + 1];
+  if (p1 == p0 || (p1 & 15) == 0) return;
+  const uint32_t cs = p1 & ~15u;
+  if (cs < p0) return;  // owned by the row holding byte cs
+  const uint32_t ce = cs + 16;
+  uint4 out = merge_bytes(make_uint4(0, 0, 0, 0),
+                          window16(P.seg, P.seg_bytes, src_base<kVal>(sm, off, i) + cs), 0,
+                          int32_t(p1 - cs));
+  for (uint32_t j = i + 1; j < uint32_t(rows) && pre[j] < ce; ++j) {
+    const uint32_t q0 = pre[j], q1 = pre[j + 1];
+    if (q1 == q0) continue;
+    const uint4 v = window16(P.seg, P.seg_bytes, src_base<kVal>(sm, off, j) + cs);
+    out = merge_bytes(out, v, int32_t(q0 - cs), int32_t((q1 < ce ? q1 : ce) - cs));
+  }
+  *reinterpret_cast<uint4*>(arena + dbase + cs) = out;
+}
+
+// V selects a diagnostic ablation (tools/ablate.py): 0 row table only,
+// 1 + SoA index, 2 + whole chunks, 3 = the full kernel (the only variant the
+// API uses unless OKV_COPY_VARIANT is set).
+template <int V>
+__global__ __launch_bounds__(kThreads) void okv_gather_kernel(CopyParams P) {
+  __shared__ GatherSmem sm;
+  const uint32_t b = blockIdx.x;
+  const uint32_t tid = threadIdx.x;
+  const BlockCount c = P.cnt[b];
+  const BlockBase B = block_base(P, b, c);
+  if (tid == 0) {
+    P.row_start[b] = B.row0;
+    if (P.key_base) P.key_base[b] = B.kb0;
+    if (P.val_base) P.val_base[b] = B.vb0;
+    P.blk_status[b] = B.st;
+  }
+  if (B.st != OKV_BLK_OK || c.rows == 0 || c.rows > uint64_t(kRCap) ||
+      c.pend >= (uint64_t(1) << 32))
+    return;  // nothing to do, or a big block (okv_copy_kernel)
+  const int rows = int(c.rows);
+  const uint64_t off = P.descs[b].offset;
+  if (tid < 64) {  // row table: lane r holds row r
+    uint32_t rec = 0, kl = 0, vl = 0;
+    if (int(tid) < rows) {
+      rec = P.rec_s[uint64_t(b) * kRCap + tid];
+      header_global(P.seg, off + rec, kl, vl);
+    }
+    const uint32_t ki = wave_incl_scan32(kl, tid), vi = wave_incl_scan32(vl, tid);
+    if (int(tid) < rows) {
+      sm.rec[tid] = rec;
+      sm.kpre[tid] = ki - kl;
+      sm.vpre[tid] = vi - vl;
+      if (int(tid) == rows - 1) {
+        sm.rec[rows] = rec + 6 + kl + vl;
+        sm.kpre[rows] = ki;
+        sm.vpre[rows] = vi;
+      }
+    }
+  }
+  __syncthreads();
+  if (V < 1) return;
+  if (int(tid) < rows) {  // SoA row index
+    const uint64_t g = B.row0 + tid;
+    const uint32_t kl = sm.kpre[tid + 1] - sm.kpre[tid], vl = sm.vpre[tid + 1] - sm.vpre[tid];
+    P.key_len[g] = uint16_t(kl);
+    P.val_len[g] = vl;
+    if (P.index_only) {
+      P.key_off[g] = off + sm.rec[tid] + 6;
+      P.val_off[g] = off + sm.rec[tid] + 6 + kl;
+    } else {
+      P.key_off[g] = B.kb0 + sm.kpre[tid];
+      P.val_off[g] = B.vb0 + sm.vpre[tid];
+    }
+  }
+  if (V < 2 || P.index_only) return;
+  gather_main<false>(P, sm, rows, off, P.key_arena, B.kb0, group_size(c.kbytes / rows));
+  gather_main<true>(P, sm, rows, off, P.val_arena, B.vb0, group_size(c.vbytes / rows));
+  if (V < 3) return;
+  if (int(tid) < 2 * rows) {
+    if (int(tid) < rows)
+      gather_tail<false>(P, sm, rows, off, P.key_arena, B.kb0, tid);
+    else
+      gather_tail<true>(P, sm, rows, off, P.val_arena, B.vb0, tid - rows);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 4 (big blocks only): LDS-staged decode with a serial header chase.
+// ---------------------------------------------------------------------------
 struct SlowRows {               // general path: 64-bit positions, batched rows
   uint64_t rec[kRowBatch];        // record position within the block
   uint64_t kpre[kRowBatch + 1];   // key-byte prefix within the block
@@ -238,13 +410,6 @@ struct GlobalSrc {
   }
 };
 
-// Lanes per row for a region whose rows average `avg` bytes.
-__device__ __forceinline__ uint32_t group_size(uint64_t avg) {
-  const uint64_t chunks = avg / 16 + 2;
-  uint32_t g = 1;
-  while (g < 64 && g < chunks) g <<= 1;
-  return g;
-}
 
 // Copy rows [0, nb) of one region (keys or values) into `arena`:
 //   row i bytes = src[spos_i, spos_i + len_i) -> arena[dbase + pre_i, ...).
@@ -334,7 +499,7 @@ __device__ __forceinline__ void materialise(const Src& src, const CopyParams& P,
 // registers, merging bytes of the following rows when the chunk spills past
 // its row (no partial stores, so neighbouring chunks never race).  The last
 // chunk of a region is zero-filled past the region end (16-byte padding).
-template <bool kVal>
+template <bool kVal, int V = 3>
 __device__ __forceinline__ void copy_region_fast(const uint4* __restrict__ s4, uint32_t bias,
                                                  uint8_t* __restrict__ arena, uint64_t dbase,
                                                  const FastRows& t, int rows, uint32_t G) {
@@ -348,6 +513,10 @@ __device__ __forceinline__ void copy_region_fast(const uint4* __restrict__ s4, u
     const uint32_t si = bias + t.rec[i] + 6 + (kVal ? t.kpre[i + 1] - t.kpre[i] : 0u);
     for (uint32_t c = cfirst + sub; c <= clast; c += G) {
       const uint32_t cs = c << 4, ce = cs + 16;
+      if (V == 6) {  // diagnostic: stores only
+        *reinterpret_cast<uint4*>(arena + dbase + cs) = make_uint4(cs, i, 0, 0);
+        continue;
+      }
       uint4 out = load16_lds_b128(s4, si + (cs - p0));
       if (ce > p1) {  // spills past row i: keep [0, p1-cs), gather the rest
         out = merge_bytes(make_uint4(0, 0, 0, 0), out, 0, int32_t(p1 - cs));
@@ -358,6 +527,10 @@ __device__ __forceinline__ void copy_region_fast(const uint4* __restrict__ s4, u
           const uint4 v = load16_lds_b128(s4, sj - (q0 - cs));
           out = merge_bytes(out, v, int32_t(q0 - cs), int32_t((q1 < ce ? q1 : ce) - cs));
         }
+      }
+      if (V == 7) {  // diagnostic: no stores
+        asm volatile("" ::"v"(out.x), "v"(out.y), "v"(out.z), "v"(out.w));
+        continue;
       }
       *reinterpret_cast<uint4*>(arena + dbase + cs) = out;
     }
@@ -400,98 +573,64 @@ __device__ __forceinline__ void materialise_fast(const CopyParams& P, CopySmem& 
   }
   if (V < 3) return;
   const uint32_t Gk = group_size(kbytes / rows), Gv = group_size(vbytes / rows);
-  copy_region_fast<false>(sm.stage, bias, P.key_arena, kb0, t, rows, Gk);
-  copy_region_fast<true>(sm.stage, bias, P.val_arena, vb0, t, rows, Gv);
+  copy_region_fast<false, V>(sm.stage, bias, P.key_arena, kb0, t, rows, Gk);
+  copy_region_fast<true, V>(sm.stage, bias, P.val_arena, vb0, t, rows, Gv);
 }
 
-// V selects a diagnostic ablation (tools/ablate.py): 0 stage only, 1 + header
-// chase, 2 + SoA index, 3 = the full kernel (the only variant the API uses
-// unless OKV_COPY_VARIANT is set).
-template <int V>
 __global__ __launch_bounds__(kThreads) void okv_copy_kernel(CopyParams P) {
   __shared__ CopySmem sm;
-  const uint32_t b = blockIdx.x;
   const uint32_t tid = threadIdx.x;
-  const BlockCount c = P.cnt[b];
-  const Prefix l = P.lp[b];
-  const Prefix t = P.tile_pre[b / kTile];
-  const uint64_t row0 = t.rows + l.rows, kb0 = t.kb + l.kb, vb0 = t.vb + l.vb;
-  int32_t st = c.status;
-  if (st == OKV_BLK_OK && (row0 + c.rows > P.row_cap || kb0 + round16(c.kbytes) > P.key_cap ||
-                           vb0 + round16(c.vbytes) > P.val_cap))
-    st = OKV_BLK_CAPACITY;
-  if (tid == 0) {
-    P.row_start[b] = row0;
-    if (P.key_base) P.key_base[b] = kb0;
-    if (P.val_base) P.val_base[b] = vb0;
-    P.blk_status[b] = st;
-  }
-  if (st != OKV_BLK_OK || c.rows == 0) return;
-  const Desc d = P.descs[b];
-  if (c.pend <= uint64_t(kStage)) {
-    // stage [offset - shift, offset + pend) with aligned 16-byte loads
-    const uint32_t shift = uint32_t(d.offset & 15);
-    const uint32_t nch = uint32_t((shift + c.pend + 15) / 16);
-    const uint4* g = reinterpret_cast<const uint4*>(P.seg + (d.offset - shift));
-    constexpr int kPer = kStage / 16 / kThreads;  // 16 chunks per lane at 64 KiB
-    const uint32_t rounds = (nch + kThreads - 1) / kThreads;  // workgroup-uniform
-    uint4 v[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      if (k < int(rounds)) {  // uniform branch; lanes past nch re-load the last chunk
-        const uint32_t ci = tid + k * kThreads;
-        v[k] = load_nt16(g + (ci < nch ? ci : nch - 1));
+  const uint32_t nbig = *P.big_count;
+  for (uint32_t k = blockIdx.x; k < nbig; k += gridDim.x) {
+    const uint32_t b = P.big_list[k];
+    const BlockCount c = P.cnt[b];
+    const BlockBase B = block_base(P, b, c);
+    if (B.st != OKV_BLK_OK) continue;  // status written by okv_gather_kernel
+    const Desc d = P.descs[b];
+    if (c.pend <= uint64_t(kStage)) {
+      // stage [offset - shift, offset + pend) with aligned 16-byte loads
+      const uint32_t shift = uint32_t(d.offset & 15);
+      const uint32_t nch = uint32_t((shift + c.pend + 15) / 16);
+      const uint4* g = reinterpret_cast<const uint4*>(P.seg + (d.offset - shift));
+      for (uint32_t ci = tid; ci < nch; ci += kThreads) sm.stage[1 + ci] = load_nt16(g + ci);
+      __syncthreads();
+      if (c.rows <= uint64_t(kFastRows)) {
+        materialise_fast<3>(P, sm, 16u + shift, int(c.rows), c.kbytes, c.vbytes, B.row0, B.kb0,
+                            B.vb0);
+      } else {
+        LdsSrc src{reinterpret_cast<const uint32_t*>(sm.stage), 16u + shift};
+        materialise<3>(src, P, sm, c.rows, c.kbytes, c.vbytes, B.row0, B.kb0, B.vb0);
       }
-    }
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const uint32_t ci = tid + k * kThreads;
-      if (k < int(rounds) && ci < nch) sm.stage[1 + ci] = v[k];
-    }
-    __syncthreads();
-    if (V == 0) {
-      if (tid == 0 && sm.stage[1 + (c.pend & 1023)].x == 0x12345678u) P.blk_status[b] = 99;
-      return;
-    }
-    if (c.rows <= uint64_t(kFastRows)) {
-      materialise_fast<V>(P, sm, 16u + shift, int(c.rows), c.kbytes, c.vbytes, row0, kb0, vb0);
     } else {
-      LdsSrc src{reinterpret_cast<const uint32_t*>(sm.stage), 16u + shift};
-      materialise<V>(src, P, sm, c.rows, c.kbytes, c.vbytes, row0, kb0, vb0);
+      GlobalSrc src{P.seg, P.seg_bytes, d.offset};
+      materialise<3>(src, P, sm, c.rows, c.kbytes, c.vbytes, B.row0, B.kb0, B.vb0);
     }
-  } else {
-    GlobalSrc src{P.seg, P.seg_bytes, d.offset};
-    materialise<V>(src, P, sm, c.rows, c.kbytes, c.vbytes, row0, kb0, vb0);
+    __syncthreads();  // LDS is reused by the next big block
   }
 }
 
 // ---------------------------------------------------------------------------
-// Pass 3 (OKV_F_INDEX_ONLY): spans into seg; one lane per block re-walks the
-// headers in HBM and writes its rows' SoA entries.
+// OKV_F_INDEX_ONLY for big blocks: one lane per block re-walks the headers.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void okv_index_kernel(CopyParams P) {
-  const uint32_t b = blockIdx.x * kThreads + threadIdx.x;
-  if (b >= P.nblk) return;
-  const BlockCount c = P.cnt[b];
-  const Prefix l = P.lp[b];
-  const Prefix t = P.tile_pre[b / kTile];
-  const uint64_t row0 = t.rows + l.rows;
-  int32_t st = c.status;
-  if (st == OKV_BLK_OK && row0 + c.rows > P.row_cap) st = OKV_BLK_CAPACITY;
-  P.row_start[b] = row0;
-  P.blk_status[b] = st;
-  if (st != OKV_BLK_OK) return;
-  const uint64_t off = P.descs[b].offset;
-  uint64_t p = 0;
-  for (uint64_t r = 0; r < c.rows; ++r) {
-    uint32_t kl, vl;
-    header_global(P.seg, off + p, kl, vl);
-    const uint64_t g = row0 + r;
-    P.key_off[g] = off + p + 6;
-    P.key_len[g] = uint16_t(kl);
-    P.val_off[g] = off + p + 6 + kl;
-    P.val_len[g] = vl;
-    p += 6 + uint64_t(kl) + uint64_t(vl);
+  const uint32_t nbig = *P.big_count;
+  for (uint32_t k = blockIdx.x * kThreads + threadIdx.x; k < nbig; k += gridDim.x * kThreads) {
+    const uint32_t b = P.big_list[k];
+    const BlockCount c = P.cnt[b];
+    const BlockBase B = block_base(P, b, c);
+    if (B.st != OKV_BLK_OK) continue;
+    const uint64_t off = P.descs[b].offset;
+    uint64_t p = 0;
+    for (uint64_t r = 0; r < c.rows; ++r) {
+      uint32_t kl, vl;
+      header_global(P.seg, off + p, kl, vl);
+      const uint64_t g = B.row0 + r;
+      P.key_off[g] = off + p + 6;
+      P.key_len[g] = uint16_t(kl);
+      P.val_off[g] = off + p + 6 + kl;
+      P.val_len[g] = vl;
+      p += 6 + uint64_t(kl) + uint64_t(vl);
+    }
   }
 }
 
@@ -606,6 +745,8 @@ struct okv_ctx {
   Prefix* d_lp = nullptr;
   Prefix* d_tile_tot = nullptr;
   Prefix* d_tile_pre = nullptr;
+  uint32_t* d_rec = nullptr;       // [nblk][kRCap] record positions (pass 1)
+  uint32_t* d_big = nullptr;       // big-block list + its counter (d_big[nblk])
   size_t cap_blocks = 0;
   Totals* d_tot = nullptr;
   Totals* h_tot = nullptr;  // pinned
@@ -670,7 +811,11 @@ int ensure_blocks(okv_ctx* ctx, uint32_t nblk) {
     (void)hipFree(ctx->d_lp);
     (void)hipFree(ctx->d_tile_tot);
     (void)hipFree(ctx->d_tile_pre);
+    (void)hipFree(ctx->d_rec);
+    (void)hipFree(ctx->d_big);
   }
+  OKV_HIP(hipMalloc(&ctx->d_rec, n * kRCap * sizeof(uint32_t)));
+  OKV_HIP(hipMalloc(&ctx->d_big, (n + 1) * sizeof(uint32_t)));
   OKV_HIP(hipMalloc(&ctx->d_cnt, n * sizeof(BlockCount)));
   OKV_HIP(hipMalloc(&ctx->d_lp, n * sizeof(Prefix)));
   OKV_HIP(hipMalloc(&ctx->d_tile_tot, (ntiles + 1) * sizeof(Prefix)));
@@ -706,9 +851,11 @@ int launch_plan(okv_ctx* ctx, const uint8_t* d_seg, uint64_t seg_bytes, const De
   if (rc) return rc;
   const uint32_t ntiles = (nblk + kTile - 1) / kTile;
   if (timed) prof_mark(ctx, 0);
+  OKV_HIP(hipMemsetAsync(ctx->d_big + nblk, 0, sizeof(uint32_t), ctx->stream));
   if (ntiles)
     hipLaunchKernelGGL(okv_count_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, d_seg,
-                       seg_bytes, d_desc, nblk, comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot);
+                       seg_bytes, d_desc, nblk, comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
+                       ctx->d_rec, ctx->d_big, ctx->d_big + nblk);
   if (timed) prof_mark(ctx, 1);
   hipLaunchKernelGGL(okv_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_tile_tot,
                      ntiles, ctx->d_tile_pre, ctx->d_tot, d_row_start, nblk);
@@ -740,6 +887,10 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   P.descs = descs;
   P.nblk = nblk;
   P.comp = comp;
+  P.index_only = index_only ? 1 : 0;
+  P.rec_s = ctx->d_rec;
+  P.big_list = ctx->d_big;
+  P.big_count = ctx->d_big + nblk;
   P.cnt = ctx->d_cnt;
   P.lp = ctx->d_lp;
   P.tile_pre = ctx->d_tile_pre;
@@ -757,18 +908,19 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   P.key_cap = index_only ? 0 : o->key_cap;
   P.val_cap = index_only ? 0 : o->val_cap;
   if (nblk) {
+    const dim3 g(nblk), t(kThreads);
+    switch (ctx->variant) {  // diagnostic ablations only; 3 is the product kernel
+      case 0: hipLaunchKernelGGL(okv_gather_kernel<0>, g, t, 0, ctx->stream, P); break;
+      case 1: hipLaunchKernelGGL(okv_gather_kernel<1>, g, t, 0, ctx->stream, P); break;
+      case 2: hipLaunchKernelGGL(okv_gather_kernel<2>, g, t, 0, ctx->stream, P); break;
+      default: hipLaunchKernelGGL(okv_gather_kernel<3>, g, t, 0, ctx->stream, P);
+    }
+    const uint32_t nbig_grid = std::min<uint32_t>(nblk, 512);
     if (index_only)
-      hipLaunchKernelGGL(okv_index_kernel, dim3((nblk + kThreads - 1) / kThreads),
+      hipLaunchKernelGGL(okv_index_kernel, dim3((nbig_grid + kThreads - 1) / kThreads),
                          dim3(kThreads), 0, ctx->stream, P);
     else
-      switch (ctx->variant) {
-        case 0: hipLaunchKernelGGL(okv_copy_kernel<0>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
-        case 1: hipLaunchKernelGGL(okv_copy_kernel<1>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
-        case 2: hipLaunchKernelGGL(okv_copy_kernel<2>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
-        case 4: hipLaunchKernelGGL(okv_copy_kernel<4>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
-        case 5: hipLaunchKernelGGL(okv_copy_kernel<5>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P); break;
-        default: hipLaunchKernelGGL(okv_copy_kernel<3>, dim3(nblk), dim3(kThreads), 0, ctx->stream, P);
-      }
+      hipLaunchKernelGGL(okv_copy_kernel, dim3(nbig_grid), dim3(kThreads), 0, ctx->stream, P);
     OKV_HIP(hipGetLastError());
   }
   prof_mark(ctx, 3);
@@ -911,6 +1063,8 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->d_lp);
   (void)hipFree(ctx->d_tile_tot);
   (void)hipFree(ctx->d_tile_pre);
+  (void)hipFree(ctx->d_rec);
+  (void)hipFree(ctx->d_big);
   (void)hipFree(ctx->d_tot);
   if (ctx->h_tot) (void)hipHostFree(ctx->h_tot);
   (void)hipFree(ctx->d_seg);

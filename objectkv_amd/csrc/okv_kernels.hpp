@@ -15,7 +15,8 @@ namespace okv {
 constexpr int kThreads = 256;      // 4 waves per workgroup
 constexpr int kTile = 256;         // blocks per pass-1 workgroup (one lane each)
 constexpr int kRowBatch = 256;     // rows per LDS row-table batch (general path)
-constexpr int kFastRows = 1024;    // max rows of a block on the fast path
+constexpr int kFastRows = 1024;    // max rows of a staged block on its fast path
+constexpr int kRCap = 64;          // record positions pass 1 keeps per block
 constexpr int kStage = 65536;      // LDS staging capacity for one block (bytes)
 constexpr int kStagePad = 64;      // guard bytes around the staged image
 
@@ -83,18 +84,30 @@ __device__ __forceinline__ uint4 load16_lds(const uint32_t* sw, uint32_t bi) {
                     funnel(w4, w3, sh));
 }
 
-// 16 bytes starting at LDS byte index bi from two aligned ds_read_b128 (lanes
-// reading consecutive chunks are bank-conflict free) and a byte funnel.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Branch-free bit select: m ? a : b per bit (one v_bfi_b32).  Plain ternary
+// chains on runtime indices compile to exec-mask branches on gfx950.
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) {
+  return (a & m) | (b & ~m);
+}
+
+// Bytes [s, s+16) of the 32-byte window (x, y), s in 0..15.
+__device__ __forceinline__ uint4 funnel32(const uint4& x, const uint4& y, uint32_t s) {
+  const uint32_t m8 = 0u - ((s >> 3) & 1u), m4 = 0u - ((s >> 2) & 1u), r = s & 3u;
+  const uint32_t a0 = bsel(m8, x.z, x.x), a1 = bsel(m8, x.w, x.y), a2 = bsel(m8, y.x, x.z),
+                 a3 = bsel(m8, y.y, x.w), a4 = bsel(m8, y.z, y.x), a5 = bsel(m8, y.w, y.y);
+  const uint32_t b0 = bsel(m4, a1, a0), b1 = bsel(m4, a2, a1), b2 = bsel(m4, a3, a2),
+                 b3 = bsel(m4, a4, a3), b4 = bsel(m4, a5, a4);
+  return make_uint4(funnel(b1, b0, r), funnel(b2, b1, r), funnel(b3, b2, r), funnel(b4, b3, r));
+}
+
+// 16 bytes starting at LDS byte index bi (relative to s4): two aligned
+// 16-byte reads + the branch-free funnel.
 __device__ __forceinline__ uint4 load16_lds_b128(const uint4* s4, uint32_t bi) {
   const uint4 x = s4[bi >> 4];
   const uint4 y = s4[(bi >> 4) + 1];
-  const uint32_t q = (bi >> 2) & 3, r = bi & 3;
-  const uint32_t d0 = q == 0 ? x.x : q == 1 ? x.y : q == 2 ? x.z : x.w;
-  const uint32_t d1 = q == 0 ? x.y : q == 1 ? x.z : q == 2 ? x.w : y.x;
-  const uint32_t d2 = q == 0 ? x.z : q == 1 ? x.w : q == 2 ? y.x : y.y;
-  const uint32_t d3 = q == 0 ? x.w : q == 1 ? y.x : q == 2 ? y.y : y.z;
-  const uint32_t d4 = q == 0 ? y.x : q == 1 ? y.y : q == 2 ? y.z : y.w;
-  return make_uint4(funnel(d1, d0, r), funnel(d2, d1, r), funnel(d3, d2, r), funnel(d4, d3, r));
+  return funnel32(x, y, bi & 15u);
 }
 
 // Mask of bytes [a, b) (0 <= a <= b <= 16) that fall in dword k of a chunk.
@@ -134,8 +147,6 @@ __device__ __forceinline__ uint4 load16_global(const uint8_t* __restrict__ seg, 
                     funnel(w[4], w[3], sh));
 }
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
 // 16-byte streaming load (nontemporal: the block is read once).
 __device__ __forceinline__ uint4 load_nt16(const uint4* p) {
   const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
@@ -144,10 +155,7 @@ __device__ __forceinline__ uint4 load_nt16(const uint4* p) {
 
 // Dword of v starting at byte o (0..15) without runtime-indexed arrays.
 __device__ __forceinline__ uint32_t dword_at(const uint4& v, uint32_t o) {
-  const uint32_t wi = o >> 2, sh = o & 3;
-  const uint32_t a = wi == 0 ? v.x : wi == 1 ? v.y : wi == 2 ? v.z : v.w;
-  const uint32_t b = wi == 0 ? v.y : wi == 1 ? v.z : wi == 2 ? v.w : 0u;
-  return funnel(b, a, sh);
+  return funnel32(v, make_uint4(0, 0, 0, 0), o).x;
 }
 
 // Store bytes [lo, hi) of the 16-byte vector v to the 16-byte aligned dst,
@@ -172,6 +180,32 @@ __device__ __forceinline__ void store_partial(uint8_t* dst, const uint4& v, uint
       o += 1;
     }
   }
+}
+
+// 16 bytes of seg starting at absolute position x from two aligned 16-byte
+// loads and the byte funnel.  16-byte lines wholly outside [0, seg_bytes)
+// are not loaded and read as zero (only masked bytes ever come from them).
+__device__ __forceinline__ uint4 window16(const uint8_t* __restrict__ seg, uint64_t seg_bytes,
+                                         int64_t x) {
+  const int64_t a = x & ~int64_t(15);
+  const uint32_t s = uint32_t(x & 15);
+  const bool v0 = a >= 0 && uint64_t(a) < seg_bytes;
+  const bool v1 = s != 0 && a + 16 >= 0 && uint64_t(a + 16) < seg_bytes;
+  const uint4 lo = *reinterpret_cast<const uint4*>(seg + (v0 ? a : 0));
+  const uint4 hi = *reinterpret_cast<const uint4*>(seg + (v1 ? a + 16 : 0));
+  const uint32_t m0 = 0u - uint32_t(v0), m1 = 0u - uint32_t(v1);
+  return funnel32(make_uint4(lo.x & m0, lo.y & m0, lo.z & m0, lo.w & m0),
+                  make_uint4(hi.x & m1, hi.y & m1, hi.z & m1, hi.w & m1), s);
+}
+
+// Wave64 inclusive scan of a 32-bit value.
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
 }
 
 // Wave64 inclusive scan of a 64-bit value (DPP-free shuffle form).

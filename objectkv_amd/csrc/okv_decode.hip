@@ -57,20 +57,28 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
       const uint64_t len = (comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
       const uint64_t orig = d.original_size;
       uint32_t* rec = rec_s + uint64_t(b) * kRCap;
+      // Software-pipelined walk: the next header's loads are issued before
+      // this record's position is stored, so waiting for them never waits
+      // for the (older) scattered store (vmcnt counts loads and stores).
+      uint32_t kl = 0, vl = 0;
+      if (p < orig && len >= 6) header_global(seg, d.offset, kl, vl);
       while (p < orig) {  // :340
         if (len - p < 6) { st = OKV_BLK_PANIC; break; }  // u16/u32 reads (:342-345)
-        uint32_t kl, vl;
-        header_global(seg, d.offset + p, kl, vl);
         const uint64_t room = len - p - 6;
         if (kl > room || vl > room - kl) {  // zero-length reads always succeed (:490-493)
           st = OKV_BLK_PANIC;                // key/value reads (:346-349)
           break;
         }
+        const uint64_t next = p + 6 + uint64_t(kl) + uint64_t(vl);
+        uint32_t nkl = 0, nvl = 0;
+        if (next < orig && len - next >= 6) header_global(seg, d.offset + next, nkl, nvl);
         if (rows < kRCap) rec[rows] = uint32_t(p);
         rows++;
         kb += kl;
         vb += vl;
-        p += 6 + uint64_t(kl) + uint64_t(vl);
+        p = next;
+        kl = nkl;
+        vl = nvl;
       }
     }
     if (st != OKV_BLK_OK) rows = kb = vb = 0;
@@ -239,70 +247,110 @@ __device__ __forceinline__ uint32_t group_size(uint64_t avg) {
 
 struct GatherSmem {
   uint32_t rec[kRCap + 1];   // record position within the block
-  uint32_t kpre[kRCap + 1];  // exclusive prefix of key lengths
+  uint32_t kpre[kRCap + 1];  // exclusive prefix of key lengths (kpre[rows] = total)
   uint32_t vpre[kRCap + 1];  // exclusive prefix of value lengths
+  uint32_t ksb[kRCap];       // source of key-region byte x of row r = off + ksb[r] + x
+  uint32_t vsb[kRCap];       // likewise for values
 };
 
-// Source position (absolute, may be < 0 for masked bytes) of region byte 0 of
-// row i: region byte x of row i lives at src_base + x.
-template <bool kVal>
-__device__ __forceinline__ int64_t src_base(const GatherSmem& sm, uint64_t off, uint32_t i) {
-  const uint32_t pre = kVal ? sm.vpre[i] : sm.kpre[i];
-  const uint32_t skip = kVal ? sm.kpre[i + 1] - sm.kpre[i] : 0u;
-  return int64_t(off + sm.rec[i] + 6 + skip) - int64_t(pre);
-}
-
-// Chunks lying wholly inside one row: lane groups of G lanes per row.
-template <bool kVal>
-__device__ __forceinline__ void gather_main(const CopyParams& P, const GatherSmem& sm, int rows,
-                                            uint64_t off, uint8_t* __restrict__ arena,
-                                            uint64_t dbase, uint32_t G) {
+// Gather one arena region (keys or values) of a block.  Each wave streams
+// contiguous 1 KiB destination tiles: lane l of tile t writes chunk 64t + l
+// (16 bytes, dwordx4), gathered from the source with two aligned 16-byte
+// loads + byte funnel (window16).  The row holding the chunk's first byte is
+// found by binary search on the lane's first chunk and by linear advance
+// after (chunks only move forward).  A chunk that spills past its row is
+// completed in registers from the following rows; past the region end it is
+// zero (the 16-byte padding).  kU tiles per iteration keep kU windows in
+// flight per lane.
+template <bool kVal, uint32_t kU, bool kShfl>
+__device__ __forceinline__ void gather_region(const CopyParams& P, const GatherSmem& sm,
+                                              int rows, uint64_t off, uint8_t* __restrict__ arena,
+                                              uint64_t dbase) {
   const uint32_t* pre = kVal ? sm.vpre : sm.kpre;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t grp = tid / G, sub = tid % G, ngrp = kThreads / G;
-  for (uint32_t i = grp; i < uint32_t(rows); i += ngrp) {
-    const uint32_t p0 = pre[i], p1 = pre[i + 1];
-    const uint32_t cf = (p0 + 15) >> 4, cl = p1 >> 4;  // 16c >= p0 and 16c + 16 <= p1
-    if (cf >= cl) continue;
-    const int64_t sb = src_base<kVal>(sm, off, i);
-    for (uint32_t c = cf + sub; c < cl; c += G) {
-      const uint4 v = window16(P.seg, P.seg_bytes, sb + int64_t(c) * 16);
-      *reinterpret_cast<uint4*>(arena + dbase + uint64_t(c) * 16) = v;
+  const uint32_t* sb = kVal ? sm.vsb : sm.ksb;
+  const uint32_t total = pre[rows];
+  const uint32_t N = (total + 15) >> 4;  // chunks, including the padded tail
+  const uint32_t T = (N + 63) >> 6;      // 1 KiB tiles
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t nw = kThreads / 64;
+  const uint32_t t0 = uint32_t(uint64_t(T) * wave / nw), t1 = uint32_t(uint64_t(T) * (wave + 1) / nw);
+  const uint32_t last = uint32_t(rows) - 1;
+  uint32_t r = 0;
+  bool searched = false;
+  for (uint32_t t = t0; t < t1; t += kU) {
+    uint4 v[kU], hi2[kU];
+    uint32_t rr[kU], shv[kU];
+    bool need2[kU];
+    // phase 1: rows and addresses; issue every load before any data is used.
+    // One aligned 16-byte load per lane; the following 16 bytes come from the
+    // neighbour lane when its line is the next one (same row), otherwise from
+    // a second load issued only on the lanes that need it.
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t c = (t + u) * 64 + lane;
+      const bool ok = (t + u) < t1 && c < N;
+      const uint32_t x = (ok ? c : (t0 * 64 + lane < N ? t0 * 64 + lane : 0)) << 4;
+      if (!searched) {  // binary search: r = #{k in [1, rows] : pre[k] <= x}
+        uint32_t pos = 0;
+#pragma unroll
+        for (uint32_t st = 64; st; st >>= 1) {
+          const uint32_t j = pos + st;
+          if (j <= last && pre[j] <= x) pos = j;
+        }
+        r = pos;
+        searched = true;
+      } else {
+        while (r < last && pre[r + 1] <= x) ++r;
+      }
+      rr[u] = r;
+      const uint64_t src = off + sb[r] + x;
+      if (!kShfl) {  // two aligned 16-byte loads + funnel
+        v[u] = window16(P.seg, P.seg_bytes, int64_t(src));
+        continue;
+      }
+      const uint64_t a = src & ~uint64_t(15);
+      shv[u] = uint32_t(src & 15);
+      const uint32_t na = __shfl_down(uint32_t(a), 1, 64);
+      need2[u] = shv[u] != 0 && !(lane != 63 && na == uint32_t(a) + 16u);
+      v[u] = *reinterpret_cast<const uint4*>(P.seg + a);
+      hi2[u] = make_uint4(0, 0, 0, 0);
+      if (need2[u] && a + 16 < P.seg_bytes) hi2[u] = *reinterpret_cast<const uint4*>(P.seg + a + 16);
+    }
+    // phase 2: neighbour exchange and byte funnel
+#pragma unroll
+    for (uint32_t u = 0; u < kU && kShfl; ++u) {
+      uint4 hi;
+      hi.x = __shfl_down(v[u].x, 1, 64);
+      hi.y = __shfl_down(v[u].y, 1, 64);
+      hi.z = __shfl_down(v[u].z, 1, 64);
+      hi.w = __shfl_down(v[u].w, 1, 64);
+      if (need2[u]) hi = hi2[u];
+      v[u] = funnel32(v[u], hi, shv[u]);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t c = (t + u) * 64 + lane;
+      if ((t + u) < t1 && c < N) {
+        const uint32_t x = c << 4, xe = x + 16;
+        uint4 out = v[u];
+        const uint32_t ri = rr[u];
+        if (xe > pre[ri + 1]) {  // spills past row ri (or past the region end)
+          out = merge_bytes(make_uint4(0, 0, 0, 0), out, 0, int32_t(pre[ri + 1] - x));
+          for (uint32_t j = ri + 1; j <= last && pre[j] < xe; ++j) {
+            const uint32_t q0 = pre[j], q1 = pre[j + 1];
+            if (q1 == q0) continue;
+            const uint4 w = window16(P.seg, P.seg_bytes, int64_t(off + sb[j]) + int64_t(x));
+            out = merge_bytes(out, w, int32_t(q0 - x), int32_t((q1 < xe ? q1 : xe) - x));
+          }
+        }
+        *reinterpret_cast<uint4*>(arena + dbase + uint64_t(x)) = out;
+      }
     }
   }
 }
 
-// The chunk holding row i's end when it starts inside row i and spills past
-// it: assembled from rows i, i+1, ... (zero past the region end = padding).
-template <bool kVal>
-__device__ __forceinline__ void gather_tail(const CopyParams& P, const GatherSmem& sm, int rows,
-                                            uint64_t off, uint8_t* __restrict__ arena,
-                                            uint64_t dbase, uint32_t i) {
-  const uint32_t* pre = kVal ? sm.vpre : sm.kpre;
-  const uint32_t p0 = pre[i], p1 = pre[i + 1];
-  if (p1 == p0 || (p1 & 15) == 0) return;
-  const uint32_t cs = p1 & ~15u;
-  if (cs < p0) return;  // owned by the row holding byte cs
-  const uint32_t ce = cs + 16;
-  uint4 out = merge_bytes(make_uint4(0, 0, 0, 0),
-                          window16(P.seg, P.seg_bytes, src_base<kVal>(sm, off, i) + cs), 0,
-                          int32_t(p1 - cs));
-  for (uint32_t j = i + 1; j < uint32_t(rows) && pre[j] < ce; ++j) {
-    const uint32_t q0 = pre[j], q1 = pre[j + 1];
-    if (q1 == q0) continue;
-    const uint4 v = window16(P.seg, P.seg_bytes, src_base<kVal>(sm, off, j) + cs);
-    out = merge_bytes(out, v, int32_t(q0 - cs), int32_t((q1 < ce ? q1 : ce) - cs));
-  }
-  *reinterpret_cast<uint4*>(arena + dbase + cs) = out;
-}
-
-// V selects a diagnostic ablation (tools/ablate.py): 0 row table only,
-// 1 + SoA index, 2 + whole chunks, 3 = the full kernel (the only variant the
-// API uses unless OKV_COPY_VARIANT is set).
 template <int V>
-__global__ __launch_bounds__(kThreads) void okv_gather_kernel(CopyParams P) {
-  __shared__ GatherSmem sm;
-  const uint32_t b = blockIdx.x;
+__device__ __forceinline__ void gather_block(const CopyParams& P, GatherSmem& sm, uint32_t b) {
   const uint32_t tid = threadIdx.x;
   const BlockCount c = P.cnt[b];
   const BlockBase B = block_base(P, b, c);
@@ -328,6 +376,8 @@ __global__ __launch_bounds__(kThreads) void okv_gather_kernel(CopyParams P) {
       sm.rec[tid] = rec;
       sm.kpre[tid] = ki - kl;
       sm.vpre[tid] = vi - vl;
+      sm.ksb[tid] = rec + 6 - (ki - kl);       // >= 0: earlier keys precede rec
+      sm.vsb[tid] = rec + 6 + kl - (vi - vl);  // >= 0: earlier values precede rec
       if (int(tid) == rows - 1) {
         sm.rec[rows] = rec + 6 + kl + vl;
         sm.kpre[rows] = ki;
@@ -351,14 +401,23 @@ __global__ __launch_bounds__(kThreads) void okv_gather_kernel(CopyParams P) {
     }
   }
   if (V < 2 || P.index_only) return;
-  gather_main<false>(P, sm, rows, off, P.key_arena, B.kb0, group_size(c.kbytes / rows));
-  gather_main<true>(P, sm, rows, off, P.val_arena, B.vb0, group_size(c.vbytes / rows));
-  if (V < 3) return;
-  if (int(tid) < 2 * rows) {
-    if (int(tid) < rows)
-      gather_tail<false>(P, sm, rows, off, P.key_arena, B.kb0, tid);
-    else
-      gather_tail<true>(P, sm, rows, off, P.val_arena, B.vb0, tid - rows);
+  // diagnostic sweep: 3 = window loads x4 (product), 5 = shuffle x2, 6 = shuffle x4
+  constexpr uint32_t kU = V == 5 ? 2 : 4;
+  constexpr bool kShfl = V == 5 || V == 6;
+  gather_region<false, kU, kShfl>(P, sm, rows, off, P.key_arena, B.kb0);
+  gather_region<true, kU, kShfl>(P, sm, rows, off, P.val_arena, B.vb0);
+}
+
+// V selects a diagnostic ablation (tools/ablate.py): 0 row table only,
+// 1 + SoA index, >= 2 the full kernel (the only variant the API uses unless
+// OKV_COPY_VARIANT is set).
+// Grid: one workgroup per block, or a persistent grid striding over blocks.
+template <int V>
+__global__ __launch_bounds__(kThreads) void okv_gather_kernel(CopyParams P) {
+  __shared__ GatherSmem sm;
+  for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
+    gather_block<V>(P, sm, b);
+    if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
   }
 }
 
@@ -761,6 +820,7 @@ struct okv_ctx {
   size_t cap_hash = 0;
   // per-pass event timing (okv_profile)
   int variant = 3;  // diagnostic ablation selector (OKV_COPY_VARIANT)
+  uint32_t gather_grid = 0;  // 0: one workgroup per block; else persistent grid size
   bool prof = false;
   std::vector<hipEvent_t> ev;  // 4 per timed call
   size_t ev_used = 0;
@@ -908,11 +968,13 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   P.key_cap = index_only ? 0 : o->key_cap;
   P.val_cap = index_only ? 0 : o->val_cap;
   if (nblk) {
-    const dim3 g(nblk), t(kThreads);
+    const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk),
+        t(kThreads);
     switch (ctx->variant) {  // diagnostic ablations only; 3 is the product kernel
       case 0: hipLaunchKernelGGL(okv_gather_kernel<0>, g, t, 0, ctx->stream, P); break;
       case 1: hipLaunchKernelGGL(okv_gather_kernel<1>, g, t, 0, ctx->stream, P); break;
-      case 2: hipLaunchKernelGGL(okv_gather_kernel<2>, g, t, 0, ctx->stream, P); break;
+      case 5: hipLaunchKernelGGL(okv_gather_kernel<5>, g, t, 0, ctx->stream, P); break;
+      case 6: hipLaunchKernelGGL(okv_gather_kernel<6>, g, t, 0, ctx->stream, P); break;
       default: hipLaunchKernelGGL(okv_gather_kernel<3>, g, t, 0, ctx->stream, P);
     }
     const uint32_t nbig_grid = std::min<uint32_t>(nblk, 512);
@@ -1036,6 +1098,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   okv_ctx* ctx = new okv_ctx();
   ctx->device = device;
   if (const char* v = getenv("OKV_COPY_VARIANT")) ctx->variant = atoi(v);
+  if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
   if (stream) {
     ctx->stream = static_cast<hipStream_t>(stream);
   } else {

@@ -153,6 +153,16 @@ __device__ __forceinline__ uint4 load_nt16(const uint4* p) {
   return make_uint4(t.x, t.y, t.z, t.w);
 }
 
+// 16-byte streaming store (nontemporal).
+__device__ __forceinline__ void store_nt16(uint4* p, const uint4& v) {
+  u32x4 t;
+  t.x = v.x;
+  t.y = v.y;
+  t.z = v.z;
+  t.w = v.w;
+  __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(p));
+}
+
 // Dword of v starting at byte o (0..15) without runtime-indexed arrays.
 __device__ __forceinline__ uint32_t dword_at(const uint4& v, uint32_t o) {
   return funnel32(v, make_uint4(0, 0, 0, 0), o).x;

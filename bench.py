@@ -228,8 +228,8 @@ def main():
                       "copy": round(copy_ms, 4)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": "okv_copy_kernel" if not index_only
-                     else "okv_index_kernel", "algorithmic_bytes_per_launch": int(alg)},
+                     "traffic": traffic, "kernel": "okv_gather_kernel" if not index_only
+                     else "okv_gather_kernel (index)", "algorithmic_bytes_per_launch": int(alg)},
         "cpu_baseline": cpu,
     }
     if e2e:

@@ -57,28 +57,22 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
       const uint64_t len = (comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
       const uint64_t orig = d.original_size;
       uint32_t* rec = rec_s + uint64_t(b) * kRCap;
-      // Software-pipelined walk: the next header's loads are issued before
-      // this record's position is stored, so waiting for them never waits
-      // for the (older) scattered store (vmcnt counts loads and stores).
-      uint32_t kl = 0, vl = 0;
-      if (p < orig && len >= 6) header_global(seg, d.offset, kl, vl);
+      // The walk is a dependent chain (record i+1 starts where i ends), so
+      // this kernel is bound by HBM latency x the longest block's row count.
       while (p < orig) {  // :340
         if (len - p < 6) { st = OKV_BLK_PANIC; break; }  // u16/u32 reads (:342-345)
+        uint32_t kl, vl;
+        header_global(seg, d.offset + p, kl, vl);
         const uint64_t room = len - p - 6;
         if (kl > room || vl > room - kl) {  // zero-length reads always succeed (:490-493)
           st = OKV_BLK_PANIC;                // key/value reads (:346-349)
           break;
         }
-        const uint64_t next = p + 6 + uint64_t(kl) + uint64_t(vl);
-        uint32_t nkl = 0, nvl = 0;
-        if (next < orig && len - next >= 6) header_global(seg, d.offset + next, nkl, nvl);
         if (rows < kRCap) rec[rows] = uint32_t(p);
         rows++;
         kb += kl;
         vb += vl;
-        p = next;
-        kl = nkl;
-        vl = nvl;
+        p += 6 + uint64_t(kl) + uint64_t(vl);
       }
     }
     if (st != OKV_BLK_OK) rows = kb = vb = 0;

@@ -43,7 +43,12 @@ extern "C" {
 #define OKV_R_EOF (-302)             /* io.EOF from RowIter.Next */
 #define OKV_R_CLOSED (-303)          /* ErrClosed          segment_row_iter.go:27 */
 #define OKV_R_ALREADY_CLOSED (-304)  /* ErrAlreadyClosed   segment_reader.go:478 */
-#define OKV_R_BLOCK (-305)           /* block decode error / panic (see okv_reader_last_block_status) */
+#define OKV_R_BLOCK_EOF (-305)       /* ReadBlockWithStat: reader.Read error (:310-313) */
+#define OKV_R_BLOCK_SHORT (-306)     /* ReadBlockWithStat: ErrUnexpectedBytesRead (:314-316) */
+#define OKV_R_PANIC (-307)           /* a Go panic: mustReadBytes (:506-512) or rows[0] of an
+                                        empty block (segment_row_iter.go:95, :147) */
+#define OKV_R_UNSUPPORTED (-308)     /* zstd block (device zstd not implemented yet) */
+#define OKV_R_GPU (-309)             /* the GPU decode itself failed (okv_last_error) */
 
 /* ---- SegmentWriter ------------------------------------------------------- */
 typedef struct okv_writer okv_writer;
@@ -78,6 +83,44 @@ const uint8_t *okv_meta_last_key(const okv_meta *m, uint64_t *len);
 int okv_meta_block(const okv_meta *m, uint64_t i, okv_block_desc *desc, uint64_t *hash,
                    const uint8_t **first_key, uint64_t *first_key_len);
 void okv_meta_free(okv_meta *m);
+
+/* ---- SegmentReader / RowIter over the GPU decode -------------------------- */
+/* A row as Go's KVPair (segment_reader.go:285-288): NULL pointer = nil slice.
+ * Pointers stay valid until okv_reader_free. */
+typedef struct okv_row {
+  const uint8_t *key;
+  uint64_t key_len;
+  const uint8_t *val;
+  uint64_t val_len;
+} okv_row;
+
+typedef struct okv_reader okv_reader;
+typedef struct okv_iter okv_iter;
+
+/* NewSegmentReader (segment_reader.go:65-72) over `len` bytes (what the
+ * io.ReadSeeker holds; copied) with the file length `file_bytes`.  Block
+ * reads decode the whole index in one batched GPU call on `ctx` the first
+ * time any block is needed; rows are then served from that decode. */
+okv_reader *okv_reader_open(okv_ctx *ctx, const uint8_t *data, uint64_t len, int64_t file_bytes);
+int okv_reader_fetch_metadata(okv_reader *r);                                  /* :91-141 */
+int okv_reader_load_metadata(okv_reader *r, const uint8_t *meta, uint64_t len); /* :147 + :75 */
+int okv_reader_num_blocks(okv_reader *r, uint64_t *n); /* btree entries (unique first keys) */
+/* ReadBlockWithStat on the i-th btree entry in ascending FirstKey order (:295-355).
+ * *rows points to n rows (valid until free). */
+int okv_reader_read_block(okv_reader *r, uint64_t i, const okv_row **rows, uint64_t *n);
+int okv_reader_get_row(okv_reader *r, const uint8_t *key, size_t klen, okv_row *out); /* :362 */
+/* GetRange [start, end) (:410-475); an empty start is UnboundStart, end == {0xff} UnboundEnd.
+ * Go ranges a map over the candidate blocks; this returns them in ascending FirstKey order. */
+int okv_reader_get_range(okv_reader *r, const uint8_t *start, size_t slen, const uint8_t *end,
+                         size_t elen, const okv_row **rows, uint64_t *n);
+int okv_reader_close(okv_reader *r); /* :481-487 (OKV_R_ALREADY_CLOSED the second time) */
+void okv_reader_free(okv_reader *r);
+
+/* RowIter (segment_row_iter.go:11-212); direction 0 ascending, 1 descending. */
+okv_iter *okv_reader_row_iter(okv_reader *r, int direction);
+int okv_iter_next(okv_iter *it, okv_row *out);                     /* OKV_R_EOF at the end */
+int okv_iter_seek(okv_iter *it, const uint8_t *key, size_t klen); /* empty = UnboundStart */
+void okv_iter_free(okv_iter *it);
 
 /* ---- synthetic segments (bench / tests) ---------------------------------- */
 #define OKV_SYNTH_FIXED 0 /* C1/C2: 16 B big-endian index key, 64 B splitmix64(seed) value */

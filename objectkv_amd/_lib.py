@@ -30,7 +30,16 @@ SYMBOLS = [
     "okv_meta_fetch", "okv_meta_parse", "okv_meta_num_blocks", "okv_meta_compression",
     "okv_meta_descs", "okv_meta_first_key", "okv_meta_last_key", "okv_meta_block",
     "okv_meta_free", "okv_synth_segment",
+    "okv_reader_open", "okv_reader_fetch_metadata", "okv_reader_load_metadata",
+    "okv_reader_num_blocks", "okv_reader_read_block", "okv_reader_get_row",
+    "okv_reader_get_range", "okv_reader_close", "okv_reader_free", "okv_reader_row_iter",
+    "okv_iter_next", "okv_iter_seek", "okv_iter_free",
 ]
+
+
+class Row(C.Structure):
+    _fields_ = [("key", C.c_void_p), ("key_len", C.c_uint64), ("val", C.c_void_p),
+                ("val_len", C.c_uint64)]
 
 
 class BlockDesc(C.Structure):
@@ -116,6 +125,20 @@ def lib():
                                  C.POINTER(u64)]),
         "okv_meta_free": (None, [p]),
         "okv_synth_segment": (p, [i32, u64, u64, u64, u64, u64]),
+        "okv_reader_open": (p, [p, p, u64, C.c_int64]),
+        "okv_reader_fetch_metadata": (i32, [p]),
+        "okv_reader_load_metadata": (i32, [p, p, u64]),
+        "okv_reader_num_blocks": (i32, [p, C.POINTER(u64)]),
+        "okv_reader_read_block": (i32, [p, u64, C.POINTER(C.POINTER(Row)), C.POINTER(u64)]),
+        "okv_reader_get_row": (i32, [p, p, C.c_size_t, C.POINTER(Row)]),
+        "okv_reader_get_range": (i32, [p, p, C.c_size_t, p, C.c_size_t,
+                                       C.POINTER(C.POINTER(Row)), C.POINTER(u64)]),
+        "okv_reader_close": (i32, [p]),
+        "okv_reader_free": (None, [p]),
+        "okv_reader_row_iter": (p, [p, i32]),
+        "okv_iter_next": (i32, [p, C.POINTER(Row)]),
+        "okv_iter_seek": (i32, [p, p, C.c_size_t]),
+        "okv_iter_free": (None, [p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -1272,12 +1272,12 @@ int okv_profile_read(okv_ctx* ctx, double* ms, uint64_t* calls) {
 
 void* okv_device_alloc(okv_ctx* ctx, size_t bytes) {
   void* p = nullptr;
-  if (ctx) hipSetDevice(ctx->device);
+  if (ctx) (void)hipSetDevice(ctx->device);
   if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) return nullptr;
   return p;
 }
 void okv_device_free(okv_ctx* ctx, void* p) {
-  if (ctx) hipSetDevice(ctx->device);
+  if (ctx) (void)hipSetDevice(ctx->device);
   if (p) (void)hipFree(p);
 }
 void* okv_host_alloc(size_t bytes) {

@@ -19,6 +19,7 @@ import pytest
 
 from oracle import coracle as CO
 from oracle import pyoracle as P
+from tests import reference_cases as RC
 from tests.conftest import GOLDEN, unpack
 
 R200 = [(b"key%03d" % i, b"value%03d" % i) for i in range(200)]
@@ -45,48 +46,47 @@ def test_xxh64_spec_and_implementations():
         assert P.xxh64(d, seed) == P.xxh64_py(d, seed) == CO.xxh64(d, seed)
 
 
-# ---- reference known answers (segment_reader_test.go) ----------------------
+# ---- reference known answers (tests/reference_cases.py) ----------------------
 
 
-def test_reference_known_answers_uncompressed():
-    """TestReadUncompressed, segment_reader_test.go:12-269."""
+class OracleImpl:
+    """Adapter: the Python restatement (oracle/pyoracle.py)."""
+    GoError, GoPanic, EOF, FATAL = P.GoError, P.GoPanic, P.EOF, P.FATAL
+    DirectionAscending, DirectionDescending = P.DirectionAscending, P.DirectionDescending
+    UnboundStart, UnboundEnd = P.UnboundStart, P.UnboundEnd
+
+    @staticmethod
+    def write(rows, **kw):
+        return write(rows, **kw)
+
+    @staticmethod
+    def reader(data, file_bytes):
+        return P.SegmentReader(data, file_bytes)
+
+    @staticmethod
+    def stats(r, meta):
+        md = r.BytesToMetadata(meta)
+        return [(st.FirstKey, st.Offset, st.BlockSize, st.OriginalSize, st.CompressedSize)
+                for st in md.BlockIndex.ascend()]
+
+    @staticmethod
+    def first_last(r, meta):
+        md = r.BytesToMetadata(meta)
+        return md.FirstKey, md.LastKey
+
+    @staticmethod
+    def read_block(r, i):
+        return r.ReadBlockWithStat(r._md().BlockIndex.ascend()[i])
+
+
+@pytest.mark.parametrize("case", RC.CASES, ids=lambda c: c.__name__)
+def test_reference_cases_oracle(case):
+    case(OracleImpl)
+
+
+def test_reference_known_answers_c_oracle():
+    """The C restatement reproduces TestReadUncompressed's writer output and index."""
     seg, flen, meta = write(R200)
-    r = P.SegmentReader(seg, flen)
-    md = r.BytesToMetadata(meta)
-    r.LoadCachedMetadata(md)
-    assert md.FirstKey == b"key000" and md.LastKey == b"key199"  # :61-66
-    assert md.BlockIndex.Len() == 2  # :77
-    b0, ok = md.BlockIndex.Get(b"key000")
-    assert ok and b0.FirstKey == b"key000" and b0.OriginalSize == 3600  # :81-86
-    assert b0.CompressedSize == 0 and b0.Offset == 0  # :87-92
-    b1, ok = md.BlockIndex.Get(b"key180")
-    assert ok and b1.OriginalSize == 400 and b1.CompressedSize == 0  # :94-102
-    assert b1.Offset == 4096  # :103
-    rows = r.ReadBlockWithStat(b0)
-    assert rows[0].Key == b"key000" and rows[0].Value == b"value000"  # :116-121
-    rows2 = r.ReadBlockWithStat(b1)
-    assert len(rows) + len(rows2) == 200  # :131
-    assert rows2[0].Key == b"key180" and rows2[0].Value == b"value180"  # :135-140
-    assert rows2[-1].Key == b"key199" and rows2[-1].Value == b"value199"  # :142-147
-    assert r.GetRow(b"key000").Value == b"value000"  # :150-159
-    with pytest.raises(P.GoError) as e:
-        r.GetRow(b"fuhguiregui")  # :161-164
-    assert e.value.kind == P.ErrNoRows
-    assert r.GetRow(b"key101").Value == b"value101"  # :166-179
-    assert r.GetRow(b"key199").Value == b"value199"  # :181-190
-    g = r.GetRange(b"key000", b"key180")  # :193-212
-    assert len(g) == 180 and g[0].Key == b"key000" and g[-1].Key == b"key179"
-    assert g[-1].Value == b"value179"
-    assert len(r.GetRange(b"", b"key180")) == 180  # :215-222
-    g = r.GetRange(b"key180", b"\xff")  # :224-244
-    assert len(g) == 20 and g[0].Key == b"key180" and g[-1].Key == b"key199"
-    g = r.GetRange(b"key199", b"\xff")  # :246-259
-    assert len(g) == 1 and g[0].Key == b"key199" and g[0].Value == b"value199"
-    r.Close()  # :261-268
-    with pytest.raises(P.GoError) as e:
-        r.Close()
-    assert e.value.kind == P.ErrAlreadyClosed
-    # the C restatement derives the same bytes and index
     w = CO.Writer()
     for k, v in R200:
         assert w.write_row(k, v) == 0
@@ -96,38 +96,11 @@ def test_reference_known_answers_uncompressed():
     assert rc == 0 and [(e["first_key"], e["offset"], e["original_size"], e["compressed_size"])
                         for e in cm["entries"]] == [(b"key000", 0, 3600, 0),
                                                    (b"key180", 4096, 400, 0)]
-
-
-def test_reference_known_answers_blank_value():
-    """TestReadBlankRecordUncompressed, segment_reader_test.go:271-326."""
-    seg, flen, meta = write(R200 + [(b"key200", b"")])
-    r = P.SegmentReader(seg, flen)
-    r.LoadCachedMetadata(r.BytesToMetadata(meta))
-    row = r.GetRow(b"key200")
-    assert row.Key == b"key200" and P._b(row.Value) == b""  # :316-325
-    assert row.Value is None  # Q4: readBytes(0) returns nil (segment_reader.go:490-493)
-
-
-def test_reference_known_answers_single_row():
-    """TestReadSingleRecordUncompressed, segment_reader_test.go:328-511."""
-    seg, flen, meta = write(R200[:1])
-    r = P.SegmentReader(seg, flen)
-    md = r.BytesToMetadata(meta)
-    r.LoadCachedMetadata(md)
-    assert md.FirstKey == b"key000" and md.LastKey == b"key000"
-    assert md.BlockIndex.Len() == 1  # :388
-    b0, _ = md.BlockIndex.Get(b"key000")
-    assert b0.OriginalSize == 20 and b0.CompressedSize == 0 and b0.Offset == 0  # :392-403
-    rows = r.ReadBlockWithStat(b0)
-    assert rows[0].Key == b"key000" and rows[-1].Value == b"value000"
-    assert r.GetRow(b"key000").Value == b"value000"
-    with pytest.raises(P.GoError):
-        r.GetRow(b"fuhguiregui")
-    assert len(r.GetRange(b"key000", b"key000")) == 0  # :457-464
-    assert len(r.GetRange(b"", b"key000")) == 0  # :466-473
-    g = r.GetRange(b"", b"\xff")  # :476-495
-    assert len(g) == 1 and g[0].Key == b"key000"
-    assert len(r.GetRange(b"key000", b"\xff")) == 1  # :497-510
+    rnd = bytes(random.Random(1).getrandbits(8) for _ in range(10))
+    assert CO.fetch_meta(seg + rnd, flen)[0] == -201  # ErrInvalidMagicNumber
+    assert CO.fetch_meta(rnd + seg, flen)[0] == -203  # ErrMismatchedMetaBlockHash
+    rc, m = CO.fetch_meta(seg, flen)
+    assert rc == 0 and m["first_key"] == b"key000" and len(m["entries"]) == 2
 
 
 def test_reference_zstd_known_answers_are_parity_unpinned():
@@ -138,41 +111,6 @@ def test_reference_zstd_known_answers_are_parity_unpinned():
     with pytest.raises(NotImplementedError):
         P.SegmentWriter(P.SegmentWriterOptions(ZSTDCompressionLevel=1)).WriteRow(b"k", b"v")
     assert CO.Writer(zstd_level=1).write_row(b"k", b"v") == -106
-
-
-def test_reference_corrupt_file_end():
-    """TestReadCorruptFileEnd, segment_reader_test.go:727-776 (10 trailing
-    random bytes; crypto/rand replaced by a seeded generator)."""
-    seg, flen, meta = write(R200)
-    rnd = bytes(random.Random(1).getrandbits(8) for _ in range(10))
-    r = P.SegmentReader(seg + rnd, flen)
-    with pytest.raises(P.GoError) as e:
-        r.FetchAndLoadMetadata()
-    assert e.value.kind == P.ErrInvalidMagicNumber and e.value.kind in P.FATAL
-    rc, _ = CO.fetch_meta(seg + rnd, flen)
-    assert rc == -201
-
-
-def test_reference_corrupt_file_middle():
-    """TestReadCorruptFileMiddle, segment_reader_test.go:778-830: 10 bytes
-    written straight into the sink after row 101 shift every offset."""
-    w = P.SegmentWriter(P.SegmentWriterOptions())
-    for i, (k, v) in enumerate(R200):
-        w.WriteRow(k, v)
-        if i == 101:
-            w.external += bytes(random.Random(2).getrandbits(8) for _ in range(10))
-    flen, meta = w.Close()
-    data = bytes(w.external)
-    r = P.SegmentReader(data, flen)
-    with pytest.raises(P.GoError) as e:
-        r.FetchAndLoadMetadata()
-    assert e.value.kind == P.ErrMismatchedMetaBlockHash and e.value.kind in P.FATAL
-    rc, _ = CO.fetch_meta(data, flen)
-    assert rc == -203
-    # and the intact file loads
-    seg, flen2, meta2 = write(R200)
-    rc, m = CO.fetch_meta(seg, flen2)
-    assert rc == 0 and m["first_key"] == b"key000" and len(m["entries"]) == 2
 
 
 def test_reference_writer_errors():
@@ -197,95 +135,6 @@ def test_reference_writer_errors():
         w.WriteRow(b"a", b"b")
     assert e.value.kind == P.ErrWriterClosed
 
-
-def test_reference_larger_than_block():
-    """TestSegmentWriterLargerThanBlock segment_writer_test.go:73-112: a 10 511 B
-    row pads to 12 288 (Q2 rule: (len/DBS+1)*DBS)."""
-    rows = [(b"a" * 511, b"b" * 10000)] + [(b"key%d" % i, b"value%d" % i) for i in range(200)]
-    seg, flen, meta = write(rows)
-    md = P.bytes_to_metadata(meta)
-    assert [st.desc()[:3] for st in md.entries] == [(0, 12288, 10517), (12288, 4096, 3600),
-                                                    (16384, 4096, 180)]
-    total = sum(len(P.read_block(seg, st.desc(), 0)[1]) for st in md.entries)
-    assert total == 201
-
-
-# ---- RowIter (segment_row_iter_test.go) ----------------------------------------
-
-
-def _iter_reader():
-    seg, flen, meta = write(R200)
-    r = P.SegmentReader(seg, flen)
-    return r
-
-
-def test_reference_rowiter_next():
-    """TestRowIterNext segment_row_iter_test.go:12-134."""
-    r = _iter_reader()
-    it = r.RowIter(P.DirectionAscending)
-    assert it.Next().Key == b"key000"
-    assert it.Next().Key == b"key001"
-    for _ in range(198):
-        row = it.Next()
-    assert row.Key == b"key199" and row.Value == b"value199"
-    with pytest.raises(P.GoError) as e:
-        it.Next()
-    assert e.value.kind == P.EOF
-    it = r.RowIter(P.DirectionDescending)
-    assert it.Next().Key == b"key199"
-    assert it.Next().Key == b"key198"
-    for _ in range(197):
-        row = it.Next()
-    assert row.Key == b"key001" and row.Value == b"value001"
-
-
-def _eof(it):
-    with pytest.raises(P.GoError) as e:
-        it.Next()
-    assert e.value.kind == P.EOF
-
-
-def test_reference_rowiter_seek():
-    """TestRowIterSeek segment_row_iter_test.go:136-378."""
-    r = _iter_reader()
-    it = r.RowIter(P.DirectionAscending)
-    it.Seek(b"key010")
-    assert it.Next().Key == b"key010" and it.Next().Key == b"key011"
-    it.Seek(P.UnboundStart)
-    assert it.Next().Key == b"key000"
-    it.Seek(b"key200")
-    _eof(it)
-    it.Seek(P.UnboundEnd)
-    _eof(it)
-    it = r.RowIter(P.DirectionDescending)
-    it.Seek(b"key010")
-    assert it.Next().Key == b"key010" and it.Next().Key == b"key009"
-    it.Seek(P.UnboundStart)
-    _eof(it)
-    it.Seek(P.UnboundEnd)
-    assert it.Next().Key == b"key199"
-    it.Seek(b"key200")
-    assert it.Next().Key == b"key199"
-    it.Seek(b"key")
-    _eof(it)
-    it.Seek(P.UnboundEnd)
-    assert it.Next().Key == b"key199"
-    it.Seek(b"key000")
-    assert it.Next().Key == b"key000"
-    _eof(it)
-
-
-def test_reference_rollover_descending_seek():
-    """TestRollover segment_row_iter_test.go:380-450 (run with BloomFilter=nil:
-    the bloom only feeds GetRow, not RowIter)."""
-    rows = [(b"key%03d" % i, b"value%03d-I-SHOULD-NOT-SHOW" % i) for i in range(1, 200, 2)]
-    seg, flen, meta = write(rows + [(b"key900", b"value900")])
-    r = P.SegmentReader(seg, flen)
-    it = r.RowIter(P.DirectionDescending)
-    it.Seek(b"key006")
-    got = [it.Next().Key for _ in range(3)]
-    assert got == [b"key005", b"key003", b"key001"]
-    _eof(it)
 
 
 # ---- the two restatements agree ---------------------------------------------

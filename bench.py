@@ -37,6 +37,8 @@ CONFIGS = {
     "c3": (1, 3, 65536, 57344, 65536,
            "C3: 65536 x 64 KiB blocks, Zipf key 8-256 B / value 0-4096 B"),
     "c2": (0, 1, 256, 3584, 4096, "C2: 256 x 4 KiB blocks, fixed 16 B key / 64 B value"),
+    "c5": (1, 3, 16384, 57344, 65536,
+           "C5: 1 GiB segment per GPU (16384 x 64 KiB C3-style blocks)"),
 }
 
 

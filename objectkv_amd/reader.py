@@ -84,8 +84,8 @@ class SegmentReader:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h:
-            lib().okv_reader_free(h)
+        if h and _lib._lib is not None:
+            _lib._lib.okv_reader_free(h)
             self._h = None
 
     def FetchAndLoadMetadata(self):
@@ -143,8 +143,8 @@ class RowIter:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h:
-            lib().okv_iter_free(h)
+        if h and _lib._lib is not None:
+            _lib._lib.okv_iter_free(h)
             self._h = None
 
     def Next(self) -> KVPair:
@@ -162,4 +162,3 @@ class RowIter:
 
 __all__ = ["SegmentReader", "RowIter", "KVPair", "GoError", "GoPanic", "DirectionAscending",
            "DirectionDescending", "UnboundStart", "UnboundEnd", "FATAL"]
-_ = _lib

@@ -112,8 +112,9 @@ class SegmentWriter:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h:
-            lib().okv_writer_free(h)
+        L = _lib._lib
+        if h and L is not None:
+            L.okv_writer_free(h)
             self._h = None
 
 
@@ -229,8 +230,9 @@ class Decoder:
         self.device = device
 
     def close(self):
-        if getattr(self, "_ctx", None):
-            lib().okv_close(self._ctx)
+        L = _lib._lib
+        if getattr(self, "_ctx", None) and L is not None:
+            L.okv_close(self._ctx)
             self._ctx = None
 
     __del__ = close

@@ -67,6 +67,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--e2e", action="store_true", help="also time the host-buffer path")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="control-plane backend (barrier, max time); gloo for rehearsals")
+    ap.add_argument("--device-mod", type=int, default=0,
+                    help="rehearsal only: map LOCAL_RANK -> LOCAL_RANK %% N (ranks share a GPU)")
     args = ap.parse_args()
 
     import torch
@@ -76,11 +80,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.device_mod:
+        local %= args.device_mod
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local)
@@ -143,7 +152,8 @@ def main():
     dec.profile(False)
     t_max = t_elapsed
     if dist:
-        tt = torch.tensor([t_elapsed], dtype=torch.float64, device=dev)
+        tdev = dev if args.dist_backend == "nccl" else "cpu"
+        tt = torch.tensor([t_elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
     ms_per_step = 1e3 * t_max / args.steps

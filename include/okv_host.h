@@ -25,13 +25,7 @@ extern "C" {
 #endif
 
 /* Go error sentinels (values shared with the test oracle) */
-#define OKV_W_KEY_TOO_LARGE (-101)   /* ErrKeyTooLarge   segment_writer.go:71 */
-#define OKV_W_VALUE_TOO_LARGE (-102) /* ErrValueTooLarge :72 */
-#define OKV_W_CLOSED (-103)          /* ErrWriterClosed  :69 */
-#define OKV_W_INVALID_KEY (-104)     /* ErrInvalidKey    :74 */
-#define OKV_W_NIL_WRITER (-105)      /* Go panics in Close (:212) -- see okv_writer_close */
-#define OKV_W_UNSUPPORTED (-106)     /* zstd level > 0: encoder not implemented */
-#define OKV_W_NO_ROWS (-107)         /* ErrNoRowsWritten :73 (reachable only with strict_go == 0) */
+/* OKV_W_* (SegmentWriter sentinels) are defined in okv_sst.h */
 #define OKV_M_MAGIC (-201)           /* ErrInvalidMagicNumber      segment_reader.go:84 */
 #define OKV_M_VERSION (-202)         /* ErrUnknownSegmentVersion   :81 */
 #define OKV_M_HASH (-203)            /* ErrMismatchedMetaBlockHash :82 */

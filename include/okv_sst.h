@@ -41,6 +41,16 @@ extern "C" {
 #define OKV_E_NOMEM (-4)
 #define OKV_E_NODEV (-5)    /* no GPU / bad device id */
 
+/* Go SegmentWriter sentinels returned by the encode (values shared with
+ * okv_host.h and the test oracle; segment_writer.go:69-74) */
+#define OKV_W_KEY_TOO_LARGE (-101)   /* ErrKeyTooLarge */
+#define OKV_W_VALUE_TOO_LARGE (-102) /* ErrValueTooLarge */
+#define OKV_W_CLOSED (-103)          /* ErrWriterClosed */
+#define OKV_W_INVALID_KEY (-104)     /* ErrInvalidKey: empty key (WriteRow :89-91) */
+#define OKV_W_NIL_WRITER (-105)      /* Go panics in Close when no block is open (:212, Q1) */
+#define OKV_W_UNSUPPORTED (-106)     /* zstd level > 0: encoder not implemented */
+#define OKV_W_NO_ROWS (-107)         /* ErrNoRowsWritten (:221-223) */
+
 /* ---- per-block status (okv_decode_out.blk_status) ---------------------- */
 /* Mirrors what ReadBlockWithStat does for that block (segment_reader.go). */
 #define OKV_BLK_OK 0
@@ -60,6 +70,8 @@ extern "C" {
 #define OKV_F_INDEX_ONLY 2u  /* key_off/val_off are byte offsets into seg; no arenas written */
 #define OKV_F_ASYNC 4u       /* with DEVICE_PTRS: enqueue on the ctx stream and return;
                                 totals are NOT filled (call okv_decode_totals after okv_sync) */
+#define OKV_F_NO_CLOSE 8u    /* encode: stop after blocks + block index + meta block; the
+                                meta XXH64 and the 25-byte trailer are left to okv_encode_close */
 
 /* One data-block index entry: BlockStat (sst/block_stat.go:9-24) without
  * FirstKey and Hash, which the decode does not need. */
@@ -150,6 +162,98 @@ uint64_t okv_xxh64(const void *data, size_t len, uint64_t seed);
 int okv_hash_blocks(okv_ctx *ctx, const uint8_t *seg, uint64_t seg_bytes,
                     const okv_block_desc *descs, uint32_t nblk, uint64_t *hashes,
                     uint32_t flags);
+
+/* ======================================================================== *
+ * Encode: SegmentWriter.WriteRow x n -> Close (segment_writer.go:80-328)
+ * ======================================================================== */
+
+/* Rows to encode, structure of arrays (the okv_decode_out layout, so a decode
+ * feeds an encode directly -- the compaction shape).  Row i is
+ *   key   = key_arena[key_off[i] .. +key_len[i]]
+ *   value = val_arena[val_off[i] .. +val_len[i]]
+ * in the order WriteRow would be called ("expected that rows are written in
+ * order", segment_writer.go:78; the writer does not check it and neither do
+ * we).  key_arena_bytes / val_arena_bytes are the arena extents (host mode
+ * stages that many bytes; device mode uses them only for validation). */
+typedef struct okv_rows {
+  const uint8_t *key_arena;
+  const uint64_t *key_off;
+  const uint16_t *key_len;
+  const uint8_t *val_arena;
+  const uint64_t *val_off;
+  const uint32_t *val_len;
+  uint64_t n_rows;
+  uint64_t key_arena_bytes, val_arena_bytes;
+} okv_rows;
+
+/* SegmentWriterOptions (segment_writer_option.go:5-16).  BloomFilter is not
+ * supported (writes bloom byte 0, as BloomFilter == nil). */
+typedef struct okv_encode_opts {
+  uint64_t threshold_bytes; /* DataBlockThresholdBytes (default 3584) */
+  uint64_t block_size;      /* DataBlockSize (default 4096) */
+  int compression;          /* OKV_COMP_NONE, or OKV_COMP_LZ4: Go writes raw bytes with
+                               CompressedSize = OriginalSize and meta byte 2 (Q7);
+                               OKV_COMP_ZSTD -> OKV_W_UNSUPPORTED */
+  int strict_go;            /* 1: a Close with no open block panics in Go (Q1) ->
+                               OKV_W_NIL_WRITER; 0: write the footer normally */
+} okv_encode_opts;
+
+/* Output: the segment file, written as the Go writer writes it:
+ *   seg[0 .. data_bytes)                      data blocks (BlockStat order)
+ *   seg[data_bytes .. +meta_bytes)            meta block (generateMetaBlock :284-328)
+ *   seg[data_bytes + meta_bytes .. +25)       trailer: u64 meta offset, u64 XXH64(meta),
+ *                                             u8 version 1, u64 magic (:226-276)
+ * plus the block index as arrays.  Any of blk_first_row / blk_desc / blk_hash
+ * may be NULL.  FirstKey of block b = key of row blk_first_row[b]. */
+typedef struct okv_encode_out {
+  uint8_t *seg;
+  uint64_t seg_cap;
+  uint64_t *blk_first_row;  /* [blk_cap + 1]; entry n_blocks = n_rows */
+  okv_block_desc *blk_desc; /* [blk_cap] Offset, BlockSize, OriginalSize, CompressedSize */
+  uint64_t *blk_hash;       /* [blk_cap] BlockStat.Hash */
+  uint64_t blk_cap;
+  /* filled on return (also with OKV_E_CAPACITY): */
+  uint64_t n_blocks;
+  uint64_t data_bytes;  /* sum of BlockSize == meta block offset */
+  uint64_t meta_bytes;
+  uint64_t file_bytes;  /* data + meta + 25: Close()'s first return value */
+  uint64_t meta_hash;   /* 0 with OKV_F_NO_CLOSE until okv_encode_close */
+  uint64_t bad_row;     /* OKV_W_INVALID_KEY: the first row with an empty key */
+} okv_encode_out;
+
+/*
+ * Encode rows into one segment on the GPU.  flags: OKV_F_DEVICE_PTRS (rows and
+ * every output pointer are device pointers; seg must be 16-byte aligned),
+ * OKV_F_NO_CLOSE.  Returns OKV_OK; OKV_E_CAPACITY (sizes in out set, nothing
+ * written: call again with seg_cap >= file_bytes and blk_cap >= n_blocks --
+ * a call with zero capacities is the size query); OKV_W_INVALID_KEY (bad_row
+ * set); OKV_W_NIL_WRITER (strict_go and the last row closed a block, or no
+ * rows); OKV_W_NO_ROWS (no rows, strict_go == 0); OKV_W_UNSUPPORTED; or an
+ * OKV_E_* error.
+ */
+int okv_encode_rows(okv_ctx *ctx, const okv_rows *rows, const okv_encode_opts *opts,
+                    okv_encode_out *out, uint32_t flags);
+
+/* Close after OKV_F_NO_CLOSE: XXH64 of the meta block on the host (one
+ * sequential hash, segment_writer.go:248) and the trailer written into seg.
+ * flags: OKV_F_DEVICE_PTRS as given to okv_encode_rows. */
+int okv_encode_close(okv_ctx *ctx, okv_encode_out *out, uint32_t flags);
+
+/* Per-phase encode timing (HIP events on the ctx stream, enabled by
+ * okv_profile(ctx, 1)): ms[4] = cut (E1-E9), pack, block hash, meta block,
+ * summed over the profiled okv_encode_rows calls. */
+int okv_encode_profile_read(okv_ctx *ctx, double *ms, uint64_t *calls);
+int okv_encode_profile_reset(okv_ctx *ctx);
+
+/* Deterministic C1/C2/C4 rows on the device: key = row index big-endian in
+ * key_len bytes, value = val_len bytes of splitmix64(seed) 8-byte LE words,
+ * drawn in row order (oracle/pyoracle.py rows_fixed).  Rows first_row ..
+ * first_row + n - 1, packed: key_off[i] = i * key_len, val_off[i] = i * val_len
+ * (relative to this call's arenas).  All pointers are device pointers. */
+int okv_synth_rows_fixed(okv_ctx *ctx, uint64_t seed, uint64_t first_row, uint64_t n,
+                         uint32_t key_len, uint32_t val_len, uint8_t *key_arena,
+                         uint64_t *key_off, uint16_t *key_len_out, uint8_t *val_arena,
+                         uint64_t *val_off, uint32_t *val_len_out);
 
 /* Per-kernel timing with HIP events recorded on the context stream around
  * each launch of okv_decode_blocks (pass 1 count, pass 2 scan, pass 3

@@ -16,7 +16,10 @@ LIB_PATH = os.path.join(_HERE, "libokv_sst.so")
 OKV_OK, OKV_E_ARG, OKV_E_HIP, OKV_E_CAPACITY, OKV_E_NOMEM, OKV_E_NODEV = 0, -1, -2, -3, -4, -5
 BLK_OK, BLK_EOF, BLK_SHORT, BLK_PANIC, BLK_UNSUPPORTED, BLK_CAPACITY = 0, 1, 2, 3, 4, 5
 COMP_NONE, COMP_ZSTD, COMP_LZ4 = 0, 1, 2
-F_DEVICE_PTRS, F_INDEX_ONLY, F_ASYNC = 1, 2, 4
+F_DEVICE_PTRS, F_INDEX_ONLY, F_ASYNC, F_NO_CLOSE = 1, 2, 4, 8
+# SegmentWriter sentinels (okv_sst.h OKV_W_*)
+W_KEY_TOO_LARGE, W_VALUE_TOO_LARGE, W_CLOSED, W_INVALID_KEY = -101, -102, -103, -104
+W_NIL_WRITER, W_UNSUPPORTED, W_NO_ROWS = -105, -106, -107
 SYNTH_FIXED, SYNTH_ZIPF = 0, 1
 
 # exported symbols declared by include/*.h (checked by tests/test_abi.py)
@@ -25,6 +28,8 @@ SYMBOLS = [
     "okv_abi_version", "okv_decode_plan", "okv_decode_blocks", "okv_decode_totals",
     "okv_xxh64", "okv_hash_blocks", "okv_device_alloc", "okv_device_free", "okv_host_alloc",
     "okv_host_free", "okv_memcpy", "okv_profile", "okv_profile_read",
+    "okv_encode_rows", "okv_encode_close", "okv_encode_profile_read", "okv_encode_profile_reset",
+    "okv_synth_rows_fixed",
     "okv_writer_new", "okv_writer_write_row", "okv_writer_close", "okv_writer_data",
     "okv_writer_meta", "okv_writer_num_blocks", "okv_writer_block", "okv_writer_free",
     "okv_meta_fetch", "okv_meta_parse", "okv_meta_num_blocks", "okv_meta_compression",
@@ -54,6 +59,26 @@ class DecodeOut(C.Structure):
                 ("val_arena", C.c_void_p), ("row_cap", C.c_uint64), ("key_cap", C.c_uint64),
                 ("val_cap", C.c_uint64), ("n_rows", C.c_uint64), ("key_bytes", C.c_uint64),
                 ("val_bytes", C.c_uint64), ("n_bad_blocks", C.c_uint64)]
+
+
+class Rows(C.Structure):
+    _fields_ = [("key_arena", C.c_void_p), ("key_off", C.c_void_p), ("key_len", C.c_void_p),
+                ("val_arena", C.c_void_p), ("val_off", C.c_void_p), ("val_len", C.c_void_p),
+                ("n_rows", C.c_uint64), ("key_arena_bytes", C.c_uint64),
+                ("val_arena_bytes", C.c_uint64)]
+
+
+class EncodeOpts(C.Structure):
+    _fields_ = [("threshold_bytes", C.c_uint64), ("block_size", C.c_uint64),
+                ("compression", C.c_int), ("strict_go", C.c_int)]
+
+
+class EncodeOut(C.Structure):
+    _fields_ = [("seg", C.c_void_p), ("seg_cap", C.c_uint64), ("blk_first_row", C.c_void_p),
+                ("blk_desc", C.c_void_p), ("blk_hash", C.c_void_p), ("blk_cap", C.c_uint64),
+                ("n_blocks", C.c_uint64), ("data_bytes", C.c_uint64),
+                ("meta_bytes", C.c_uint64), ("file_bytes", C.c_uint64),
+                ("meta_hash", C.c_uint64), ("bad_row", C.c_uint64)]
 
 
 _lib = None
@@ -105,6 +130,12 @@ def lib():
         "okv_memcpy": (i32, [p, p, p, C.c_size_t, i32]),
         "okv_profile": (i32, [p, i32]),
         "okv_profile_read": (i32, [p, C.POINTER(C.c_double), C.POINTER(u64)]),
+        "okv_encode_rows": (i32, [p, C.POINTER(Rows), C.POINTER(EncodeOpts),
+                                  C.POINTER(EncodeOut), u32]),
+        "okv_encode_close": (i32, [p, C.POINTER(EncodeOut), u32]),
+        "okv_encode_profile_read": (i32, [p, C.POINTER(C.c_double), C.POINTER(u64)]),
+        "okv_encode_profile_reset": (i32, [p]),
+        "okv_synth_rows_fixed": (i32, [p, u64, u64, u64, u32, u32, p, p, p, p, p, p]),
         "okv_writer_new": (p, [u64, u64, i32, i32]),
         "okv_writer_write_row": (i32, [p, p, C.c_size_t, p, C.c_size_t]),
         "okv_writer_close": (i32, [p, i32, C.POINTER(u64), C.POINTER(u64)]),

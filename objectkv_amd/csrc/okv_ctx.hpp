@@ -1,0 +1,89 @@
+// okv_ctx.hpp -- the per-GPU context shared by the decode (okv_decode.hip)
+// and encode (okv_encode.hip) translation units.  Internal header.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "okv_kernels.hpp"
+#include "okv_sst.h"
+
+namespace okv {
+struct EncScratch;  // okv_encode.hip
+void enc_release(okv_ctx* ctx);
+// okv_decode.hip: enqueue XXH64 of each block's BlockSize bytes (device pointers).
+void launch_hash(hipStream_t stream, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
+                 uint32_t nblk, uint64_t* out);
+}  // namespace okv
+
+struct okv_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+  // pass-1/2 scratch
+  okv::BlockCount* d_cnt = nullptr;
+  okv::Prefix* d_lp = nullptr;
+  okv::Prefix* d_tile_tot = nullptr;
+  okv::Prefix* d_tile_pre = nullptr;
+  uint32_t* d_rec = nullptr;       // [nblk][kRCap] record positions (pass 1)
+  uint32_t* d_big = nullptr;       // big-block list + its counter (d_big[nblk])
+  size_t cap_blocks = 0;
+  okv::Totals* d_tot = nullptr;
+  okv::Totals* h_tot = nullptr;  // pinned
+  // host-mode staging buffers (device side)
+  uint8_t* d_seg = nullptr;
+  size_t cap_seg = 0;
+  okv::Desc* d_desc = nullptr;
+  size_t cap_desc = 0;
+  void* d_out = nullptr;
+  size_t cap_out = 0;
+  uint64_t* d_hash = nullptr;
+  size_t cap_hash = 0;
+  // per-pass event timing (okv_profile)
+  int variant = 3;  // diagnostic ablation selector (OKV_COPY_VARIANT)
+  uint32_t gather_grid = 0;  // 0: one workgroup per block; else persistent grid size
+  bool prof = false;
+  std::vector<hipEvent_t> ev;  // 4 per timed call
+  size_t ev_used = 0;
+  double prof_ms[3] = {0, 0, 0};
+  uint64_t prof_calls = 0;
+  okv::EncScratch* enc = nullptr;  // encode scratch (okv_encode.hip)
+};
+
+namespace okv {
+
+inline int set_err(okv_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
+  if (c) {
+    c->err = what;
+    if (e != hipSuccess) {
+      c->err += ": ";
+      c->err += hipGetErrorString(e);
+    }
+  }
+  return code;
+}
+
+#define OKV_HIP(call)                                             \
+  do {                                                            \
+    hipError_t e_ = (call);                                       \
+    if (e_ != hipSuccess) return set_err(ctx, OKV_E_HIP, #call, e_); \
+  } while (0)
+
+inline int grow(okv_ctx* ctx, void** p, size_t* cap, size_t need) {
+  if (need <= *cap && *p) return OKV_OK;
+  if (*p) {
+    OKV_HIP(hipStreamSynchronize(ctx->stream));
+    OKV_HIP(hipFree(*p));
+    *p = nullptr;
+  }
+  size_t c = std::max<size_t>(need, 4096);
+  c = (c + 4095) & ~size_t(4095);
+  OKV_HIP(hipMalloc(p, c));
+  *cap = c;
+  return OKV_OK;
+}
+
+}  // namespace okv

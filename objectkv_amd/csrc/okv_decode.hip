@@ -28,6 +28,7 @@
 #include <string>
 #include <vector>
 
+#include "okv_ctx.hpp"
 #include "okv_kernels.hpp"
 #include "okv_sst.h"
 
@@ -692,24 +693,6 @@ __global__ __launch_bounds__(kThreads) void okv_index_kernel(CopyParams P) {
 // XXH64 has four independent accumulators, so four lanes share one block
 // (lane q owns stripe word q); the merge and tail run on lane q == 0.
 // ---------------------------------------------------------------------------
-__device__ constexpr uint64_t XP1 = 11400714785074694791ULL, XP2 = 14029467366897019727ULL,
-                              XP3 = 1609587929392839161ULL, XP4 = 9650029242287828579ULL,
-                              XP5 = 2870177450012600261ULL;
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
-  return (x << r) | (x >> (64 - r));
-}
-__device__ __forceinline__ uint64_t xround(uint64_t acc, uint64_t in) {
-  acc += in * XP2;
-  acc = rotl64(acc, 31);
-  return acc * XP1;
-}
-__device__ __forceinline__ uint64_t ld64u(const uint8_t* p) {  // unaligned LE load
-  uint64_t v = 0;
-#pragma unroll
-  for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
-  return v;
-}
-
 __global__ __launch_bounds__(kThreads) void okv_hash_kernel(const uint8_t* __restrict__ seg,
                                                             uint64_t seg_bytes,
                                                             const Desc* __restrict__ descs,
@@ -781,6 +764,14 @@ __global__ __launch_bounds__(kThreads) void okv_hash_kernel(const uint8_t* __res
   out[b] = h;
 }
 
+void launch_hash(hipStream_t stream, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
+                 uint32_t nblk, uint64_t* out) {
+  if (!nblk) return;
+  const uint64_t threads = uint64_t(nblk) * 4;
+  hipLaunchKernelGGL(okv_hash_kernel, dim3(uint32_t((threads + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, stream, seg, seg_bytes, descs, nblk, out);
+}
+
 }  // namespace okv
 
 // ===========================================================================
@@ -788,72 +779,7 @@ __global__ __launch_bounds__(kThreads) void okv_hash_kernel(const uint8_t* __res
 // ===========================================================================
 using namespace okv;
 
-struct okv_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  bool own_stream = false;
-  std::string err;
-  // pass-1/2 scratch
-  BlockCount* d_cnt = nullptr;
-  Prefix* d_lp = nullptr;
-  Prefix* d_tile_tot = nullptr;
-  Prefix* d_tile_pre = nullptr;
-  uint32_t* d_rec = nullptr;       // [nblk][kRCap] record positions (pass 1)
-  uint32_t* d_big = nullptr;       // big-block list + its counter (d_big[nblk])
-  size_t cap_blocks = 0;
-  Totals* d_tot = nullptr;
-  Totals* h_tot = nullptr;  // pinned
-  // host-mode staging buffers (device side)
-  uint8_t* d_seg = nullptr;
-  size_t cap_seg = 0;
-  Desc* d_desc = nullptr;
-  size_t cap_desc = 0;
-  void* d_out = nullptr;
-  size_t cap_out = 0;
-  uint64_t* d_hash = nullptr;
-  size_t cap_hash = 0;
-  // per-pass event timing (okv_profile)
-  int variant = 3;  // diagnostic ablation selector (OKV_COPY_VARIANT)
-  uint32_t gather_grid = 0;  // 0: one workgroup per block; else persistent grid size
-  bool prof = false;
-  std::vector<hipEvent_t> ev;  // 4 per timed call
-  size_t ev_used = 0;
-  double prof_ms[3] = {0, 0, 0};
-  uint64_t prof_calls = 0;
-};
-
 namespace {
-
-int set_err(okv_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
-  if (c) {
-    c->err = what;
-    if (e != hipSuccess) {
-      c->err += ": ";
-      c->err += hipGetErrorString(e);
-    }
-  }
-  return code;
-}
-
-#define OKV_HIP(call)                                             \
-  do {                                                            \
-    hipError_t e_ = (call);                                       \
-    if (e_ != hipSuccess) return set_err(ctx, OKV_E_HIP, #call, e_); \
-  } while (0)
-
-int grow(okv_ctx* ctx, void** p, size_t* cap, size_t need) {
-  if (need <= *cap && *p) return OKV_OK;
-  if (*p) {
-    OKV_HIP(hipStreamSynchronize(ctx->stream));
-    OKV_HIP(hipFree(*p));
-    *p = nullptr;
-  }
-  size_t c = std::max<size_t>(need, 4096);
-  c = (c + 4095) & ~size_t(4095);
-  OKV_HIP(hipMalloc(p, c));
-  *cap = c;
-  return OKV_OK;
-}
 
 int ensure_blocks(okv_ctx* ctx, uint32_t nblk) {
   const size_t n = std::max<size_t>(nblk, 1);
@@ -1128,6 +1054,7 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->d_desc);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_hash);
+  okv::enc_release(ctx);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1229,9 +1156,7 @@ int okv_hash_blocks(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes,
     d_h = ctx->d_hash;
   }
   if (nblk) {
-    const uint64_t threads = uint64_t(nblk) * 4;
-    hipLaunchKernelGGL(okv_hash_kernel, dim3(uint32_t((threads + kThreads - 1) / kThreads)),
-                       dim3(kThreads), 0, ctx->stream, d_seg, seg_bytes, d_desc, nblk, d_h);
+    launch_hash(ctx->stream, d_seg, seg_bytes, d_desc, nblk, d_h);
     OKV_HIP(hipGetLastError());
   }
   if (!(flags & OKV_F_DEVICE_PTRS)) {

@@ -1,0 +1,1196 @@
+// okv_encode.hip -- MI355X (gfx950) segment encode: SegmentWriter.WriteRow x n
+// followed by Close, for a batch of rows already in HBM.
+//
+// The reference writer (/root/reference/sst/segment_writer.go:80-328) appends
+// each framed row [u16 LE klen][u32 LE vlen][key][value] to the open block and
+// flushes it once its length reaches DataBlockThresholdBytes (:138-143); the
+// flush pads it to (len/DataBlockSize + 1) * DataBlockSize bytes (Q2,
+// :171-182), hashes the padded block with XXH64 (:185) and appends a BlockStat
+// (block_stat.go:9-42).  Close writes the meta block (:284-328) and the
+// 25-byte trailer (:226-276).
+//
+// The greedy cut is a chain: the block starting at row a ends at the first
+// row b with P(b) - P(a-1) >= T (P = inclusive prefix of record sizes), and
+// the next block starts at b+1.  Launches (DESIGN.md "Encode"):
+//   E1 okv_enc_size_kernel   record sizes, 2048-row tile scans, empty-key check
+//   E2 okv_enc_scan_kernel   tile totals -> tile prefixes (one workgroup)
+//   E3 okv_enc_next_kernel   next(a) - a for every row: 2048-row tiles stage
+//                            P over the tile + 2048 rows of lookahead in LDS and
+//                            merge targets P(a-1)+T against it (global
+//                            galloping search past the window)
+//   E4 okv_enc_jump0_kernel  per chunk of C rows and entry offset j < W (W =
+//                            longest block in rows): walk next() to the chunk
+//                            end -> (exit offset, blocks started)
+//   E5 okv_enc_jump_kernel   pointer doubling of those tables over chunks
+//   E6 okv_enc_resolve_kernel the chain's entry and block count per chunk
+//   E7 okv_enc_emit_kernel   block first rows
+//   E8 okv_enc_stat_kernel   OriginalSize, BlockSize, meta entry sizes + scans
+//   E9 okv_enc_offset_kernel BlockStat.Offset and meta entry offsets
+//   E10 okv_enc_pack_kernel  one workgroup per block: every lane assembles
+//                            aligned 16-byte chunks of the padded block
+//                            (header bytes synthesised, key/value bytes from
+//                            two aligned loads + funnel) and stores them whole
+//   E11 okv_hash_kernel      XXH64 per block (shared with the decode)
+//   E12 okv_enc_meta_kernel  block index entries + meta head
+// The meta block's XXH64 is one sequential hash; it runs on the host
+// (okv_encode_close).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "okv_ctx.hpp"
+#include "okv_kernels.hpp"
+#include "okv_sst.h"
+
+extern "C" uint64_t okv_xxh64(const void* data, size_t len, uint64_t seed);
+
+namespace okv {
+
+constexpr int kEItems = 8;
+constexpr uint32_t kETile = kThreads * kEItems;  // rows (or blocks) per scan tile
+constexpr uint32_t kLook = 2048;                 // lookahead rows staged by E3
+constexpr uint32_t kPackRows = 512;              // rows per LDS batch in E10
+constexpr uint64_t kNone = ~uint64_t(0);
+
+struct EncTotals {
+  unsigned long long min_size;    // smallest record (6 + k + v)
+  unsigned long long bad_row;     // first row with an empty key (kNone: none)
+  unsigned long long wmax;        // max over rows of next(a) - a
+  unsigned long long total_raw;   // P(n-1)
+  unsigned long long nb;          // blocks
+  unsigned long long data_bytes;  // sum of BlockSize
+  unsigned long long meta_ent;    // sum of meta index entry sizes
+  unsigned long long last_raw;    // OriginalSize of the last block (Q1)
+  unsigned long long head;        // meta head bytes (keys, bloom, compression, count)
+  unsigned long long pad[7];
+};
+
+struct EncScratch {
+  uint64_t* pl = nullptr;        // [n] tile-local inclusive prefix of record sizes
+  uint32_t* nx = nullptr;        // [n] next(a) - a
+  size_t cap_rows = 0;
+  uint64_t* tile_tot = nullptr;  // [ntiles]
+  uint64_t* tile_pre = nullptr;  // [ntiles]
+  size_t cap_tiles = 0;
+  uint32_t* jt = nullptr;        // [levels][nch][W] exit offsets
+  uint32_t* jb = nullptr;        // [levels][nch][W] blocks started
+  size_t cap_jump = 0;
+  uint32_t* entry = nullptr;     // [nch]
+  uint64_t* kbase = nullptr;     // [nch]
+  size_t cap_chunks = 0;
+  uint64_t* first = nullptr;     // [nb+1]
+  Desc* desc = nullptr;          // [nb]
+  uint64_t* hash = nullptr;      // [nb]
+  uint64_t* bsl = nullptr;       // [nb] tile-local inclusive BlockSize scan
+  uint64_t* esl = nullptr;       // [nb] tile-local inclusive meta entry size scan
+  uint64_t* moff = nullptr;      // [nb] meta entry offsets (relative to the meta block)
+  size_t cap_blocks = 0;
+  uint64_t* btile = nullptr;     // [4][nbtiles]: BlockSize tot/pre, entry tot/pre
+  size_t cap_btiles = 0;
+  EncTotals* d_tot = nullptr;
+  EncTotals* h_tot = nullptr;    // pinned
+  // host-mode staging
+  uint8_t* d_in = nullptr;
+  size_t cap_in = 0;
+  uint8_t* d_outseg = nullptr;
+  size_t cap_outseg = 0;
+  std::vector<uint8_t> meta_host;
+  // profiling (okv_encode_profile_read): cut, pack, hash, meta
+  std::vector<hipEvent_t> ev;
+  size_t ev_used = 0;
+  double ms[4] = {0, 0, 0, 0};
+  uint64_t calls = 0;
+};
+
+void enc_release(okv_ctx* ctx) {
+  EncScratch* e = ctx->enc;
+  if (!e) return;
+  void* ps[] = {e->pl, e->nx, e->tile_tot, e->tile_pre, e->jt, e->jb, e->entry, e->kbase,
+                e->first, e->desc, e->hash, e->bsl, e->esl, e->moff, e->btile, e->d_tot,
+                e->d_in, e->d_outseg};
+  for (void* p : ps)
+    if (p) (void)hipFree(p);
+  if (e->h_tot) (void)hipHostFree(e->h_tot);
+  for (hipEvent_t v : e->ev) (void)hipEventDestroy(v);
+  delete e;
+  ctx->enc = nullptr;
+}
+
+// ---------------------------------------------------------------------------
+// Shared device helpers
+// ---------------------------------------------------------------------------
+// P(i) = sum of record sizes of rows 0..i (P(-1) = 0).
+__device__ __forceinline__ uint64_t Pg(const uint64_t* __restrict__ pl,
+                                       const uint64_t* __restrict__ tile_pre, int64_t i) {
+  return i < 0 ? 0 : pl[i] + tile_pre[uint64_t(i) / kETile];
+}
+
+// Workgroup exclusive scan of one u64 per thread (kThreads threads); also
+// returns the workgroup total.  `sm` holds kThreads/64 + 1 entries.
+__device__ __forceinline__ uint64_t wg_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t inc = wave_incl_scan(v, lane);
+  if (lane == 63) sm[wave] = inc;
+  __syncthreads();
+  uint64_t before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) {
+    const uint64_t t = sm[w];
+    before += (w < wave) ? t : 0;
+    tot += t;
+  }
+  __syncthreads();
+  total = tot;
+  return before + inc - v;
+}
+
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t o = __shfl_xor(v, d, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t o = __shfl_xor(v, d, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+__global__ void okv_enc_init_kernel(EncTotals* t) {
+  t->min_size = kNone;
+  t->bad_row = kNone;
+  t->wmax = 0;
+  t->total_raw = 0;
+  t->nb = 0;
+  t->data_bytes = 0;
+  t->meta_ent = 0;
+  t->last_raw = 0;
+  t->head = 0;
+}
+
+// ---------------------------------------------------------------------------
+// E1: record sizes (WriteRow :121-125 frames 6 + len(key) + len(val) bytes),
+// tile-local inclusive scan, empty-key check (:89-91), smallest record.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void okv_enc_size_kernel(
+    const uint16_t* __restrict__ key_len, const uint32_t* __restrict__ val_len, uint64_t n,
+    uint64_t* __restrict__ pl, uint64_t* __restrict__ tile_tot, EncTotals* __restrict__ tot) {
+  __shared__ uint64_t sm[kThreads / 64 + 1];
+  const uint64_t base = uint64_t(blockIdx.x) * kETile + uint64_t(threadIdx.x) * kEItems;
+  uint64_t loc[kEItems];
+  uint64_t sum = 0, mn = kNone, bad = kNone;
+#pragma unroll
+  for (int i = 0; i < kEItems; ++i) {
+    const uint64_t r = base + i;
+    if (r < n) {
+      const uint32_t kl = key_len[r];
+      const uint64_t s = 6u + uint64_t(kl) + uint64_t(val_len[r]);
+      if (kl == 0 && r < bad) bad = r;
+      mn = s < mn ? s : mn;
+      sum += s;
+    }
+    loc[i] = sum;
+  }
+  uint64_t total;
+  const uint64_t ex = wg_excl_scan(sum, sm, total);
+#pragma unroll
+  for (int i = 0; i < kEItems; ++i)
+    if (base + i < n) pl[base + i] = ex + loc[i];
+  if (threadIdx.x == 0) tile_tot[blockIdx.x] = total;
+  mn = wave_min64(mn);
+  bad = wave_min64(bad);
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&tot->min_size, (unsigned long long)mn);
+    if (bad != kNone) atomicMin(&tot->bad_row, (unsigned long long)bad);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// E2: one workgroup of 1024 threads: exclusive scan of n u64 values.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void okv_enc_scan_kernel(const uint64_t* __restrict__ in,
+                                                            uint64_t n,
+                                                            uint64_t* __restrict__ out,
+                                                            unsigned long long* __restrict__ total) {
+  __shared__ uint64_t sm[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t carry = 0;
+  for (uint64_t b = 0; b < n; b += 1024) {
+    const uint64_t i = b + threadIdx.x;
+    const uint64_t v = i < n ? in[i] : 0;
+    const uint64_t inc = wave_incl_scan(v, lane);
+    if (lane == 63) sm[wave] = inc;
+    __syncthreads();
+    uint64_t before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      const uint64_t t = sm[w];
+      before += (w < wave) ? t : 0;
+      tot += t;
+    }
+    if (i < n) out[i] = carry + before + inc - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && total) *total = carry;
+}
+
+// ---------------------------------------------------------------------------
+// E3: next(a) = 1 + min{b >= a : P(b) >= P(a-1) + T}, or n if none
+// (WriteRow's `blockBuffer.Len() >= DataBlockThresholdBytes`, :138).
+// ---------------------------------------------------------------------------
+__device__ uint64_t next_far(const uint64_t* __restrict__ pl, const uint64_t* __restrict__ tp,
+                             uint64_t n, uint64_t lo, uint64_t target) {
+  // all rows < lo have P < target; galloping then binary search on HBM
+  uint64_t step = 1, hi;
+  for (;;) {
+    hi = lo + step - 1;
+    if (hi >= n) {
+      hi = n;
+      break;
+    }
+    if (Pg(pl, tp, int64_t(hi)) >= target) break;
+    lo = hi + 1;
+    step <<= 1;
+  }
+  uint64_t L = lo, H = hi;
+  while (L < H) {
+    const uint64_t m = L + (H - L) / 2;
+    if (Pg(pl, tp, int64_t(m)) >= target)
+      H = m;
+    else
+      L = m + 1;
+  }
+  return L >= n ? n : L + 1;
+}
+
+__global__ __launch_bounds__(kThreads) void okv_enc_next_kernel(
+    const uint64_t* __restrict__ pl, const uint64_t* __restrict__ tp, uint64_t n, uint64_t T,
+    uint32_t* __restrict__ nx, EncTotals* __restrict__ tot) {
+  __shared__ uint64_t W[kETile + kLook + 1];
+  const uint64_t cs = uint64_t(blockIdx.x) * kETile;
+  // W[m] = P(cs - 1 + m), m < M
+  const uint64_t M = std::min<uint64_t>(n - cs + 1, kETile + kLook + 1);
+  for (uint32_t m = threadIdx.x; m < M; m += kThreads) W[m] = Pg(pl, tp, int64_t(cs + m) - 1);
+  __syncthreads();
+  const bool complete = cs - 1 + M == n;  // the window reaches the last row
+  const uint32_t a0 = threadIdx.x * kEItems;  // tile-relative first row
+  uint64_t wmax = 0;
+  uint32_t mb = 0;
+  for (int i = 0; i < kEItems; ++i) {
+    const uint32_t ar = a0 + i;
+    if (cs + ar >= n) break;
+    const uint64_t target = W[ar] + T;
+    uint64_t next;
+    if (i == 0) {  // binary search in W[ar+1, M)
+      uint32_t L = ar + 1, H = uint32_t(M);
+      while (L < H) {
+        const uint32_t m = (L + H) >> 1;
+        if (W[m] >= target)
+          H = m;
+        else
+          L = m + 1;
+      }
+      mb = L;
+    } else {  // targets only grow: advance linearly
+      mb = std::max(mb, ar + 1);
+      while (mb < M && W[mb] < target) ++mb;
+    }
+    if (mb < M)
+      next = cs + mb;  // b = cs - 1 + mb, next = b + 1
+    else if (complete)
+      next = n;
+    else
+      next = next_far(pl, tp, n, cs - 1 + M, target);
+    const uint64_t d = next - (cs + ar);
+    nx[cs + ar] = uint32_t(d);
+    wmax = d > wmax ? d : wmax;
+  }
+  wmax = wave_max64(wmax);
+  if ((threadIdx.x & 63) == 0) atomicMax(&tot->wmax, (unsigned long long)wmax);
+}
+
+// ---------------------------------------------------------------------------
+// E4-E7: the block-start chain.  Chunk c = rows [cC, cC + C), C >= W, so a
+// chain leaving chunk c enters chunk c+1 at offset < W.  Level-k tables give,
+// for entry offset j of chunk c, the entry offset after 2^k chunks and the
+// number of blocks started on the way.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void okv_enc_jump0_kernel(const uint32_t* __restrict__ nx,
+                                                                 uint64_t n, uint64_t C,
+                                                                 uint32_t W, uint64_t nch,
+                                                                 uint32_t* __restrict__ jt,
+                                                                 uint32_t* __restrict__ jb) {
+  const uint64_t gid = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  const uint64_t c = gid / W, j = gid % W;
+  if (c >= nch) return;
+  const uint64_t ce = std::min<uint64_t>(n, (c + 1) * C);
+  uint64_t pos = c * C + j;
+  uint32_t cnt = 0;
+  while (pos < ce) {
+    ++cnt;
+    pos += nx[pos];
+  }
+  jt[gid] = uint32_t(pos - ce);
+  jb[gid] = cnt;
+}
+
+__global__ __launch_bounds__(kThreads) void okv_enc_jump_kernel(
+    const uint32_t* __restrict__ jt0, const uint32_t* __restrict__ jb0, uint32_t* __restrict__ jt1,
+    uint32_t* __restrict__ jb1, uint32_t W, uint64_t nch, uint64_t h) {
+  const uint64_t gid = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  const uint64_t c = gid / W;
+  if (c >= nch) return;
+  const uint32_t e = jt0[gid], b = jb0[gid];
+  if (c + h < nch) {
+    const uint64_t g2 = (c + h) * W + e;
+    jt1[gid] = jt0[g2];
+    jb1[gid] = b + jb0[g2];
+  } else {
+    jt1[gid] = e;
+    jb1[gid] = b;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void okv_enc_resolve_kernel(
+    const uint32_t* __restrict__ jt, const uint32_t* __restrict__ jb, uint32_t levels, uint32_t W,
+    uint64_t nch, uint32_t* __restrict__ entry, uint64_t* __restrict__ kbase,
+    EncTotals* __restrict__ tot) {
+  const uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (c >= nch) return;
+  const uint64_t lv = nch * W;
+  uint64_t cur = 0, cnt = 0;
+  uint32_t pos = 0;
+  for (int k = int(levels) - 1; k >= 0; --k) {
+    if ((c >> k) & 1) {
+      const uint64_t idx = uint64_t(k) * lv + cur * W + pos;
+      cnt += jb[idx];
+      pos = jt[idx];
+      cur += uint64_t(1) << k;
+    }
+  }
+  entry[c] = pos;
+  kbase[c] = cnt;
+  if (c == nch - 1) tot->nb = cnt + jb[c * W + pos];
+}
+
+__global__ __launch_bounds__(kThreads) void okv_enc_emit_kernel(
+    const uint32_t* __restrict__ nx, uint64_t n, uint64_t C, uint64_t nch,
+    const uint32_t* __restrict__ entry, const uint64_t* __restrict__ kbase,
+    uint64_t* __restrict__ first) {
+  const uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (c >= nch) return;
+  const uint64_t ce = std::min<uint64_t>(n, (c + 1) * C);
+  uint64_t pos = c * C + entry[c], k = kbase[c];
+  while (pos < ce) {
+    first[k++] = pos;
+    pos += nx[pos];
+  }
+  if (c == nch - 1) first[k] = n;
+}
+
+// ---------------------------------------------------------------------------
+// E8: per block OriginalSize (:160-163), BlockSize (Q2: len + DBS - len % DBS,
+// :171-182), CompressedSize (LZ4 flag: the raw length, :165-167), meta index
+// entry size (2 + len(FirstKey) + 40, block_stat.go:27-42) and tile scans.
+// ---------------------------------------------------------------------------
+struct StatParams {
+  const uint64_t* first;
+  const uint64_t* pl;
+  const uint64_t* tp;
+  const uint16_t* key_len;
+  uint64_t nb, D;
+  int lz4;
+  Desc* desc;
+  uint64_t* bsl;
+  uint64_t* esl;
+  uint64_t* btile_tot;
+  uint64_t* etile_tot;
+  EncTotals* tot;
+};
+
+__global__ __launch_bounds__(kThreads) void okv_enc_stat_kernel(StatParams P) {
+  __shared__ uint64_t sm[kThreads / 64 + 1];
+  const uint64_t base = uint64_t(blockIdx.x) * kETile + uint64_t(threadIdx.x) * kEItems;
+  uint64_t lb[kEItems], le[kEItems];
+  uint64_t sb = 0, se = 0;
+#pragma unroll
+  for (int i = 0; i < kEItems; ++i) {
+    const uint64_t k = base + i;
+    if (k < P.nb) {
+      const uint64_t r0 = P.first[k], r1 = P.first[k + 1];
+      const uint64_t raw = Pg(P.pl, P.tp, int64_t(r1) - 1) - Pg(P.pl, P.tp, int64_t(r0) - 1);
+      const uint64_t bs = (raw / P.D + 1) * P.D;
+      const uint64_t es = 42u + P.key_len[r0];
+      Desc d;
+      d.offset = 0;
+      d.block_size = bs;
+      d.original_size = raw;
+      d.compressed_size = P.lz4 ? raw : 0;
+      P.desc[k] = d;
+      sb += bs;
+      se += es;
+      if (k == P.nb - 1) P.tot->last_raw = raw;
+    }
+    lb[i] = sb;
+    le[i] = se;
+  }
+  uint64_t tb, te;
+  const uint64_t xb = wg_excl_scan(sb, sm, tb);
+  const uint64_t xe = wg_excl_scan(se, sm, te);
+#pragma unroll
+  for (int i = 0; i < kEItems; ++i) {
+    if (base + i < P.nb) {
+      P.bsl[base + i] = xb + lb[i];
+      P.esl[base + i] = xe + le[i];
+    }
+  }
+  if (threadIdx.x == 0) {
+    P.btile_tot[blockIdx.x] = tb;
+    P.etile_tot[blockIdx.x] = te;
+  }
+}
+
+// E9: Offset = running sum of BlockSize (:197-203); meta entry offsets.
+__global__ __launch_bounds__(kThreads) void okv_enc_offset_kernel(
+    Desc* __restrict__ desc, const uint64_t* __restrict__ bsl, const uint64_t* __restrict__ esl,
+    const uint64_t* __restrict__ btile_pre, const uint64_t* __restrict__ etile_pre, uint64_t nb,
+    const uint16_t* __restrict__ key_len, uint64_t n, const uint64_t* __restrict__ first,
+    uint64_t* __restrict__ moff, EncTotals* __restrict__ tot) {
+  const uint64_t k = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  // meta head: u16+FirstKey, u16+lastKey, bloom byte, compression byte,
+  // index-type byte, u64 entry count (:288-325)
+  const uint64_t head = 2u + key_len[0] + 2u + key_len[n - 1] + 3u + 8u;
+  if (k == 0) tot->head = head;
+  if (k >= nb) return;
+  const uint64_t t = k / kETile;
+  desc[k].offset = btile_pre[t] + bsl[k] - desc[k].block_size;
+  moff[k] = head + etile_pre[t] + esl[k] - (42u + key_len[first[k]]);
+}
+
+// ---------------------------------------------------------------------------
+// E10: pack.  One workgroup per block; lane l of a pass owns destination
+// chunk q (16 bytes at Offset + 16q) and assembles it from the records that
+// overlap it: header bytes synthesised from (klen, vlen), key and value bytes
+// gathered from the arenas with two aligned 16-byte loads + funnel.  Chunks
+// past OriginalSize are the zero padding.  Every chunk is stored whole, once.
+// ---------------------------------------------------------------------------
+struct PackParams {
+  const uint8_t* key_arena;
+  const uint64_t* key_off;
+  const uint16_t* key_len;
+  const uint8_t* val_arena;
+  const uint64_t* val_off;
+  const uint32_t* val_len;
+  const uint64_t* pl;
+  const uint64_t* tp;
+  const uint64_t* first;
+  const Desc* desc;
+  uint8_t* seg;
+};
+
+struct __align__(16) PackSmem {
+  uint64_t rel[kPackRows + 1];  // record start within the block
+  uint64_t ko[kPackRows];
+  uint64_t vo[kPackRows];
+  uint32_t kl[kPackRows];
+  uint32_t vl[kPackRows];
+};
+
+// Field bytes src[0, flen) land at window offsets [d, d + flen); merge the
+// part inside [0, 16) into out.  Only 16-byte lines holding a needed byte
+// are loaded.
+__device__ __forceinline__ void place_field(uint4& out, const uint8_t* src, int64_t d,
+                                            uint64_t flen) {
+  const int64_t lo = d > 0 ? d : 0;
+  const int64_t hi64 = d + int64_t(flen);
+  const int64_t hi = hi64 < 16 ? hi64 : 16;
+  if (lo >= hi) return;
+  const uintptr_t v = reinterpret_cast<uintptr_t>(src) - uintptr_t(d);  // window byte 0
+  const uintptr_t a = v & ~uintptr_t(15);
+  const uint32_t s = uint32_t(v & 15);
+  const uintptr_t safe = (v + uintptr_t(lo)) & ~uintptr_t(15);  // holds a needed byte
+  const bool n0 = int64_t(16 - s) > lo;
+  const bool n1 = s != 0 && hi > int64_t(16 - s);
+  const uint4 x = *reinterpret_cast<const uint4*>(n0 ? a : safe);
+  const uint4 y = *reinterpret_cast<const uint4*>(n1 ? a + 16 : safe);
+  const uint32_t m0 = 0u - uint32_t(n0), m1 = 0u - uint32_t(n1);
+  const uint4 w = funnel32(make_uint4(x.x & m0, x.y & m0, x.z & m0, x.w & m0),
+                           make_uint4(y.x & m1, y.y & m1, y.z & m1, y.w & m1), s);
+  out = merge_bytes(out, w, int32_t(lo), int32_t(hi));
+}
+
+// The 6 header bytes [u16 klen][u32 vlen] at window offset d (-5 <= d <= 15).
+__device__ __forceinline__ void place_header(uint4& out, uint32_t kl, uint32_t vl, int64_t d) {
+  const int64_t lo = d > 0 ? d : 0;
+  const int64_t hi = d + 6 < 16 ? d + 6 : 16;
+  if (lo >= hi) return;
+  const uint4 H = make_uint4(kl | (vl << 16), vl >> 16, 0, 0);
+  const uint4 Z = make_uint4(0, 0, 0, 0);
+  const uint4 w = d > 0 ? funnel32(Z, H, uint32_t(16 - d)) : funnel32(H, Z, uint32_t(-d));
+  out = merge_bytes(out, w, int32_t(lo), int32_t(hi));
+}
+
+__global__ __launch_bounds__(kThreads) void okv_enc_pack_kernel(PackParams P) {
+  __shared__ PackSmem sm;
+  const uint64_t k = blockIdx.x;
+  const Desc d = P.desc[k];
+  const uint64_t r0 = P.first[k], r1 = P.first[k + 1];
+  const uint64_t base = Pg(P.pl, P.tp, int64_t(r0) - 1);
+  const uint64_t L = d.original_size, S = d.block_size;
+  uint8_t* dst = P.seg + d.offset;
+  for (uint64_t b0 = r0;; b0 += kPackRows) {
+    const uint64_t b1 = std::min<uint64_t>(r1, b0 + kPackRows);
+    const uint32_t nbat = uint32_t(b1 - b0);
+    for (uint32_t i = threadIdx.x; i <= nbat; i += kThreads) {
+      const uint64_t g = b0 + i;
+      sm.rel[i] = Pg(P.pl, P.tp, int64_t(g) - 1) - base;
+      if (i < nbat) {
+        sm.ko[i] = P.key_off[g];
+        sm.kl[i] = P.key_len[g];
+        sm.vo[i] = P.val_off[g];
+        sm.vl[i] = P.val_len[g];
+      }
+    }
+    __syncthreads();
+    const bool last = b1 == r1;
+    const uint64_t q0 = (sm.rel[0] + 15) >> 4;
+    const uint64_t q1 = last ? (S >> 4) : ((sm.rel[nbat] + 15) >> 4);
+    for (uint64_t q = q0 + threadIdx.x; q < q1; q += kThreads) {
+      const uint64_t pos = q << 4;
+      uint4 out = make_uint4(0, 0, 0, 0);
+      if (pos < L) {
+        // last record of the batch starting at or before pos
+        uint32_t lo = 0, hi = nbat;  // rel[lo] <= pos < rel[hi]
+        while (hi - lo > 1) {
+          const uint32_t m = (lo + hi) >> 1;
+          if (sm.rel[m] <= pos)
+            lo = m;
+          else
+            hi = m;
+        }
+        for (uint64_t i = lo;; ++i) {
+          const uint64_t g = b0 + i;
+          if (g >= r1) break;
+          uint64_t rs, ko, vo;
+          uint32_t kl, vl;
+          if (i < nbat) {
+            rs = sm.rel[i];
+            ko = sm.ko[i];
+            vo = sm.vo[i];
+            kl = sm.kl[i];
+            vl = sm.vl[i];
+          } else {  // the chunk runs into the next batch
+            rs = Pg(P.pl, P.tp, int64_t(g) - 1) - base;
+            ko = P.key_off[g];
+            vo = P.val_off[g];
+            kl = P.key_len[g];
+            vl = P.val_len[g];
+          }
+          if (rs >= pos + 16) break;
+          const int64_t dh = int64_t(rs) - int64_t(pos);
+          place_header(out, kl, vl, dh);
+          place_field(out, P.key_arena + ko, dh + 6, kl);
+          place_field(out, P.val_arena + vo, dh + 6 + kl, vl);
+        }
+      }
+      *reinterpret_cast<uint4*>(dst + pos) = out;
+    }
+    if (last) break;
+    __syncthreads();
+  }
+}
+
+// E10 (general DataBlockSize, not a multiple of 16): one byte per lane.
+__global__ __launch_bounds__(kThreads) void okv_enc_pack_bytes_kernel(PackParams P, uint64_t nb,
+                                                                      uint64_t data_bytes) {
+  for (uint64_t x = uint64_t(blockIdx.x) * kThreads + threadIdx.x; x < data_bytes;
+       x += uint64_t(gridDim.x) * kThreads) {
+    uint64_t lo = 0, hi = nb;  // block: desc[lo].offset <= x
+    while (hi - lo > 1) {
+      const uint64_t m = (lo + hi) >> 1;
+      if (P.desc[m].offset <= x)
+        lo = m;
+      else
+        hi = m;
+    }
+    const Desc d = P.desc[lo];
+    const uint64_t p = x - d.offset;
+    uint8_t byte = 0;
+    if (p < d.original_size) {
+      const uint64_t r0 = P.first[lo], r1 = P.first[lo + 1];
+      const uint64_t base = Pg(P.pl, P.tp, int64_t(r0) - 1);
+      uint64_t a = r0, b = r1;  // row: P(a-1) - base <= p
+      while (b - a > 1) {
+        const uint64_t m = (a + b) >> 1;
+        if (Pg(P.pl, P.tp, int64_t(m) - 1) - base <= p)
+          a = m;
+        else
+          b = m;
+      }
+      const uint64_t o = p - (Pg(P.pl, P.tp, int64_t(a) - 1) - base);
+      const uint32_t kl = P.key_len[a], vl = P.val_len[a];
+      if (o < 2)
+        byte = uint8_t(kl >> (8 * o));
+      else if (o < 6)
+        byte = uint8_t(vl >> (8 * (o - 2)));
+      else if (o < 6 + uint64_t(kl))
+        byte = P.key_arena[P.key_off[a] + (o - 6)];
+      else
+        byte = P.val_arena[P.val_off[a] + (o - 6 - kl)];
+    }
+    P.seg[x] = byte;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// E12: meta block = head + one entry per block (BlockStat.toBytes,
+// block_stat.go:27-42), written at seg + data_bytes.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void put_le(uint8_t* p, uint64_t v, int nbytes) {
+  for (int i = 0; i < nbytes; ++i) p[i] = uint8_t(v >> (8 * i));
+}
+__device__ __forceinline__ void put_bytes(uint8_t* p, const uint8_t* s, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) p[i] = s[i];
+}
+
+struct MetaParams {
+  const uint8_t* key_arena;
+  const uint64_t* key_off;
+  const uint16_t* key_len;
+  uint64_t n;
+  const uint64_t* first;
+  const Desc* desc;
+  const uint64_t* hash;
+  const uint64_t* moff;
+  uint64_t nb;
+  int comp_byte;
+  uint8_t* meta;
+};
+
+__global__ __launch_bounds__(kThreads) void okv_enc_meta_kernel(MetaParams P) {
+  const uint64_t k = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (k == 0) {  // generateMetaBlock head (:288-325)
+    uint8_t* p = P.meta;
+    const uint32_t k0 = P.key_len[0], kz = P.key_len[P.n - 1];
+    put_le(p, k0, 2);
+    put_bytes(p + 2, P.key_arena + P.key_off[0], k0);
+    p += 2 + k0;
+    put_le(p, kz, 2);
+    put_bytes(p + 2, P.key_arena + P.key_off[P.n - 1], kz);
+    p += 2 + kz;
+    p[0] = 0;  // no bloom filter
+    p[1] = uint8_t(P.comp_byte);
+    p[2] = 0;  // not a partitioned block index
+    put_le(p + 3, P.nb, 8);
+  }
+  if (k >= P.nb) return;
+  uint8_t* p = P.meta + P.moff[k];
+  const uint64_t r = P.first[k];
+  const uint32_t kl = P.key_len[r];
+  put_le(p, kl, 2);
+  put_bytes(p + 2, P.key_arena + P.key_off[r], kl);
+  p += 2 + kl;
+  const Desc d = P.desc[k];
+  put_le(p, d.offset, 8);
+  put_le(p + 8, d.block_size, 8);
+  put_le(p + 16, d.original_size, 8);
+  put_le(p + 24, d.compressed_size, 8);
+  put_le(p + 32, P.hash[k], 8);
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic fixed-shape rows (oracle/pyoracle.py rows_fixed).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, uint64_t w) {
+  uint64_t z = seed + (w + 1) * 0x9E3779B97F4A7C15ULL;  // state after draw w
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kThreads) void okv_synth_fixed_kernel(
+    uint64_t seed, uint64_t first_row, uint64_t n, uint32_t kl, uint32_t vl,
+    uint8_t* __restrict__ key_arena, uint64_t* __restrict__ key_off,
+    uint16_t* __restrict__ key_len, uint8_t* __restrict__ val_arena,
+    uint64_t* __restrict__ val_off, uint32_t* __restrict__ val_len) {
+  const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t row = first_row + i;
+  uint8_t* k = key_arena + i * kl;
+  for (uint32_t b = 0; b < kl; ++b) {
+    const uint32_t from_end = kl - 1 - b;
+    k[b] = from_end < 8 ? uint8_t(row >> (8 * from_end)) : 0;
+  }
+  const uint32_t wpr = (vl + 7) / 8;
+  uint8_t* v = val_arena + i * vl;
+  for (uint32_t w = 0; w < wpr; ++w) {
+    const uint64_t x = splitmix_at(seed, row * wpr + w);
+    const uint32_t nbytes = std::min<uint32_t>(8, vl - 8 * w);
+    if (nbytes == 8 && (reinterpret_cast<uintptr_t>(v + 8 * w) & 7) == 0)
+      *reinterpret_cast<uint64_t*>(v + 8 * w) = x;
+    else
+      for (uint32_t b = 0; b < nbytes; ++b) v[8 * w + b] = uint8_t(x >> (8 * b));
+  }
+  key_off[i] = i * kl;
+  key_len[i] = uint16_t(kl);
+  val_off[i] = i * vl;
+  val_len[i] = vl;
+}
+
+}  // namespace okv
+
+// ===========================================================================
+// Host orchestration
+// ===========================================================================
+namespace okv {
+namespace {
+
+struct DevRows {
+  const uint8_t* ka;
+  const uint64_t* ko;
+  const uint16_t* kl;
+  const uint8_t* va;
+  const uint64_t* vo;
+  const uint32_t* vl;
+  uint64_t n;
+};
+
+int dev_realloc(okv_ctx* ctx, void** p, size_t bytes) {
+  if (*p) {
+    OKV_HIP(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(*p);
+    *p = nullptr;
+  }
+  OKV_HIP(hipMalloc(p, std::max<size_t>(bytes, 256)));
+  return OKV_OK;
+}
+
+int enc_scratch(okv_ctx* ctx, EncScratch** out) {
+  if (!ctx->enc) {
+    EncScratch* e = new EncScratch();
+    ctx->enc = e;
+    OKV_HIP(hipMalloc(&e->d_tot, sizeof(EncTotals)));
+    OKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&e->h_tot), sizeof(EncTotals), 0));
+  }
+  *out = ctx->enc;
+  return OKV_OK;
+}
+
+int ensure_rows(okv_ctx* ctx, EncScratch* e, uint64_t n) {
+  const uint64_t nt = (n + kETile - 1) / kETile + 1;
+  int rc;
+  if (n > e->cap_rows || !e->pl) {
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->pl), n * 8))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->nx), n * 4))) return rc;
+    e->cap_rows = n;
+  }
+  if (nt > e->cap_tiles || !e->tile_tot) {
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->tile_tot), nt * 8))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->tile_pre), nt * 8))) return rc;
+    e->cap_tiles = nt;
+  }
+  return OKV_OK;
+}
+
+int ensure_jump(okv_ctx* ctx, EncScratch* e, size_t entries, uint64_t nch) {
+  int rc;
+  if (entries > e->cap_jump || !e->jt) {
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->jt), entries * 4))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->jb), entries * 4))) return rc;
+    e->cap_jump = entries;
+  }
+  if (nch > e->cap_chunks || !e->entry) {
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->entry), nch * 4))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->kbase), nch * 8))) return rc;
+    e->cap_chunks = nch;
+  }
+  return OKV_OK;
+}
+
+int ensure_blocks_enc(okv_ctx* ctx, EncScratch* e, uint64_t nb) {
+  const uint64_t nbt = (nb + kETile - 1) / kETile + 1;
+  int rc;
+  if (nb + 1 > e->cap_blocks || !e->first) {
+    const size_t c = nb + 1;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->first), c * 8))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->desc), c * sizeof(Desc)))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->hash), c * 8))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->bsl), c * 8))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->esl), c * 8))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->moff), c * 8))) return rc;
+    e->cap_blocks = c;
+  }
+  if (nbt > e->cap_btiles || !e->btile) {
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->btile), 4 * nbt * 8))) return rc;
+    e->cap_btiles = nbt;
+  }
+  return OKV_OK;
+}
+
+int read_enc_totals(okv_ctx* ctx, EncScratch* e) {
+  OKV_HIP(hipMemcpyAsync(e->h_tot, e->d_tot, sizeof(EncTotals), hipMemcpyDeviceToHost,
+                         ctx->stream));
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  return OKV_OK;
+}
+
+void enc_mark(okv_ctx* ctx, EncScratch* e, int k) {  // 5 events per profiled call
+  if (!ctx->prof) return;
+  while (e->ev.size() < e->ev_used + 5) {
+    hipEvent_t v;
+    if (hipEventCreate(&v) != hipSuccess) return;
+    e->ev.push_back(v);
+  }
+  (void)hipEventRecord(e->ev[e->ev_used + k], ctx->stream);
+  if (k == 4) e->ev_used += 5;
+}
+
+uint32_t ceil_div(uint64_t a, uint64_t b) { return uint32_t((a + b - 1) / b); }
+
+struct Plan {
+  uint64_t nb, data_bytes, meta_bytes, file_bytes, last_raw;
+};
+
+// Block boundaries, BlockStat sizes/offsets and meta layout (E1-E9).
+int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opts& o, Plan* pl,
+             uint64_t* bad_row) {
+  const uint64_t n = R.n;
+  const uint64_t T = o.threshold_bytes, D = o.block_size;
+  const uint32_t ntiles = ceil_div(n, kETile);
+  int rc;
+  if ((rc = ensure_rows(ctx, e, n))) return rc;
+  enc_mark(ctx, e, 0);
+  hipLaunchKernelGGL(okv_enc_init_kernel, dim3(1), dim3(1), 0, ctx->stream, e->d_tot);
+  hipLaunchKernelGGL(okv_enc_size_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, R.kl,
+                     R.vl, n, e->pl, e->tile_tot, e->d_tot);
+  hipLaunchKernelGGL(okv_enc_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, e->tile_tot,
+                     uint64_t(ntiles), e->tile_pre, &e->d_tot->total_raw);
+  hipLaunchKernelGGL(okv_enc_next_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, e->pl,
+                     e->tile_pre, n, T, e->nx, e->d_tot);
+  OKV_HIP(hipGetLastError());
+  if ((rc = read_enc_totals(ctx, e))) return rc;
+  if (e->h_tot->bad_row != kNone) {
+    *bad_row = e->h_tot->bad_row;
+    return set_err(ctx, OKV_W_INVALID_KEY, "key cannot be empty (ErrInvalidKey)");
+  }
+  // chunking for the chain: C >= W rows per chunk
+  const uint64_t W = std::max<uint64_t>(1, e->h_tot->wmax);
+  uint64_t C = 4096;
+  while (C < W) C <<= 1;
+  const uint64_t nch = (n + C - 1) / C;
+  uint32_t levels = 0;
+  while ((uint64_t(1) << levels) < nch) ++levels;  // 2^levels >= nch
+  const uint64_t lv = nch * W;
+  if ((rc = ensure_jump(ctx, e, lv * std::max<uint32_t>(levels, 1), nch))) return rc;
+  hipLaunchKernelGGL(okv_enc_jump0_kernel, dim3(ceil_div(lv, kThreads)), dim3(kThreads), 0,
+                     ctx->stream, e->nx, n, C, uint32_t(W), nch, e->jt, e->jb);
+  for (uint32_t k = 1; k < levels; ++k)
+    hipLaunchKernelGGL(okv_enc_jump_kernel, dim3(ceil_div(lv, kThreads)), dim3(kThreads), 0,
+                       ctx->stream, e->jt + (k - 1) * lv, e->jb + (k - 1) * lv, e->jt + k * lv,
+                       e->jb + k * lv, uint32_t(W), nch, uint64_t(1) << (k - 1));
+  hipLaunchKernelGGL(okv_enc_resolve_kernel, dim3(ceil_div(nch, kThreads)), dim3(kThreads), 0,
+                     ctx->stream, e->jt, e->jb, levels, uint32_t(W), nch, e->entry, e->kbase,
+                     e->d_tot);
+  OKV_HIP(hipGetLastError());
+  if ((rc = read_enc_totals(ctx, e))) return rc;
+  const uint64_t nb = e->h_tot->nb;
+  if (nb == 0 || nb > n || nb >= (uint64_t(1) << 32))
+    return set_err(ctx, OKV_E_HIP, "encode: inconsistent block count");
+  if ((rc = ensure_blocks_enc(ctx, e, nb))) return rc;
+  const uint32_t nbt = ceil_div(nb, kETile);
+  uint64_t* btot = e->btile;
+  uint64_t* bpre = e->btile + e->cap_btiles;
+  uint64_t* etot = e->btile + 2 * e->cap_btiles;
+  uint64_t* epre = e->btile + 3 * e->cap_btiles;
+  hipLaunchKernelGGL(okv_enc_emit_kernel, dim3(ceil_div(nch, kThreads)), dim3(kThreads), 0,
+                     ctx->stream, e->nx, n, C, nch, e->entry, e->kbase, e->first);
+  StatParams sp;
+  sp.first = e->first;
+  sp.pl = e->pl;
+  sp.tp = e->tile_pre;
+  sp.key_len = R.kl;
+  sp.nb = nb;
+  sp.D = D;
+  sp.lz4 = o.compression == OKV_COMP_LZ4;
+  sp.desc = e->desc;
+  sp.bsl = e->bsl;
+  sp.esl = e->esl;
+  sp.btile_tot = btot;
+  sp.etile_tot = etot;
+  sp.tot = e->d_tot;
+  hipLaunchKernelGGL(okv_enc_stat_kernel, dim3(nbt), dim3(kThreads), 0, ctx->stream, sp);
+  hipLaunchKernelGGL(okv_enc_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, btot,
+                     uint64_t(nbt), bpre, &e->d_tot->data_bytes);
+  hipLaunchKernelGGL(okv_enc_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, etot,
+                     uint64_t(nbt), epre, &e->d_tot->meta_ent);
+  hipLaunchKernelGGL(okv_enc_offset_kernel, dim3(ceil_div(nb, kThreads)), dim3(kThreads), 0,
+                     ctx->stream, e->desc, e->bsl, e->esl, bpre, epre, nb, R.kl, n, e->first,
+                     e->moff, e->d_tot);
+  OKV_HIP(hipGetLastError());
+  if ((rc = read_enc_totals(ctx, e))) return rc;
+  pl->nb = nb;
+  pl->data_bytes = e->h_tot->data_bytes;
+  pl->meta_bytes = e->h_tot->head + e->h_tot->meta_ent;
+  pl->file_bytes = pl->data_bytes + pl->meta_bytes + 25;
+  pl->last_raw = e->h_tot->last_raw;
+  return OKV_OK;
+}
+
+// Data blocks, block hashes and the meta block into seg (E10-E12).
+int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opts& o,
+              const Plan& pl, uint8_t* seg) {
+  enc_mark(ctx, e, 1);
+  PackParams pp;
+  pp.key_arena = R.ka;
+  pp.key_off = R.ko;
+  pp.key_len = R.kl;
+  pp.val_arena = R.va;
+  pp.val_off = R.vo;
+  pp.val_len = R.vl;
+  pp.pl = e->pl;
+  pp.tp = e->tile_pre;
+  pp.first = e->first;
+  pp.desc = e->desc;
+  pp.seg = seg;
+  if (o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0) {
+    hipLaunchKernelGGL(okv_enc_pack_kernel, dim3(uint32_t(pl.nb)), dim3(kThreads), 0,
+                       ctx->stream, pp);
+  } else {
+    const uint32_t g = std::min<uint64_t>(65536, (pl.data_bytes + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(okv_enc_pack_bytes_kernel, dim3(std::max<uint32_t>(g, 1)),
+                       dim3(kThreads), 0, ctx->stream, pp, pl.nb, pl.data_bytes);
+  }
+  enc_mark(ctx, e, 2);
+  launch_hash(ctx->stream, seg, pl.data_bytes, e->desc, uint32_t(pl.nb), e->hash);
+  enc_mark(ctx, e, 3);
+  MetaParams mp;
+  mp.key_arena = R.ka;
+  mp.key_off = R.ko;
+  mp.key_len = R.kl;
+  mp.n = R.n;
+  mp.first = e->first;
+  mp.desc = e->desc;
+  mp.hash = e->hash;
+  mp.moff = e->moff;
+  mp.nb = pl.nb;
+  mp.comp_byte = o.compression == OKV_COMP_LZ4 ? 2 : 0;
+  mp.meta = seg + pl.data_bytes;
+  hipLaunchKernelGGL(okv_enc_meta_kernel, dim3(ceil_div(pl.nb, kThreads)), dim3(kThreads), 0,
+                     ctx->stream, mp);
+  enc_mark(ctx, e, 4);
+  OKV_HIP(hipGetLastError());
+  return OKV_OK;
+}
+
+// The 25-byte trailer (segment_writer.go:226-276): meta offset, XXH64(meta),
+// version 1, magic 69696969696969 (:21).
+void trailer_bytes(uint64_t meta_off, uint64_t meta_hash, uint8_t t[25]) {
+  const uint64_t magic = 69696969696969ULL;
+  for (int i = 0; i < 8; ++i) {
+    t[i] = uint8_t(meta_off >> (8 * i));
+    t[8 + i] = uint8_t(meta_hash >> (8 * i));
+    t[17 + i] = uint8_t(magic >> (8 * i));
+  }
+  t[16] = 1;
+}
+
+int close_device(okv_ctx* ctx, EncScratch* e, okv_encode_out* out) {
+  uint8_t* meta = out->seg + out->data_bytes;
+  e->meta_host.resize(out->meta_bytes);
+  OKV_HIP(hipMemcpyAsync(e->meta_host.data(), meta, out->meta_bytes, hipMemcpyDeviceToHost,
+                         ctx->stream));
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  out->meta_hash = okv_xxh64(e->meta_host.data(), e->meta_host.size(), 0);  // :248
+  static thread_local uint8_t t[25];
+  trailer_bytes(out->data_bytes, out->meta_hash, t);
+  OKV_HIP(hipMemcpyAsync(meta + out->meta_bytes, t, 25, hipMemcpyHostToDevice, ctx->stream));
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  out->file_bytes = out->data_bytes + out->meta_bytes + 25;
+  return OKV_OK;
+}
+
+void close_host(okv_encode_out* out) {
+  uint8_t* meta = out->seg + out->data_bytes;
+  out->meta_hash = okv_xxh64(meta, out->meta_bytes, 0);
+  trailer_bytes(out->data_bytes, out->meta_hash, meta + out->meta_bytes);
+  out->file_bytes = out->data_bytes + out->meta_bytes + 25;
+}
+
+}  // namespace
+}  // namespace okv
+
+// ===========================================================================
+// C-ABI (include/okv_sst.h)
+// ===========================================================================
+using namespace okv;
+
+extern "C" {
+
+int okv_encode_rows(okv_ctx* ctx, const okv_rows* rows, const okv_encode_opts* opts,
+                    okv_encode_out* out, uint32_t flags) {
+  if (!ctx || !rows || !opts || !out) return OKV_E_ARG;
+  out->n_blocks = out->data_bytes = out->meta_bytes = out->file_bytes = 0;
+  out->meta_hash = 0;
+  out->bad_row = kNone;
+  if (opts->compression == OKV_COMP_ZSTD)
+    return set_err(ctx, OKV_W_UNSUPPORTED, "zstd encode not implemented");
+  if (opts->compression != OKV_COMP_NONE && opts->compression != OKV_COMP_LZ4)
+    return set_err(ctx, OKV_E_ARG, "compression");
+  if (opts->block_size == 0) return set_err(ctx, OKV_E_ARG, "block_size == 0");
+  const uint64_t n = rows->n_rows;
+  if (n == 0)  // Close with no open block: Go panics (Q1) or ErrNoRowsWritten (:221)
+    return opts->strict_go ? set_err(ctx, OKV_W_NIL_WRITER, "Close on nil blockWriter (Q1)")
+                           : set_err(ctx, OKV_W_NO_ROWS, "ErrNoRowsWritten");
+  if (n >= (uint64_t(1) << 32) - kETile) return set_err(ctx, OKV_E_ARG, "n_rows >= 2^32");
+  if (!rows->key_off || !rows->key_len || !rows->val_off || !rows->val_len ||
+      (!rows->key_arena && rows->key_arena_bytes) || (!rows->val_arena && rows->val_arena_bytes))
+    return set_err(ctx, OKV_E_ARG, "rows");
+  OKV_HIP(hipSetDevice(ctx->device));
+  EncScratch* e;
+  int rc = enc_scratch(ctx, &e);
+  if (rc) return rc;
+  const bool dev = flags & OKV_F_DEVICE_PTRS;
+  DevRows R;
+  R.n = n;
+  if (dev) {
+    R.ka = rows->key_arena;
+    R.ko = rows->key_off;
+    R.kl = rows->key_len;
+    R.va = rows->val_arena;
+    R.vo = rows->val_off;
+    R.vl = rows->val_len;
+  } else {  // stage the host rows in one device buffer
+    const auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t oka = 0, ova = oka + al(rows->key_arena_bytes),
+                 oko = ova + al(rows->val_arena_bytes), okl = oko + al(n * 8),
+                 ovo = okl + al(n * 2), ovl = ovo + al(n * 8), end = ovl + al(n * 4);
+    if ((rc = grow(ctx, reinterpret_cast<void**>(&e->d_in), &e->cap_in, end + 64))) return rc;
+    uint8_t* b = e->d_in;
+    const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+    if (rows->key_arena_bytes)
+      OKV_HIP(hipMemcpyAsync(b + oka, rows->key_arena, rows->key_arena_bytes, h2d, ctx->stream));
+    if (rows->val_arena_bytes)
+      OKV_HIP(hipMemcpyAsync(b + ova, rows->val_arena, rows->val_arena_bytes, h2d, ctx->stream));
+    OKV_HIP(hipMemcpyAsync(b + oko, rows->key_off, n * 8, h2d, ctx->stream));
+    OKV_HIP(hipMemcpyAsync(b + okl, rows->key_len, n * 2, h2d, ctx->stream));
+    OKV_HIP(hipMemcpyAsync(b + ovo, rows->val_off, n * 8, h2d, ctx->stream));
+    OKV_HIP(hipMemcpyAsync(b + ovl, rows->val_len, n * 4, h2d, ctx->stream));
+    R.ka = b + oka;
+    R.va = b + ova;
+    R.ko = reinterpret_cast<const uint64_t*>(b + oko);
+    R.kl = reinterpret_cast<const uint16_t*>(b + okl);
+    R.vo = reinterpret_cast<const uint64_t*>(b + ovo);
+    R.vl = reinterpret_cast<const uint32_t*>(b + ovl);
+  }
+  Plan pl;
+  uint64_t bad = kNone;
+  rc = enc_plan(ctx, e, R, *opts, &pl, &bad);
+  if (rc == OKV_W_INVALID_KEY) out->bad_row = bad;
+  if (rc) return rc;
+  out->n_blocks = pl.nb;
+  out->data_bytes = pl.data_bytes;
+  out->meta_bytes = pl.meta_bytes;
+  out->file_bytes = pl.file_bytes;
+  if (opts->strict_go && pl.last_raw >= opts->threshold_bytes)
+    return set_err(ctx, OKV_W_NIL_WRITER, "Close on nil blockWriter (Q1): last row closed a block");
+  const bool want_idx = out->blk_first_row || out->blk_desc || out->blk_hash;
+  if (out->seg_cap < pl.file_bytes || (want_idx && out->blk_cap < pl.nb) || !out->seg)
+    return set_err(ctx, OKV_E_CAPACITY, "encode output capacity too small (sizes set)");
+  uint8_t* seg = out->seg;
+  if (!dev) {
+    if ((rc = grow(ctx, reinterpret_cast<void**>(&e->d_outseg), &e->cap_outseg,
+                   pl.file_bytes + 64)))
+      return rc;
+    seg = e->d_outseg;
+  }
+  if ((rc = enc_write(ctx, e, R, *opts, pl, seg))) return rc;
+  const hipMemcpyKind k = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  if (out->blk_first_row)
+    OKV_HIP(hipMemcpyAsync(out->blk_first_row, e->first, (pl.nb + 1) * 8, k, ctx->stream));
+  if (out->blk_desc)
+    OKV_HIP(hipMemcpyAsync(out->blk_desc, e->desc, pl.nb * sizeof(Desc), k, ctx->stream));
+  if (out->blk_hash)
+    OKV_HIP(hipMemcpyAsync(out->blk_hash, e->hash, pl.nb * 8, k, ctx->stream));
+  if (!dev) {
+    OKV_HIP(hipMemcpyAsync(out->seg, seg, pl.data_bytes + pl.meta_bytes, k, ctx->stream));
+    OKV_HIP(hipStreamSynchronize(ctx->stream));
+    if (!(flags & OKV_F_NO_CLOSE)) close_host(out);
+    return OKV_OK;
+  }
+  if (!(flags & OKV_F_NO_CLOSE)) return close_device(ctx, e, out);
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  return OKV_OK;
+}
+
+int okv_encode_close(okv_ctx* ctx, okv_encode_out* out, uint32_t flags) {
+  if (!ctx || !out || !out->seg || !out->meta_bytes) return OKV_E_ARG;
+  if (out->seg_cap < out->data_bytes + out->meta_bytes + 25)
+    return set_err(ctx, OKV_E_CAPACITY, "seg_cap");
+  if (!(flags & OKV_F_DEVICE_PTRS)) {
+    close_host(out);
+    return OKV_OK;
+  }
+  OKV_HIP(hipSetDevice(ctx->device));
+  EncScratch* e;
+  int rc = enc_scratch(ctx, &e);
+  if (rc) return rc;
+  return close_device(ctx, e, out);
+}
+
+int okv_encode_profile_read(okv_ctx* ctx, double* ms, uint64_t* calls) {
+  if (!ctx) return OKV_E_ARG;
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  EncScratch* e = ctx->enc;
+  if (e) {
+    for (size_t i = 0; i + 5 <= e->ev_used; i += 5) {
+      for (int k = 0; k < 4; ++k) {
+        float t = 0.f;
+        OKV_HIP(hipEventElapsedTime(&t, e->ev[i + k], e->ev[i + k + 1]));
+        e->ms[k] += t;
+      }
+      e->calls++;
+    }
+    e->ev_used = 0;
+  }
+  for (int k = 0; k < 4; ++k) ms[k] = e ? e->ms[k] : 0.0;
+  if (calls) *calls = e ? e->calls : 0;
+  return OKV_OK;
+}
+
+int okv_encode_profile_reset(okv_ctx* ctx) {
+  if (!ctx) return OKV_E_ARG;
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  if (EncScratch* e = ctx->enc) {
+    e->ev_used = 0;
+    e->calls = 0;
+    for (double& m : e->ms) m = 0;
+  }
+  return OKV_OK;
+}
+
+int okv_synth_rows_fixed(okv_ctx* ctx, uint64_t seed, uint64_t first_row, uint64_t n,
+                         uint32_t key_len, uint32_t val_len, uint8_t* key_arena,
+                         uint64_t* key_off, uint16_t* key_len_out, uint8_t* val_arena,
+                         uint64_t* val_off, uint32_t* val_len_out) {
+  if (!ctx || key_len > 65535 || !key_off || !key_len_out || !val_off || !val_len_out)
+    return OKV_E_ARG;
+  if (!n) return OKV_OK;
+  OKV_HIP(hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(okv_synth_fixed_kernel, dim3(ceil_div(n, kThreads)), dim3(kThreads), 0,
+                     ctx->stream, seed, first_row, n, key_len, val_len, key_arena, key_off,
+                     key_len_out, val_arena, val_off, val_len_out);
+  OKV_HIP(hipGetLastError());
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  return OKV_OK;
+}
+
+}  // extern "C"

@@ -228,4 +228,23 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x, int lane) {
   return x;
 }
 
+// XXH64 (cespare/xxhash v2.2.0 == canonical XXH64, seed 0) building blocks.
+__device__ constexpr uint64_t XP1 = 11400714785074694791ULL, XP2 = 14029467366897019727ULL,
+                              XP3 = 1609587929392839161ULL, XP4 = 9650029242287828579ULL,
+                              XP5 = 2870177450012600261ULL;
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
+  return (x << r) | (x >> (64 - r));
+}
+__device__ __forceinline__ uint64_t xround(uint64_t acc, uint64_t in) {
+  acc += in * XP2;
+  acc = rotl64(acc, 31);
+  return acc * XP1;
+}
+__device__ __forceinline__ uint64_t ld64u(const uint8_t* p) {  // unaligned LE load
+  uint64_t v = 0;
+#pragma unroll
+  for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+  return v;
+}
+
 }  // namespace okv

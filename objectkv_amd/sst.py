@@ -334,3 +334,169 @@ class Decoder:
                                           compression, flags, C.byref(r), C.byref(k),
                                           C.byref(v)), "okv_decode_plan(device)")
         return r.value, k.value, v.value
+
+
+# ---- device encode (okv_encode_rows) ----------------------------------------------
+
+
+@dataclass
+class Encoded:
+    """Result of one GPU encode: the segment file bytes and the block index
+    (BlockStat order).  ``first_row[b]`` is the row whose key is FirstKey."""
+    seg: np.ndarray          # uint8[file_bytes]
+    file_bytes: int
+    data_bytes: int
+    meta_bytes: int
+    meta_hash: int
+    first_row: np.ndarray    # uint64[n_blocks + 1]
+    descs: np.ndarray        # uint64[n_blocks, 4]
+    hashes: np.ndarray       # uint64[n_blocks]
+
+    @property
+    def n_blocks(self):
+        return self.descs.shape[0]
+
+    def meta(self) -> bytes:
+        return self.seg[self.data_bytes:self.data_bytes + self.meta_bytes].tobytes()
+
+
+def pack_rows(rows):
+    """[(key, value), ...] -> SoA numpy arrays (okv_rows layout)."""
+    keys = [bytes(k) for k, _ in rows]
+    vals = [bytes(v) if v is not None else b"" for _, v in rows]
+    kl = np.array([len(k) for k in keys], np.uint16)
+    vl = np.array([len(v) for v in vals], np.uint32)
+    ko = np.zeros(len(keys), np.uint64)
+    vo = np.zeros(len(vals), np.uint64)
+    if len(keys):
+        ko[1:] = np.cumsum(kl[:-1], dtype=np.uint64)
+        vo[1:] = np.cumsum(vl[:-1], dtype=np.uint64)
+    ka = np.frombuffer(b"".join(keys) + b"\0" * 16, np.uint8)
+    va = np.frombuffer(b"".join(vals) + b"\0" * 16, np.uint8)
+    return dict(key_arena=ka, key_off=ko, key_len=kl, val_arena=va, val_off=vo, val_len=vl)
+
+
+class Encoder(Decoder):
+    """GPU SegmentWriter batch encode on one okv_ctx (shares the Decoder's
+    context management)."""
+
+    def profile_read_encode(self):
+        """-> ({'cut', 'pack', 'hash', 'meta'} ms summed, calls)"""
+        ms = (C.c_double * 4)()
+        n = C.c_uint64()
+        self._check(lib().okv_encode_profile_read(self._ctx, ms, C.byref(n)),
+                    "okv_encode_profile_read")
+        return {"cut": ms[0], "pack": ms[1], "hash": ms[2], "meta": ms[3]}, n.value
+
+    def profile_reset_encode(self):
+        self._check(lib().okv_encode_profile_reset(self._ctx), "okv_encode_profile_reset")
+
+    @staticmethod
+    def _opts(threshold, block_size, compression, strict_go):
+        return _lib.EncodeOpts(threshold, block_size, compression, int(strict_go))
+
+    def encode(self, rows, threshold=3584, block_size=4096, compression=COMP_NONE,
+               strict_go=True) -> Encoded:
+        """Host-buffer encode: rows is a list of (key, value) pairs or the dict
+        of SoA arrays from pack_rows()."""
+        r = rows if isinstance(rows, dict) else pack_rows(rows)
+        n = int(r["key_len"].size)
+        R = _lib.Rows(_ptr(r["key_arena"]), _ptr(r["key_off"]), _ptr(r["key_len"]),
+                      _ptr(r["val_arena"]), _ptr(r["val_off"]), _ptr(r["val_len"]), n,
+                      int(r["key_arena"].size), int(r["val_arena"].size))
+        o = self._opts(threshold, block_size, compression, strict_go)
+        out = _lib.EncodeOut()
+        rc = lib().okv_encode_rows(self._ctx, C.byref(R), C.byref(o), C.byref(out), 0)
+        if rc != OKV_E_CAPACITY:
+            self._check(rc, "okv_encode_rows(size)")
+        nb = out.n_blocks
+        seg = np.zeros(out.file_bytes, np.uint8)
+        first = np.zeros(nb + 1, np.uint64)
+        descs = np.zeros((nb, 4), np.uint64)
+        hashes = np.zeros(nb, np.uint64)
+        out = _lib.EncodeOut(_ptr(seg), seg.size, _ptr(first), _ptr(descs), _ptr(hashes), nb)
+        rc = lib().okv_encode_rows(self._ctx, C.byref(R), C.byref(o), C.byref(out), 0)
+        self._check(rc, "okv_encode_rows")
+        return Encoded(seg, out.file_bytes, out.data_bytes, out.meta_bytes, out.meta_hash,
+                       first, descs, hashes)
+
+    def encode_device(self, rows: dict, n_rows: int, out: dict, threshold=3584,
+                      block_size=4096, compression=COMP_NONE, strict_go=True, close=True,
+                      key_arena_bytes=0, val_arena_bytes=0):
+        """Device-resident encode.  rows: torch tensors key_arena, key_off,
+        key_len, val_arena, val_off, val_len; out: torch tensors seg (uint8),
+        optional first_row, desc (int64 [cap, 4]), hash.  Returns the filled
+        okv_encode_out (raises OkvError, e.g. OKV_E_CAPACITY with sizes in
+        .out)."""
+        R = _lib.Rows(_ptr(rows["key_arena"]), _ptr(rows["key_off"]), _ptr(rows["key_len"]),
+                      _ptr(rows["val_arena"]), _ptr(rows["val_off"]), _ptr(rows["val_len"]),
+                      n_rows, key_arena_bytes, val_arena_bytes)
+        o = self._opts(threshold, block_size, compression, strict_go)
+        g = out.get
+        caps = [t.shape[0] for t in (g("first_row"), g("desc"), g("hash")) if t is not None]
+        blk_cap = min([caps[0] - 1 if g("first_row") is not None else caps[0]] + caps[1:]) \
+            if caps else 0
+        eo = _lib.EncodeOut(_ptr(g("seg")), g("seg").numel() if g("seg") is not None else 0,
+                            _ptr(g("first_row")), _ptr(g("desc")), _ptr(g("hash")), blk_cap)
+        flags = F_DEVICE_PTRS | (0 if close else _lib.F_NO_CLOSE)
+        rc = lib().okv_encode_rows(self._ctx, C.byref(R), C.byref(o), C.byref(eo), flags)
+        if rc:
+            err = OkvError(rc, f"okv_encode_rows(device): {self.error()}")
+            err.out = eo
+            raise err
+        return eo
+
+    def close_device(self, eo):
+        """okv_encode_close on a device segment (meta XXH64 on the host)."""
+        self._check(lib().okv_encode_close(self._ctx, C.byref(eo), F_DEVICE_PTRS),
+                    "okv_encode_close")
+        return eo
+
+    def synth_fixed_device(self, seed, first_row, n, key_len, val_len, t: dict):
+        """Fill torch tensors (key_arena, key_off, key_len, val_arena, val_off,
+        val_len) with rows_fixed rows first_row .. first_row + n - 1."""
+        self._check(lib().okv_synth_rows_fixed(
+            self._ctx, seed, first_row, n, key_len, val_len, _ptr(t["key_arena"]),
+            _ptr(t["key_off"]), _ptr(t["key_len"]), _ptr(t["val_arena"]), _ptr(t["val_off"]),
+            _ptr(t["val_len"])), "okv_synth_rows_fixed")
+
+
+class GpuSegmentWriter:
+    """sst.SegmentWriter (segment_writer.go:35-328) whose Close encodes on the
+    GPU.  WriteRow validates each row exactly as Go does (:80-91) and buffers
+    it; Close runs okv_encode_rows over the buffered rows and returns
+    (file length, meta block bytes).  ``data()`` is what the Go writer's sink
+    holds afterwards."""
+
+    def __init__(self, encoder: Encoder, threshold=3584, block_size=4096, zstd_level=0,
+                 lz4=False, strict_go=True):
+        self._enc = encoder
+        self._opts = dict(threshold=threshold, block_size=block_size,
+                          compression=COMP_ZSTD if zstd_level > 0 else
+                          (COMP_LZ4 if lz4 else COMP_NONE), strict_go=strict_go)
+        self._rows = []
+        self._closed = False
+        self.result = None
+
+    def WriteRow(self, key, val):
+        key = b"" if key is None else bytes(key)
+        val = b"" if val is None else bytes(val)
+        if len(key) > 0xFFFF:
+            raise OkvError(_lib.W_KEY_TOO_LARGE, "ErrKeyTooLarge")
+        if len(val) > 0xFFFFFFFF:
+            raise OkvError(_lib.W_VALUE_TOO_LARGE, "ErrValueTooLarge")
+        if self._closed:
+            raise OkvError(_lib.W_CLOSED, "ErrWriterClosed")
+        if not key:
+            raise OkvError(_lib.W_INVALID_KEY, "key cannot be empty: ErrInvalidKey")
+        self._rows.append((key, val))
+
+    def Close(self):
+        if self._closed:  # Go: blockWriter is nil after the first Close -> panic (Q1)
+            raise OkvError(_lib.W_NIL_WRITER, "Close on a closed writer")
+        self.result = self._enc.encode(self._rows, **self._opts)
+        self._closed = True
+        return self.result.file_bytes, self.result.meta()
+
+    def data(self) -> np.ndarray:
+        return self.result.seg

@@ -168,22 +168,32 @@ def crafted_case():
     return {"name": "crafted_edges", "kind": "crafted", "segment_z": packed(seg_b), "blocks": blocks}
 
 
+def writer_inputs():
+    """(name, rows, writer options) of the reference test inputs
+    (sst/segment_reader_test.go, segment_writer_test.go, segment_row_iter_test.go);
+    also the device-encode parity inputs (tests/test_encode_gpu.py)."""
+    r200 = [(b"key%03d" % i, b"value%03d" % i) for i in range(200)]
+    big = [(b"a" * 511, b"b" * 10000)] + [(b"key%d" % i, b"value%d" % i) for i in range(200)]
+    return [
+        ("ref_read_uncompressed_200", r200, {}),  # segment_reader_test.go:12-269
+        ("ref_blank_value", r200 + [(b"key200", b"")], {}),  # :271-326
+        ("ref_single_row", r200[:1], {}),  # :328-511
+        ("ref_larger_than_block", big, {}),  # segment_writer_test.go:73-112
+        ("ref_writer_no_compression",
+         [(b"key%d" % i, b"value%d" % i) for i in range(200)], {}),  # :12-40
+        ("ref_rollover_no_bloom",
+         [(b"key%03d" % i, b"value%03d-I-SHOULD-NOT-SHOW" % i) for i in range(1, 200, 2)]
+         + [(b"key900", b"value900")], {}),  # segment_row_iter_test.go:380-450
+        ("lz4_flag_200", r200, {"lz4": True}),  # Q7
+    ]
+
+
 def main(out_path=os.path.join(HERE, "golden.json")):
     cases = []
     # reference test inputs (sst/segment_reader_test.go, segment_writer_test.go,
     # segment_row_iter_test.go)
-    r200 = [(b"key%03d" % i, b"value%03d" % i) for i in range(200)]
-    cases.append(writer_case("ref_read_uncompressed_200", r200))  # segment_reader_test.go:12-269
-    cases.append(writer_case("ref_blank_value", r200 + [(b"key200", b"")]))  # :271-326
-    cases.append(writer_case("ref_single_row", r200[:1]))  # :328-511
-    big = [(b"a" * 511, b"b" * 10000)] + [(b"key%d" % i, b"value%d" % i) for i in range(200)]
-    cases.append(writer_case("ref_larger_than_block", big))  # segment_writer_test.go:73-112
-    cases.append(writer_case("ref_writer_no_compression",
-                             [(b"key%d" % i, b"value%d" % i) for i in range(200)]))  # :12-40
-    cases.append(writer_case("ref_rollover_no_bloom",
-                             [(b"key%03d" % i, b"value%03d-I-SHOULD-NOT-SHOW" % i)
-                              for i in range(1, 200, 2)] + [(b"key900", b"value900")]))
-    cases.append(writer_case("lz4_flag_200", r200, lz4=True))  # Q7
+    for name, rows, kw in writer_inputs():
+        cases.append(writer_case(name, rows, **kw))
     cases.append(synth_case("c2_fixed_256x4k", "fixed", 1, 256, 3584, 4096))
     cases.append(synth_case("c3_zipf_8x64k", "zipf", 3, 8, 57344, 65536))
     cases.append(crafted_case())

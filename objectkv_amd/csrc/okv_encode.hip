@@ -65,7 +65,8 @@ struct EncTotals {
   unsigned long long meta_ent;    // sum of meta index entry sizes
   unsigned long long last_raw;    // OriginalSize of the last block (Q1)
   unsigned long long head;        // meta head bytes (keys, bloom, compression, count)
-  unsigned long long pad[7];
+  unsigned long long fault;       // a chain-table invariant failed (never expected)
+  unsigned long long pad[6];
 };
 
 struct EncScratch {
@@ -174,6 +175,7 @@ __global__ void okv_enc_init_kernel(EncTotals* t) {
   t->meta_ent = 0;
   t->last_raw = 0;
   t->head = 0;
+  t->fault = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -345,11 +347,16 @@ __global__ __launch_bounds__(kThreads) void okv_enc_jump0_kernel(const uint32_t*
 
 __global__ __launch_bounds__(kThreads) void okv_enc_jump_kernel(
     const uint32_t* __restrict__ jt0, const uint32_t* __restrict__ jb0, uint32_t* __restrict__ jt1,
-    uint32_t* __restrict__ jb1, uint32_t W, uint64_t nch, uint64_t h) {
+    uint32_t* __restrict__ jb1, uint32_t W, uint64_t nch, uint64_t h, EncTotals* tot) {
   const uint64_t gid = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   const uint64_t c = gid / W;
   if (c >= nch) return;
-  const uint32_t e = jt0[gid], b = jb0[gid];
+  uint32_t e = jt0[gid];
+  const uint32_t b = jb0[gid];
+  if (e >= W) {  // exits land below W by construction (C >= W); guard the gather
+    tot->fault = 1;
+    e = W - 1;
+  }
   if (c + h < nch) {
     const uint64_t g2 = (c + h) * W + e;
     jt1[gid] = jt0[g2];
@@ -375,6 +382,10 @@ __global__ __launch_bounds__(kThreads) void okv_enc_resolve_kernel(
       cnt += jb[idx];
       pos = jt[idx];
       cur += uint64_t(1) << k;
+      if (pos >= W) {
+        tot->fault = 1;
+        pos = W - 1;
+      }
     }
   }
   entry[c] = pos;
@@ -385,16 +396,23 @@ __global__ __launch_bounds__(kThreads) void okv_enc_resolve_kernel(
 __global__ __launch_bounds__(kThreads) void okv_enc_emit_kernel(
     const uint32_t* __restrict__ nx, uint64_t n, uint64_t C, uint64_t nch,
     const uint32_t* __restrict__ entry, const uint64_t* __restrict__ kbase,
-    uint64_t* __restrict__ first) {
+    uint64_t* __restrict__ first, uint64_t nb, EncTotals* __restrict__ tot) {
   const uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (c >= nch) return;
   const uint64_t ce = std::min<uint64_t>(n, (c + 1) * C);
   uint64_t pos = c * C + entry[c], k = kbase[c];
   while (pos < ce) {
+    if (k >= nb) {
+      tot->fault = 1;
+      return;
+    }
     first[k++] = pos;
     pos += nx[pos];
   }
-  if (c == nch - 1) first[k] = n;
+  if (c == nch - 1) {
+    if (k != nb) tot->fault = 1;
+    first[nb] = n;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -896,14 +914,14 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   for (uint32_t k = 1; k < levels; ++k)
     hipLaunchKernelGGL(okv_enc_jump_kernel, dim3(ceil_div(lv, kThreads)), dim3(kThreads), 0,
                        ctx->stream, e->jt + (k - 1) * lv, e->jb + (k - 1) * lv, e->jt + k * lv,
-                       e->jb + k * lv, uint32_t(W), nch, uint64_t(1) << (k - 1));
+                       e->jb + k * lv, uint32_t(W), nch, uint64_t(1) << (k - 1), e->d_tot);
   hipLaunchKernelGGL(okv_enc_resolve_kernel, dim3(ceil_div(nch, kThreads)), dim3(kThreads), 0,
                      ctx->stream, e->jt, e->jb, levels, uint32_t(W), nch, e->entry, e->kbase,
                      e->d_tot);
   OKV_HIP(hipGetLastError());
   if ((rc = read_enc_totals(ctx, e))) return rc;
   const uint64_t nb = e->h_tot->nb;
-  if (nb == 0 || nb > n || nb >= (uint64_t(1) << 32))
+  if (e->h_tot->fault || nb == 0 || nb > n || nb >= (uint64_t(1) << 32))
     return set_err(ctx, OKV_E_HIP, "encode: inconsistent block count");
   if ((rc = ensure_blocks_enc(ctx, e, nb))) return rc;
   const uint32_t nbt = ceil_div(nb, kETile);
@@ -912,7 +930,7 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   uint64_t* etot = e->btile + 2 * e->cap_btiles;
   uint64_t* epre = e->btile + 3 * e->cap_btiles;
   hipLaunchKernelGGL(okv_enc_emit_kernel, dim3(ceil_div(nch, kThreads)), dim3(kThreads), 0,
-                     ctx->stream, e->nx, n, C, nch, e->entry, e->kbase, e->first);
+                     ctx->stream, e->nx, n, C, nch, e->entry, e->kbase, e->first, nb, e->d_tot);
   StatParams sp;
   sp.first = e->first;
   sp.pl = e->pl;
@@ -937,6 +955,7 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
                      e->moff, e->d_tot);
   OKV_HIP(hipGetLastError());
   if ((rc = read_enc_totals(ctx, e))) return rc;
+  if (e->h_tot->fault) return set_err(ctx, OKV_E_HIP, "encode: block chain inconsistent");
   pl->nb = nb;
   pl->data_bytes = e->h_tot->data_bytes;
   pl->meta_bytes = e->h_tot->head + e->h_tot->meta_ent;

@@ -64,6 +64,9 @@ def lib():
         L.oref_fetch_meta.argtypes = [p, u64, C.c_int64, C.POINTER(Meta), C.POINTER(u64),
                                       C.POINTER(u64)]
         L.oref_meta_free.argtypes = [C.POINTER(Meta)]
+        L.oref_encode_go.restype = C.c_int
+        L.oref_encode_go.argtypes = [p, p, p, p, p, p, u64, u64, u64, C.c_int, C.c_int,
+                                     C.POINTER(u64)]
         L.oref_decode_range_go.restype = u64
         L.oref_decode_range_go.argtypes = [p, u64, p, u64, C.c_int, C.c_int, C.POINTER(u64)]
         L.oref_block_counts.argtypes = [p, u64, p, u64, C.c_int, p, p, p, p]
@@ -197,3 +200,16 @@ def decode_go(seg, descs: np.ndarray, compression=0, threads=1):
     rows = lib().oref_decode_range_go(_ptr(s), len(seg), _ptr(descs), len(descs), compression,
                                       threads, C.byref(pay))
     return rows, pay.value
+
+
+def encode_go(rows: dict, n, threshold=3584, block_size=4096, lz4=False, threads=1):
+    """CPU encode baseline over SoA numpy arrays (okv_rows layout); returns the
+    total segment bytes written by `threads` key-range shards."""
+    fb = C.c_uint64()
+    rc = lib().oref_encode_go(_ptr(rows["key_arena"]), _ptr(rows["key_off"]),
+                              _ptr(rows["key_len"]), _ptr(rows["val_arena"]),
+                              _ptr(rows["val_off"]), _ptr(rows["val_len"]), n, threshold,
+                              block_size, int(lz4), threads, C.byref(fb))
+    if rc:
+        raise RuntimeError(f"oref_encode_go: {rc}")
+    return fb.value

@@ -523,6 +523,68 @@ uint64_t oref_decode_range_go(const uint8_t *seg, uint64_t seg_len, const oref_b
   return rows;
 }
 
+/* CPU baseline for the encode: SegmentWriter.WriteRow x n + Close with Go's
+ * per-row allocation (rowBuf := make([]byte, 6+len(key)+len(val)) and two
+ * copies, segment_writer.go:121-125).  `threads` writers encode contiguous
+ * row ranges as separate segments (key-range shards). */
+typedef struct {
+  const uint8_t *ka, *va;
+  const uint64_t *ko, *vo;
+  const uint16_t *kl;
+  const uint32_t *vl;
+  uint64_t lo, hi, T, D;
+  int lz4;
+  uint64_t bytes;
+  int rc;
+} enc_job;
+
+static void *enc_run(void *arg) {
+  enc_job *j = (enc_job *)arg;
+  oref_writer *w = oref_writer_new(j->T, j->D, 0, j->lz4);
+  j->rc = 0;
+  for (uint64_t i = j->lo; i < j->hi && !j->rc; i++) {
+    const size_t k = j->kl[i], v = j->vl[i];
+    uint8_t *row = (uint8_t *)malloc(6 + k + v); /* :121 make */
+    memcpy(row + 6, j->ka + j->ko[i], k);        /* :124 */
+    memcpy(row + 6 + k, j->va + j->vo[i], v);    /* :125 */
+    j->rc = oref_writer_write_row(w, row + 6, k, row + 6 + k, v);
+    free(row);
+  }
+  uint64_t flen = 0;
+  if (!j->rc) j->rc = oref_writer_close(w, NULL, &flen, NULL, NULL);
+  j->bytes = flen;
+  oref_writer_free(w);
+  return NULL;
+}
+
+int oref_encode_go(const uint8_t *key_arena, const uint64_t *key_off, const uint16_t *key_len,
+                   const uint8_t *val_arena, const uint64_t *val_off, const uint32_t *val_len,
+                   uint64_t n, uint64_t threshold, uint64_t block_size, int lz4, int threads,
+                   uint64_t *file_bytes) {
+  if (threads < 1) threads = 1;
+  enc_job *jobs = (enc_job *)calloc((size_t)threads, sizeof(enc_job));
+  pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (enc_job){key_arena, val_arena, key_off, val_off, key_len, val_len,
+                        n * t / threads, n * (t + 1) / threads, threshold, block_size, lz4, 0, 0};
+    if (threads > 1)
+      pthread_create(&th[t], NULL, enc_run, &jobs[t]);
+    else
+      enc_run(&jobs[t]);
+  }
+  int rc = 0;
+  uint64_t bytes = 0;
+  for (int t = 0; t < threads; t++) {
+    if (threads > 1) pthread_join(th[t], NULL);
+    if (jobs[t].rc) rc = jobs[t].rc;
+    bytes += jobs[t].bytes;
+  }
+  free(jobs);
+  free(th);
+  if (file_bytes) *file_bytes = bytes;
+  return rc;
+}
+
 /* ======================================================================= */
 /* SoA restatement of the product output layout                 */
 /* ======================================================================= */

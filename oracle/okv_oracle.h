@@ -125,6 +125,12 @@ void oref_rows_free(oref_rows *r);
  * bytes to *payload.  Used only by bench.py's cpu_baseline leg. */
 uint64_t oref_decode_range_go(const uint8_t *seg, uint64_t seg_len, const oref_block_desc *d,
                               uint64_t nblk, int compression, int threads, uint64_t *payload);
+/* CPU encode baseline: `threads` key-range shards, each its own segment, with
+ * Go's per-row rowBuf allocation; returns 0 or the first writer error. */
+int oref_encode_go(const uint8_t *key_arena, const uint64_t *key_off, const uint16_t *key_len,
+                   const uint8_t *val_arena, const uint64_t *val_off, const uint32_t *val_len,
+                   uint64_t n, uint64_t threshold, uint64_t block_size, int lz4, int threads,
+                   uint64_t *file_bytes);
 
 /* ---- SoA restatement of the product's output layout -------------------- */
 /* Pass 1: per-block (status, rows, key bytes, value bytes). */

@@ -201,7 +201,7 @@ def test_decode_encode_round_trip(enc, decoder, kind, th, bs):
     assert eo.file_bytes == seg.size
     assert seg_t[:seg.size].cpu().numpy().tobytes() == seg.tobytes()
     assert np.array_equal(desc_t.cpu().numpy().view(np.uint64), descs)
-    want_h = np.array([b[1] for b in w.blocks()], np.uint64)
+    want_h = np.array([b[2] for b in w.blocks()], np.uint64)
     assert np.array_equal(hash_t.cpu().numpy().view(np.uint64), want_h)
 
 

@@ -66,7 +66,8 @@ struct EncTotals {
   unsigned long long last_raw;    // OriginalSize of the last block (Q1)
   unsigned long long head;        // meta head bytes (keys, bloom, compression, count)
   unsigned long long fault;       // a chain-table invariant failed (never expected)
-  unsigned long long pad[6];
+  unsigned long long bmax;        // largest BlockSize
+  unsigned long long pad[5];
 };
 
 struct EncScratch {
@@ -176,6 +177,7 @@ __global__ void okv_enc_init_kernel(EncTotals* t) {
   t->last_raw = 0;
   t->head = 0;
   t->fault = 0;
+  t->bmax = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -185,32 +187,48 @@ __global__ void okv_enc_init_kernel(EncTotals* t) {
 __global__ __launch_bounds__(kThreads) void okv_enc_size_kernel(
     const uint16_t* __restrict__ key_len, const uint32_t* __restrict__ val_len, uint64_t n,
     uint64_t* __restrict__ pl, uint64_t* __restrict__ tile_tot, EncTotals* __restrict__ tot) {
+  __shared__ uint64_t sz[kETile];  // striped in/out, blocked compute
   __shared__ uint64_t sm[kThreads / 64 + 1];
-  const uint64_t base = uint64_t(blockIdx.x) * kETile + uint64_t(threadIdx.x) * kEItems;
-  uint64_t loc[kEItems];
-  uint64_t sum = 0, mn = kNone, bad = kNone;
+  const uint64_t tb = uint64_t(blockIdx.x) * kETile;
+  uint64_t mn = kNone, bad = kNone;
 #pragma unroll
-  for (int i = 0; i < kEItems; ++i) {
-    const uint64_t r = base + i;
+  for (int i = 0; i < kEItems; ++i) {  // coalesced loads
+    const uint32_t j = i * kThreads + threadIdx.x;
+    const uint64_t r = tb + j;
+    uint64_t s = 0;
     if (r < n) {
       const uint32_t kl = key_len[r];
-      const uint64_t s = 6u + uint64_t(kl) + uint64_t(val_len[r]);
+      s = 6u + uint64_t(kl) + uint64_t(val_len[r]);
       if (kl == 0 && r < bad) bad = r;
       mn = s < mn ? s : mn;
-      sum += s;
     }
+    sz[j] = s;
+  }
+  __syncthreads();
+  uint64_t loc[kEItems], sum = 0;
+#pragma unroll
+  for (int i = 0; i < kEItems; ++i) {
+    sum += sz[threadIdx.x * kEItems + i];
     loc[i] = sum;
   }
   uint64_t total;
   const uint64_t ex = wg_excl_scan(sum, sm, total);
 #pragma unroll
-  for (int i = 0; i < kEItems; ++i)
-    if (base + i < n) pl[base + i] = ex + loc[i];
+  for (int i = 0; i < kEItems; ++i) sz[threadIdx.x * kEItems + i] = ex + loc[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kEItems; ++i) {  // coalesced stores
+    const uint32_t j = i * kThreads + threadIdx.x;
+    if (tb + j < n) pl[tb + j] = sz[j];
+  }
   if (threadIdx.x == 0) tile_tot[blockIdx.x] = total;
+  // one same-address atomic per wave would serialise in L2: only issue it
+  // when this wave improves on the value already there (values move one way)
   mn = wave_min64(mn);
   bad = wave_min64(bad);
   if ((threadIdx.x & 63) == 0) {
-    atomicMin(&tot->min_size, (unsigned long long)mn);
+    if (mn < __atomic_load_n(&tot->min_size, __ATOMIC_RELAXED))
+      atomicMin(&tot->min_size, (unsigned long long)mn);
     if (bad != kNone) atomicMin(&tot->bad_row, (unsigned long long)bad);
   }
 }
@@ -287,6 +305,9 @@ __global__ __launch_bounds__(kThreads) void okv_enc_next_kernel(
   const uint32_t a0 = threadIdx.x * kEItems;  // tile-relative first row
   uint64_t wmax = 0;
   uint32_t mb = 0;
+  uint32_t dv[kEItems];
+#pragma unroll
+  for (int i = 0; i < kEItems; ++i) dv[i] = 0;
   for (int i = 0; i < kEItems; ++i) {
     const uint32_t ar = a0 + i;
     if (cs + ar >= n) break;
@@ -313,11 +334,20 @@ __global__ __launch_bounds__(kThreads) void okv_enc_next_kernel(
     else
       next = next_far(pl, tp, n, cs - 1 + M, target);
     const uint64_t d = next - (cs + ar);
-    nx[cs + ar] = uint32_t(d);
+    dv[i] = uint32_t(d);
     wmax = d > wmax ? d : wmax;
   }
+  if (cs + a0 + kEItems <= n) {  // 32 contiguous bytes per lane
+    uint4* q = reinterpret_cast<uint4*>(nx + cs + a0);
+    q[0] = make_uint4(dv[0], dv[1], dv[2], dv[3]);
+    q[1] = make_uint4(dv[4], dv[5], dv[6], dv[7]);
+  } else {
+    for (int i = 0; i < kEItems; ++i)
+      if (cs + a0 + i < n) nx[cs + a0 + i] = dv[i];
+  }
   wmax = wave_max64(wmax);
-  if ((threadIdx.x & 63) == 0) atomicMax(&tot->wmax, (unsigned long long)wmax);
+  if ((threadIdx.x & 63) == 0 && wmax > __atomic_load_n(&tot->wmax, __ATOMIC_RELAXED))
+    atomicMax(&tot->wmax, (unsigned long long)wmax);
 }
 
 // ---------------------------------------------------------------------------
@@ -439,7 +469,7 @@ __global__ __launch_bounds__(kThreads) void okv_enc_stat_kernel(StatParams P) {
   __shared__ uint64_t sm[kThreads / 64 + 1];
   const uint64_t base = uint64_t(blockIdx.x) * kETile + uint64_t(threadIdx.x) * kEItems;
   uint64_t lb[kEItems], le[kEItems];
-  uint64_t sb = 0, se = 0;
+  uint64_t sb = 0, se = 0, bmax = 0;
 #pragma unroll
   for (int i = 0; i < kEItems; ++i) {
     const uint64_t k = base + i;
@@ -456,6 +486,7 @@ __global__ __launch_bounds__(kThreads) void okv_enc_stat_kernel(StatParams P) {
       P.desc[k] = d;
       sb += bs;
       se += es;
+      bmax = bs > bmax ? bs : bmax;
       if (k == P.nb - 1) P.tot->last_raw = raw;
     }
     lb[i] = sb;
@@ -475,6 +506,9 @@ __global__ __launch_bounds__(kThreads) void okv_enc_stat_kernel(StatParams P) {
     P.btile_tot[blockIdx.x] = tb;
     P.etile_tot[blockIdx.x] = te;
   }
+  bmax = wave_max64(bmax);
+  if ((threadIdx.x & 63) == 0 && bmax > __atomic_load_n(&P.tot->bmax, __ATOMIC_RELAXED))
+    atomicMax(&P.tot->bmax, (unsigned long long)bmax);
 }
 
 // E9: Offset = running sum of BlockSize (:197-203); meta entry offsets.
@@ -523,47 +557,92 @@ struct __align__(16) PackSmem {
   uint32_t vl[kPackRows];
 };
 
-// Field bytes src[0, flen) land at window offsets [d, d + flen); merge the
-// part inside [0, 16) into out.  Only 16-byte lines holding a needed byte
-// are loaded.
-__device__ __forceinline__ void place_field(uint4& out, const uint8_t* src, int64_t d,
-                                            uint64_t flen) {
-  const int64_t lo = d > 0 ? d : 0;
-  const int64_t hi64 = d + int64_t(flen);
-  const int64_t hi = hi64 < 16 ? hi64 : 16;
-  if (lo >= hi) return;
-  const uintptr_t v = reinterpret_cast<uintptr_t>(src) - uintptr_t(d);  // window byte 0
+// Bytes [b, 16) of acc replaced by those of v (b clamped to [0, 16]).  Records
+// are assembled segment by segment in increasing position, so each segment
+// only has to overwrite from its own start: later segments overwrite its
+// tail.  Four med3 + 64-bit shift + bfi per chunk.
+__device__ __forceinline__ uint32_t suffix_mask(int32_t c) {
+  c = min(max(c, 0), 4);
+  return uint32_t(0xffffffffULL << (8 * c));
+}
+__device__ __forceinline__ uint4 replace_from(const uint4& acc, const uint4& v, int32_t b) {
+  uint32_t m;
+  uint4 r;
+  m = suffix_mask(b);
+  r.x = bsel(m, v.x, acc.x);
+  m = suffix_mask(b - 4);
+  r.y = bsel(m, v.y, acc.y);
+  m = suffix_mask(b - 8);
+  r.z = bsel(m, v.z, acc.z);
+  m = suffix_mask(b - 12);
+  r.w = bsel(m, v.w, acc.w);
+  return r;
+}
+
+// 16 bytes whose byte j (for j in [s, e) intersected with [0, 16)) is
+// src[j - s].  Only the 16-byte lines holding those bytes are loaded.
+__device__ __forceinline__ uint4 seg_window(const uint8_t* src, int64_t s, int64_t e) {
+  const int64_t lo = s > 0 ? s : 0;
+  const int64_t hi = e < 16 ? e : 16;
+  const uintptr_t v = reinterpret_cast<uintptr_t>(src) - uintptr_t(s);  // window byte 0
   const uintptr_t a = v & ~uintptr_t(15);
-  const uint32_t s = uint32_t(v & 15);
-  const uintptr_t safe = (v + uintptr_t(lo)) & ~uintptr_t(15);  // holds a needed byte
-  const bool n0 = int64_t(16 - s) > lo;
-  const bool n1 = s != 0 && hi > int64_t(16 - s);
+  const uint32_t sh = uint32_t(v & 15);
+  const uintptr_t safe = (v + uintptr_t(lo)) & ~uintptr_t(15);
+  const bool n0 = int64_t(16 - sh) > lo;
+  const bool n1 = sh != 0 && hi > int64_t(16 - sh);
   const uint4 x = *reinterpret_cast<const uint4*>(n0 ? a : safe);
   const uint4 y = *reinterpret_cast<const uint4*>(n1 ? a + 16 : safe);
-  const uint32_t m0 = 0u - uint32_t(n0), m1 = 0u - uint32_t(n1);
-  const uint4 w = funnel32(make_uint4(x.x & m0, x.y & m0, x.z & m0, x.w & m0),
-                           make_uint4(y.x & m1, y.y & m1, y.z & m1, y.w & m1), s);
-  out = merge_bytes(out, w, int32_t(lo), int32_t(hi));
+  return funnel32(x, y, sh);
 }
 
-// The 6 header bytes [u16 klen][u32 vlen] at window offset d (-5 <= d <= 15).
-__device__ __forceinline__ void place_header(uint4& out, uint32_t kl, uint32_t vl, int64_t d) {
-  const int64_t lo = d > 0 ? d : 0;
-  const int64_t hi = d + 6 < 16 ? d + 6 : 16;
-  if (lo >= hi) return;
+// The 6 header bytes [u16 klen][u32 vlen] placed at window offset d (-5..15).
+__device__ __forceinline__ uint4 header_window(uint32_t kl, uint32_t vl, int64_t d) {
   const uint4 H = make_uint4(kl | (vl << 16), vl >> 16, 0, 0);
   const uint4 Z = make_uint4(0, 0, 0, 0);
-  const uint4 w = d > 0 ? funnel32(Z, H, uint32_t(16 - d)) : funnel32(H, Z, uint32_t(-d));
-  out = merge_bytes(out, w, int32_t(lo), int32_t(hi));
+  return d > 0 ? funnel32(Z, H, uint32_t(16 - d)) : funnel32(H, Z, uint32_t(-d));
 }
 
+struct RecInfo {
+  uint64_t rs;  // record start (block- or region-relative, same frame as pos)
+  uint64_t ko, vo;
+  uint32_t kl, vl;
+};
+
+// Destination chunk [pos, pos + 16): records i0, i0 + 1, ... (rec(i) gives
+// them, valid while i < nrec) in increasing position; bytes no record covers
+// are padding (zero).  i0 = the last record starting at or before pos.
+template <class Rec>
+__device__ __forceinline__ uint4 assemble_chunk(const PackParams& P, uint64_t pos, uint64_t i0,
+                                                uint64_t nrec, Rec rec) {
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  int64_t last_end = 0;
+  for (uint64_t i = i0; i < nrec; ++i) {
+    const RecInfo r = rec(i);
+    if (r.rs >= pos + 16) break;
+    const int64_t hs = int64_t(r.rs) - int64_t(pos);
+    const int64_t ks = hs + 6, vs = ks + int64_t(r.kl), ve = vs + int64_t(r.vl);
+    if (ve <= 0) continue;  // record ends before this chunk (padding chunk)
+    if (ks > 0) acc = replace_from(acc, header_window(r.kl, r.vl, hs), int32_t(hs > 0 ? hs : 0));
+    if (vs > 0 && ks < 16)
+      acc = replace_from(acc, seg_window(P.key_arena + r.ko, ks, vs), int32_t(ks > 0 ? ks : 0));
+    if (r.vl && vs < 16)
+      acc = replace_from(acc, seg_window(P.val_arena + r.vo, vs, ve), int32_t(vs > 0 ? vs : 0));
+    last_end = ve;
+  }
+  if (last_end < 16) acc = replace_from(acc, make_uint4(0, 0, 0, 0), int32_t(last_end));
+  return acc;
+}
+
+// E10, general blocks (more than kPackRows rows or larger than a region): one
+// workgroup per block, rows staged kPackRows at a time; a chunk that runs into
+// the next batch reads those records from HBM.
 __global__ __launch_bounds__(kThreads) void okv_enc_pack_kernel(PackParams P) {
   __shared__ PackSmem sm;
   const uint64_t k = blockIdx.x;
   const Desc d = P.desc[k];
   const uint64_t r0 = P.first[k], r1 = P.first[k + 1];
   const uint64_t base = Pg(P.pl, P.tp, int64_t(r0) - 1);
-  const uint64_t L = d.original_size, S = d.block_size;
+  const uint64_t S = d.block_size;
   uint8_t* dst = P.seg + d.offset;
   for (uint64_t b0 = r0;; b0 += kPackRows) {
     const uint64_t b1 = std::min<uint64_t>(r1, b0 + kPackRows);
@@ -582,48 +661,117 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_kernel(PackParams P) {
     const bool last = b1 == r1;
     const uint64_t q0 = (sm.rel[0] + 15) >> 4;
     const uint64_t q1 = last ? (S >> 4) : ((sm.rel[nbat] + 15) >> 4);
+    auto rec = [&](uint64_t i) {
+      RecInfo r;
+      if (i < nbat) {
+        r.rs = sm.rel[i];
+        r.ko = sm.ko[i];
+        r.vo = sm.vo[i];
+        r.kl = sm.kl[i];
+        r.vl = sm.vl[i];
+      } else {  // the chunk runs into the next batch
+        const uint64_t g = b0 + i;
+        r.rs = Pg(P.pl, P.tp, int64_t(g) - 1) - base;
+        r.ko = P.key_off[g];
+        r.vo = P.val_off[g];
+        r.kl = P.key_len[g];
+        r.vl = P.val_len[g];
+      }
+      return r;
+    };
     for (uint64_t q = q0 + threadIdx.x; q < q1; q += kThreads) {
       const uint64_t pos = q << 4;
-      uint4 out = make_uint4(0, 0, 0, 0);
-      if (pos < L) {
-        // last record of the batch starting at or before pos
-        uint32_t lo = 0, hi = nbat;  // rel[lo] <= pos < rel[hi]
-        while (hi - lo > 1) {
-          const uint32_t m = (lo + hi) >> 1;
-          if (sm.rel[m] <= pos)
-            lo = m;
-          else
-            hi = m;
-        }
-        for (uint64_t i = lo;; ++i) {
-          const uint64_t g = b0 + i;
-          if (g >= r1) break;
-          uint64_t rs, ko, vo;
-          uint32_t kl, vl;
-          if (i < nbat) {
-            rs = sm.rel[i];
-            ko = sm.ko[i];
-            vo = sm.vo[i];
-            kl = sm.kl[i];
-            vl = sm.vl[i];
-          } else {  // the chunk runs into the next batch
-            rs = Pg(P.pl, P.tp, int64_t(g) - 1) - base;
-            ko = P.key_off[g];
-            vo = P.val_off[g];
-            kl = P.key_len[g];
-            vl = P.val_len[g];
-          }
-          if (rs >= pos + 16) break;
-          const int64_t dh = int64_t(rs) - int64_t(pos);
-          place_header(out, kl, vl, dh);
-          place_field(out, P.key_arena + ko, dh + 6, kl);
-          place_field(out, P.val_arena + vo, dh + 6 + kl, vl);
-        }
+      uint32_t lo = 0, hi = nbat;  // rel[lo] <= pos < rel[hi] (or pos in the padding)
+      while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (sm.rel[m] <= pos)
+          lo = m;
+        else
+          hi = m;
       }
-      *reinterpret_cast<uint4*>(dst + pos) = out;
+      *reinterpret_cast<uint4*>(dst + pos) = assemble_chunk(P, pos, lo, r1 - b0, rec);
     }
     if (last) break;
     __syncthreads();
+  }
+}
+
+// E10, small blocks: one workgroup packs a region of G consecutive blocks
+// (at most kPackRows records and kMaxChunks chunks).  Blocks start on 16-byte
+// boundaries, so no chunk mixes two blocks.  A chunk -> record table built in
+// LDS replaces the per-chunk search.
+constexpr int kMaxRegion = 64;
+constexpr uint32_t kMaxChunks = 4096;
+
+struct __align__(16) RegionSmem {
+  uint64_t out[kPackRows + 1];  // record start relative to the region; [nrow] = region end
+  uint64_t ko[kPackRows];
+  uint64_t vo[kPackRows];
+  uint32_t kl[kPackRows];
+  uint32_t vl[kPackRows];
+  uint16_t qrow[kMaxChunks];    // last record starting at or before chunk q
+  uint64_t bfirst[kMaxRegion + 1];
+  uint64_t brel[kMaxRegion];    // block offset - region offset
+  uint64_t bbase[kMaxRegion];   // P(first row - 1)
+};
+
+__global__ __launch_bounds__(kThreads) void okv_enc_pack_region_kernel(PackParams P, uint64_t nb,
+                                                                       uint32_t G) {
+  __shared__ RegionSmem sm;
+  const uint64_t k0 = uint64_t(blockIdx.x) * G;
+  const uint32_t g = uint32_t(std::min<uint64_t>(G, nb - k0));
+  const uint64_t O0 = P.desc[k0].offset;
+  const Desc dl = P.desc[k0 + g - 1];
+  const uint64_t nq = (dl.offset + dl.block_size - O0) >> 4;
+  if (threadIdx.x <= g) {
+    const uint32_t t = threadIdx.x;
+    const uint64_t f = P.first[k0 + t];
+    sm.bfirst[t] = f;
+    if (t < g) {
+      sm.brel[t] = P.desc[k0 + t].offset - O0;
+      sm.bbase[t] = Pg(P.pl, P.tp, int64_t(f) - 1);
+    }
+  }
+  __syncthreads();
+  const uint64_t R0 = sm.bfirst[0];
+  const uint32_t nrow = uint32_t(sm.bfirst[g] - R0);
+  for (uint32_t i = threadIdx.x; i < nrow; i += kThreads) {
+    const uint64_t r = R0 + i;
+    uint32_t lo = 0, hi = g;  // block of row r: bfirst[lo] <= r < bfirst[hi]
+    while (hi - lo > 1) {
+      const uint32_t m = (lo + hi) >> 1;
+      if (sm.bfirst[m] <= r)
+        lo = m;
+      else
+        hi = m;
+    }
+    sm.out[i] = sm.brel[lo] + Pg(P.pl, P.tp, int64_t(r) - 1) - sm.bbase[lo];
+    sm.ko[i] = P.key_off[r];
+    sm.kl[i] = P.key_len[r];
+    sm.vo[i] = P.val_off[r];
+    sm.vl[i] = P.val_len[r];
+  }
+  if (threadIdx.x == 0) sm.out[nrow] = nq << 4;
+  __syncthreads();
+  // chunk q belongs to the record whose span [out[i], out[i+1]) holds byte 16q
+  for (uint32_t i = threadIdx.x; i < nrow; i += kThreads) {
+    const uint32_t qa = uint32_t((sm.out[i] + 15) >> 4), qb = uint32_t((sm.out[i + 1] + 15) >> 4);
+    for (uint32_t q = qa; q < qb; ++q) sm.qrow[q] = uint16_t(i);
+  }
+  __syncthreads();
+  auto rec = [&](uint64_t i) {
+    RecInfo r;
+    r.rs = sm.out[i];
+    r.ko = sm.ko[i];
+    r.vo = sm.vo[i];
+    r.kl = sm.kl[i];
+    r.vl = sm.vl[i];
+    return r;
+  };
+  uint8_t* dst = P.seg + O0;
+  for (uint32_t q = threadIdx.x; q < nq; q += kThreads) {
+    const uint64_t pos = uint64_t(q) << 4;
+    *reinterpret_cast<uint4*>(dst + pos) = assemble_chunk(P, pos, sm.qrow[q], nrow, rec);
   }
 }
 
@@ -876,6 +1024,8 @@ uint32_t ceil_div(uint64_t a, uint64_t b) { return uint32_t((a + b - 1) / b); }
 
 struct Plan {
   uint64_t nb, data_bytes, meta_bytes, file_bytes, last_raw;
+  uint64_t w;     // most rows any block start can take (max next(a) - a)
+  uint64_t bmax;  // largest BlockSize
 };
 
 // Block boundaries, BlockStat sizes/offsets and meta layout (E1-E9).
@@ -961,6 +1111,8 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   pl->meta_bytes = e->h_tot->head + e->h_tot->meta_ent;
   pl->file_bytes = pl->data_bytes + pl->meta_bytes + 25;
   pl->last_raw = e->h_tot->last_raw;
+  pl->w = W;
+  pl->bmax = e->h_tot->bmax;
   return OKV_OK;
 }
 
@@ -980,7 +1132,13 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   pp.first = e->first;
   pp.desc = e->desc;
   pp.seg = seg;
-  if (o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0) {
+  const uint64_t G = std::min<uint64_t>(
+      {uint64_t(kMaxRegion), kPackRows / std::max<uint64_t>(pl.w, 1),
+       uint64_t(kMaxChunks) * 16 / std::max<uint64_t>(pl.bmax, 1)});
+  if (o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0 && G >= 1) {
+    hipLaunchKernelGGL(okv_enc_pack_region_kernel, dim3(ceil_div(pl.nb, G)), dim3(kThreads), 0,
+                       ctx->stream, pp, pl.nb, uint32_t(G));
+  } else if (o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0) {
     hipLaunchKernelGGL(okv_enc_pack_kernel, dim3(uint32_t(pl.nb)), dim3(kThreads), 0,
                        ctx->stream, pp);
   } else {

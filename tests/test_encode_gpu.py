@@ -252,3 +252,18 @@ def test_c4_shape_property(enc, decoder):
                           .reshape(-1, 64))
     h = decoder.hash_blocks(seg, md.descs)
     assert np.array_equal(h, md.hashes)
+
+
+def test_general_pack_path_vs_oracle(enc):
+    """Blocks over 64 KiB (a 150 KB value) and blocks of > 512 rows (7-byte
+    records under a 57 344-byte threshold) take the per-block pack kernel."""
+    rng = random.Random(11)
+    big = [(b"b%06d" % i, bytes(rng.getrandbits(8) for _ in range(150_000 if i % 5 == 2 else 40)))
+           for i in range(12)]
+    tiny = [(b"%c" % (33 + (i % 90)), b"") for i in range(20_000)]
+    for rows, T, D in ((big, 3584, 4096), (tiny, 57344, 65536), (big + tiny, 57344, 4096)):
+        rc, want, _ = oracle_segment(rows, T, D)
+        if rc:
+            continue
+        got = enc.encode(rows, T, D)
+        assert got.seg.tobytes() == want

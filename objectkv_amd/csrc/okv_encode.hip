@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -715,6 +716,8 @@ struct __align__(16) RegionSmem {
   uint64_t bbase[kMaxRegion];   // P(first row - 1)
 };
 
+template <int V>  // diagnostic ablation (OKV_ENC_VARIANT): 0 product, 1 tables only,
+                 // 2 tables + zero stores
 __global__ __launch_bounds__(kThreads) void okv_enc_pack_region_kernel(PackParams P, uint64_t nb,
                                                                        uint32_t G) {
   __shared__ RegionSmem sm;
@@ -769,10 +772,131 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_region_kernel(PackParam
     return r;
   };
   uint8_t* dst = P.seg + O0;
+  if (V == 1) return;
   for (uint32_t q = threadIdx.x; q < nq; q += kThreads) {
     const uint64_t pos = uint64_t(q) << 4;
-    *reinterpret_cast<uint4*>(dst + pos) = assemble_chunk(P, pos, sm.qrow[q], nrow, rec);
+    if (V == 2)
+      *reinterpret_cast<uint4*>(dst + pos) = make_uint4(sm.qrow[q], 0, 0, 0);
+    else
+      *reinterpret_cast<uint4*>(dst + pos) = assemble_chunk(P, pos, sm.qrow[q], nrow, rec);
   }
+}
+
+// E10, records smaller than a region: record-major assembly in LDS.  The
+// region's G blocks (<= kImage bytes) are built in an LDS image: zeroed (the
+// padding), then each lane ORs its records' header / key / value bytes in
+// (16-byte source windows realigned to the destination, all loads of a field
+// issued together), then the image is stored with aligned 16-byte stores.
+constexpr uint32_t kImage = 32768;
+
+// OR the first nbytes (<= 16; higher bytes of w must be zero) of w into the
+// LDS byte image at byte address d.
+__device__ __forceinline__ void lds_or16(uint32_t* img, uint32_t d, const uint4& w) {
+  const uint32_t a = d & 3, k = d >> 2;
+  const uint32_t sh = 8 * a;
+  // w shifted left by a bytes across five dwords
+  const uint32_t d0 = sh ? (w.x << sh) : w.x;
+  const uint32_t d1 = sh ? __builtin_amdgcn_alignbyte(w.y, w.x, 4 - a) : w.y;
+  const uint32_t d2 = sh ? __builtin_amdgcn_alignbyte(w.z, w.y, 4 - a) : w.z;
+  const uint32_t d3 = sh ? __builtin_amdgcn_alignbyte(w.w, w.z, 4 - a) : w.w;
+  const uint32_t d4 = sh ? (w.w >> (32 - sh)) : 0u;
+  atomicOr(img + k, d0);
+  atomicOr(img + k + 1, d1);
+  atomicOr(img + k + 2, d2);
+  atomicOr(img + k + 3, d3);
+  if (d4) atomicOr(img + k + 4, d4);
+}
+
+// Up to 4 windows (len <= 64) of a field from 5 prefetched source lines.
+struct Lines5 {
+  uint4 l[5];
+  uint32_t s;
+  uint32_t nwin;
+};
+__device__ __forceinline__ Lines5 load_lines5(const uint8_t* src, uint32_t len) {
+  Lines5 L;
+  const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
+  const uint4* line = reinterpret_cast<const uint4*>(sa & ~uintptr_t(15));
+  L.s = uint32_t(sa & 15);
+  L.nwin = (len + 15) >> 4;
+  const uint32_t nline = (L.s + len + 15) >> 4;
+#pragma unroll
+  for (int t = 0; t < 5; ++t)
+    L.l[t] = uint32_t(t) < nline ? line[t] : make_uint4(0, 0, 0, 0);
+  return L;
+}
+__device__ __forceinline__ void lds_put5(uint32_t* img, uint32_t d, const Lines5& L,
+                                         uint32_t len) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (uint32_t(t) >= L.nwin) break;
+    uint4 w = funnel32(L.l[t], L.l[t + 1], L.s);
+    const int32_t rem = int32_t(len) - 16 * t;
+    if (rem < 16) w = replace_from(w, make_uint4(0, 0, 0, 0), rem);
+    lds_or16(img, d + 16 * t, w);
+  }
+}
+
+// Copy len source bytes (len > 0) to image byte address d, 4 windows per
+// round with the round's 5 source lines loaded first.
+__device__ __forceinline__ void lds_copy_field(uint32_t* img, uint32_t d, const uint8_t* src,
+                                               uint64_t len) {
+  for (uint64_t j0 = 0; j0 < len; j0 += 64) {
+    const uint32_t part = uint32_t(std::min<uint64_t>(64, len - j0));
+    const Lines5 L = load_lines5(src + j0, part);
+    lds_put5(img, d + uint32_t(j0), L, part);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb,
+                                                                    uint32_t G) {
+  __shared__ uint4 img4[kImage / 16];
+  __shared__ uint64_t bfirst[kMaxRegion + 1], brel[kMaxRegion], bbase[kMaxRegion];
+  uint32_t* img = reinterpret_cast<uint32_t*>(img4);
+  const uint64_t k0 = uint64_t(blockIdx.x) * G;
+  const uint32_t g = uint32_t(std::min<uint64_t>(G, nb - k0));
+  const uint64_t O0 = P.desc[k0].offset;
+  const Desc dl = P.desc[k0 + g - 1];
+  const uint32_t nq = uint32_t((dl.offset + dl.block_size - O0) >> 4);
+  for (uint32_t q = threadIdx.x; q < nq; q += kThreads) img4[q] = make_uint4(0, 0, 0, 0);
+  if (threadIdx.x <= g) {
+    const uint32_t t = threadIdx.x;
+    const uint64_t f = P.first[k0 + t];
+    bfirst[t] = f;
+    if (t < g) {
+      brel[t] = P.desc[k0 + t].offset - O0;
+      bbase[t] = Pg(P.pl, P.tp, int64_t(f) - 1);
+    }
+  }
+  __syncthreads();
+  const uint64_t R0 = bfirst[0], R1 = bfirst[g];
+  for (uint64_t r = R0 + threadIdx.x; r < R1; r += kThreads) {
+    uint32_t lo = 0, hi = g;  // block of row r
+    while (hi - lo > 1) {
+      const uint32_t m = (lo + hi) >> 1;
+      if (bfirst[m] <= r)
+        lo = m;
+      else
+        hi = m;
+    }
+    const uint32_t d = uint32_t(brel[lo] + Pg(P.pl, P.tp, int64_t(r) - 1) - bbase[lo]);
+    const uint32_t kl = P.key_len[r], vl = P.val_len[r];
+    const uint64_t ko = P.key_off[r], vo = P.val_off[r];
+    if (kl <= 64 && vl <= 64) {  // all source lines of the record in flight at once
+      const Lines5 K = load_lines5(P.key_arena + ko, kl);
+      const Lines5 V = load_lines5(P.val_arena + vo, vl);
+      lds_or16(img, d, make_uint4(kl | (vl << 16), vl >> 16, 0, 0));
+      lds_put5(img, d + 6, K, kl);
+      if (vl) lds_put5(img, d + 6 + kl, V, vl);
+    } else {
+      lds_or16(img, d, make_uint4(kl | (vl << 16), vl >> 16, 0, 0));
+      lds_copy_field(img, d + 6, P.key_arena + ko, kl);
+      if (vl) lds_copy_field(img, d + 6 + kl, P.val_arena + vo, vl);
+    }
+  }
+  __syncthreads();
+  uint4* dst = reinterpret_cast<uint4*>(P.seg + O0);
+  for (uint32_t q = threadIdx.x; q < nq; q += kThreads) dst[q] = img4[q];
 }
 
 // E10 (general DataBlockSize, not a multiple of 16): one byte per lane.
@@ -1026,6 +1150,7 @@ struct Plan {
   uint64_t nb, data_bytes, meta_bytes, file_bytes, last_raw;
   uint64_t w;     // most rows any block start can take (max next(a) - a)
   uint64_t bmax;  // largest BlockSize
+  uint64_t avg_rec;  // mean record size
 };
 
 // Block boundaries, BlockStat sizes/offsets and meta layout (E1-E9).
@@ -1113,6 +1238,7 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   pl->last_raw = e->h_tot->last_raw;
   pl->w = W;
   pl->bmax = e->h_tot->bmax;
+  pl->avg_rec = e->h_tot->total_raw / n;
   return OKV_OK;
 }
 
@@ -1135,9 +1261,27 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   const uint64_t G = std::min<uint64_t>(
       {uint64_t(kMaxRegion), kPackRows / std::max<uint64_t>(pl.w, 1),
        uint64_t(kMaxChunks) * 16 / std::max<uint64_t>(pl.bmax, 1)});
-  if (o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0 && G >= 1) {
-    hipLaunchKernelGGL(okv_enc_pack_region_kernel, dim3(ceil_div(pl.nb, G)), dim3(kThreads), 0,
-                       ctx->stream, pp, pl.nb, uint32_t(G));
+  // record-major LDS assembly pays off for small records (most chunks would
+  // mix fields); large records take the chunk-major kernels
+  const uint64_t GL = std::min<uint64_t>(kMaxRegion, kImage / std::max<uint64_t>(pl.bmax, 1));
+  const bool aligned = o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0;
+  const char* evar = getenv("OKV_ENC_VARIANT");
+  const int EV = evar ? atoi(evar) : 0;
+  if (aligned && GL >= 1 && pl.avg_rec <= 512 && EV != 3) {
+    hipLaunchKernelGGL(okv_enc_pack_lds_kernel, dim3(ceil_div(pl.nb, GL)), dim3(kThreads), 0,
+                       ctx->stream, pp, pl.nb, uint32_t(GL));
+  } else if (aligned && G >= 1) {
+    const int V = EV;
+    const dim3 grid(ceil_div(pl.nb, G)), blk(kThreads);
+    if (V == 1)
+      hipLaunchKernelGGL(okv_enc_pack_region_kernel<1>, grid, blk, 0, ctx->stream, pp, pl.nb,
+                         uint32_t(G));
+    else if (V == 2)
+      hipLaunchKernelGGL(okv_enc_pack_region_kernel<2>, grid, blk, 0, ctx->stream, pp, pl.nb,
+                         uint32_t(G));
+    else
+      hipLaunchKernelGGL(okv_enc_pack_region_kernel<0>, grid, blk, 0, ctx->stream, pp, pl.nb,
+                         uint32_t(G));
   } else if (o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0) {
     hipLaunchKernelGGL(okv_enc_pack_kernel, dim3(uint32_t(pl.nb)), dim3(kThreads), 0,
                        ctx->stream, pp);

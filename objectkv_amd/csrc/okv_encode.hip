@@ -298,8 +298,11 @@ __global__ __launch_bounds__(kThreads) void okv_enc_next_kernel(
     uint32_t* __restrict__ nx, EncTotals* __restrict__ tot) {
   __shared__ uint64_t W[kETile + kLook + 1];
   const uint64_t cs = uint64_t(blockIdx.x) * kETile;
-  // W[m] = P(cs - 1 + m), m < M
-  const uint64_t M = std::min<uint64_t>(n - cs + 1, kETile + kLook + 1);
+  // a block holds at most ceil(T / smallest record) + 1 rows: stage only that
+  // much lookahead.  W[m] = P(cs - 1 + m), m < M
+  const uint64_t msz = std::max<uint64_t>(tot->min_size, 1);
+  const uint64_t look = std::min<uint64_t>(kLook, T / msz + 2);
+  const uint64_t M = std::min<uint64_t>(n - cs + 1, kETile + look + 1);
   for (uint32_t m = threadIdx.x; m < M; m += kThreads) W[m] = Pg(pl, tp, int64_t(cs + m) - 1);
   __syncthreads();
   const bool complete = cs - 1 + M == n;  // the window reaches the last row
@@ -548,6 +551,7 @@ struct PackParams {
   const uint64_t* first;
   const Desc* desc;
   uint8_t* seg;
+  uint64_t* hash;  // BlockStat.Hash, written by kernels that hash in LDS
 };
 
 struct __align__(16) PackSmem {
@@ -897,6 +901,65 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P
   __syncthreads();
   uint4* dst = reinterpret_cast<uint4*>(P.seg + O0);
   for (uint32_t q = threadIdx.x; q < nq; q += kThreads) dst[q] = img4[q];
+  // BlockStat.Hash = XXH64 of the padded block (segment_writer.go:185), from
+  // the image: four lanes per block own XXH64's four accumulators.
+  if (threadIdx.x < 4 * g) {
+    const uint32_t b = threadIdx.x >> 2, q = threadIdx.x & 3;
+    const uint32_t boff = uint32_t(brel[b]);
+    const uint64_t len = P.desc[k0 + b].block_size;
+    const uint64_t* w64 = reinterpret_cast<const uint64_t*>(img4) + (boff >> 3);
+    uint64_t acc = (q == 0) ? XP1 + XP2 : (q == 1) ? XP2 : (q == 2) ? 0 : 0 - XP1;
+    const uint32_t nstripe = uint32_t(len / 32);
+    uint32_t st = 0;
+    for (; st + 8 <= nstripe; st += 8) {  // 8 LDS reads ahead of the multiply chain
+      uint64_t x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = w64[4 * (st + u) + q];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = xround(acc, x[u]);
+    }
+    for (; st < nstripe; ++st) acc = xround(acc, w64[4 * st + q]);
+    const int lane = threadIdx.x & 63;
+    const uint64_t a1 = __shfl(acc, (lane & ~3) + 1, 64);
+    const uint64_t a2 = __shfl(acc, (lane & ~3) + 2, 64);
+    const uint64_t a3 = __shfl(acc, (lane & ~3) + 3, 64);
+    if (q == 0) {
+      uint64_t h;
+      if (len >= 32) {
+        h = rotl64(acc, 1) + rotl64(a1, 7) + rotl64(a2, 12) + rotl64(a3, 18);
+        h = (h ^ xround(0, acc)) * XP1 + XP4;
+        h = (h ^ xround(0, a1)) * XP1 + XP4;
+        h = (h ^ xround(0, a2)) * XP1 + XP4;
+        h = (h ^ xround(0, a3)) * XP1 + XP4;
+      } else {
+        h = XP5;
+      }
+      h += len;
+      const uint8_t* bytes = reinterpret_cast<const uint8_t*>(img4) + boff;
+      uint32_t t = nstripe * 32;
+      for (; t + 8 <= len; t += 8) {
+        h ^= xround(0, w64[t / 8]);
+        h = rotl64(h, 27) * XP1 + XP4;
+      }
+      if (t + 4 <= len) {
+        const uint32_t v = uint32_t(bytes[t]) | (uint32_t(bytes[t + 1]) << 8) |
+                           (uint32_t(bytes[t + 2]) << 16) | (uint32_t(bytes[t + 3]) << 24);
+        h ^= uint64_t(v) * XP1;
+        h = rotl64(h, 23) * XP2 + XP3;
+        t += 4;
+      }
+      for (; t < len; ++t) {
+        h ^= uint64_t(bytes[t]) * XP5;
+        h = rotl64(h, 11) * XP1;
+      }
+      h ^= h >> 33;
+      h *= XP2;
+      h ^= h >> 29;
+      h *= XP3;
+      h ^= h >> 32;
+      P.hash[k0 + b] = h;
+    }
+  }
 }
 
 // E10 (general DataBlockSize, not a multiple of 16): one byte per lane.
@@ -961,7 +1024,8 @@ struct MetaParams {
   const Desc* desc;
   const uint64_t* hash;
   const uint64_t* moff;
-  uint64_t nb;
+  uint64_t nb;      // entries written by this launch
+  uint64_t count;   // block index entries (the head's u64 count, :320)
   int comp_byte;
   uint8_t* meta;
 };
@@ -980,7 +1044,7 @@ __global__ __launch_bounds__(kThreads) void okv_enc_meta_kernel(MetaParams P) {
     p[0] = 0;  // no bloom filter
     p[1] = uint8_t(P.comp_byte);
     p[2] = 0;  // not a partitioned block index
-    put_le(p + 3, P.nb, 8);
+    put_le(p + 3, P.count, 8);
   }
   if (k >= P.nb) return;
   uint8_t* p = P.meta + P.moff[k];
@@ -995,6 +1059,72 @@ __global__ __launch_bounds__(kThreads) void okv_enc_meta_kernel(MetaParams P) {
   put_le(p + 16, d.original_size, 8);
   put_le(p + 24, d.compressed_size, 8);
   put_le(p + 32, P.hash[k], 8);
+}
+
+// E12 via LDS: one workgroup builds the entries of kThreads consecutive blocks
+// (one contiguous byte range of the meta block, <= kImage bytes) in an LDS
+// image and stores it with aligned 16-byte stores; the range's unaligned head
+// and tail bytes (shared with neighbouring workgroups) are stored bytewise.
+__global__ __launch_bounds__(kThreads) void okv_enc_meta_lds_kernel(MetaParams P,
+                                                                    uint64_t meta_bytes) {
+  __shared__ uint4 img4[kImage / 16 + 2];
+  __shared__ int big;
+  uint32_t* img = reinterpret_cast<uint32_t*>(img4);
+  const uint64_t k0 = uint64_t(blockIdx.x) * kThreads;
+  const uint64_t k1 = std::min<uint64_t>(P.nb, k0 + kThreads);
+  const uint64_t lo = P.moff[k0];
+  const uint64_t hi = k1 < P.nb ? P.moff[k1] : meta_bytes;
+  const uint64_t a0 = lo & ~uint64_t(15);  // image byte 0 = meta byte a0
+  const uint32_t nq = uint32_t((hi - a0 + 15) >> 4);
+  if (threadIdx.x == 0) big = (hi - a0 + 15) > kImage;
+  __syncthreads();
+  const uint64_t k = k0 + threadIdx.x;
+  if (big) {  // long first keys: byte stores
+    if (k < k1) {
+      uint8_t* p = P.meta + P.moff[k];
+      const uint64_t r = P.first[k];
+      const uint32_t kl = P.key_len[r];
+      put_le(p, kl, 2);
+      put_bytes(p + 2, P.key_arena + P.key_off[r], kl);
+      p += 2 + kl;
+      const Desc d = P.desc[k];
+      put_le(p, d.offset, 8);
+      put_le(p + 8, d.block_size, 8);
+      put_le(p + 16, d.original_size, 8);
+      put_le(p + 24, d.compressed_size, 8);
+      put_le(p + 32, P.hash[k], 8);
+    }
+    return;
+  }
+  for (uint32_t q = threadIdx.x; q < nq; q += kThreads) img4[q] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  if (k < k1) {
+    const uint32_t d = uint32_t(P.moff[k] - a0);
+    const uint64_t r = P.first[k];
+    const uint32_t kl = P.key_len[r];
+    const Desc ds = P.desc[k];
+    const uint64_t h = P.hash[k];
+    lds_or16(img, d, make_uint4(kl & 0xffffu, 0, 0, 0));  // only 2 bytes are non-zero
+    lds_copy_field(img, d + 2, P.key_arena + P.key_off[r], kl);
+    const uint32_t e = d + 2 + kl;
+    lds_or16(img, e, make_uint4(uint32_t(ds.offset), uint32_t(ds.offset >> 32),
+                                uint32_t(ds.block_size), uint32_t(ds.block_size >> 32)));
+    lds_or16(img, e + 16, make_uint4(uint32_t(ds.original_size), uint32_t(ds.original_size >> 32),
+                                     uint32_t(ds.compressed_size),
+                                     uint32_t(ds.compressed_size >> 32)));
+    lds_or16(img, e + 32, make_uint4(uint32_t(h), uint32_t(h >> 32), 0, 0));
+  }
+  __syncthreads();
+  const uint8_t* ib = reinterpret_cast<const uint8_t*>(img4);
+  for (uint32_t q = threadIdx.x; q < nq; q += kThreads) {
+    const uint64_t c0 = a0 + 16 * uint64_t(q);
+    if (c0 >= lo && c0 + 16 <= hi) {
+      *reinterpret_cast<uint4*>(P.meta + c0) = img4[q];
+    } else {  // shared with a neighbouring range
+      for (uint32_t b = 0; b < 16; ++b)
+        if (c0 + b >= lo && c0 + b < hi) P.meta[c0 + b] = ib[16 * q + b];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1258,6 +1388,8 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   pp.first = e->first;
   pp.desc = e->desc;
   pp.seg = seg;
+  pp.hash = e->hash;
+  bool hashed = false;
   const uint64_t G = std::min<uint64_t>(
       {uint64_t(kMaxRegion), kPackRows / std::max<uint64_t>(pl.w, 1),
        uint64_t(kMaxChunks) * 16 / std::max<uint64_t>(pl.bmax, 1)});
@@ -1270,6 +1402,7 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   if (aligned && GL >= 1 && pl.avg_rec <= 512 && EV != 3) {
     hipLaunchKernelGGL(okv_enc_pack_lds_kernel, dim3(ceil_div(pl.nb, GL)), dim3(kThreads), 0,
                        ctx->stream, pp, pl.nb, uint32_t(GL));
+    hashed = true;
   } else if (aligned && G >= 1) {
     const int V = EV;
     const dim3 grid(ceil_div(pl.nb, G)), blk(kThreads);
@@ -1291,7 +1424,7 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
                        dim3(kThreads), 0, ctx->stream, pp, pl.nb, pl.data_bytes);
   }
   enc_mark(ctx, e, 2);
-  launch_hash(ctx->stream, seg, pl.data_bytes, e->desc, uint32_t(pl.nb), e->hash);
+  if (!hashed) launch_hash(ctx->stream, seg, pl.data_bytes, e->desc, uint32_t(pl.nb), e->hash);
   enc_mark(ctx, e, 3);
   MetaParams mp;
   mp.key_arena = R.ka;
@@ -1303,10 +1436,20 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   mp.hash = e->hash;
   mp.moff = e->moff;
   mp.nb = pl.nb;
+  mp.count = pl.nb;
   mp.comp_byte = o.compression == OKV_COMP_LZ4 ? 2 : 0;
   mp.meta = seg + pl.data_bytes;
-  hipLaunchKernelGGL(okv_enc_meta_kernel, dim3(ceil_div(pl.nb, kThreads)), dim3(kThreads), 0,
-                     ctx->stream, mp);
+  if ((reinterpret_cast<uintptr_t>(mp.meta) & 15) == 0) {
+    // head bytes by the first lane of a one-block launch (nb = 0), entries via LDS
+    MetaParams head = mp;
+    head.nb = 0;
+    hipLaunchKernelGGL(okv_enc_meta_kernel, dim3(1), dim3(64), 0, ctx->stream, head);
+    hipLaunchKernelGGL(okv_enc_meta_lds_kernel, dim3(ceil_div(pl.nb, kThreads)), dim3(kThreads),
+                       0, ctx->stream, mp, pl.meta_bytes);
+  } else {
+    hipLaunchKernelGGL(okv_enc_meta_kernel, dim3(ceil_div(pl.nb, kThreads)), dim3(kThreads), 0,
+                       ctx->stream, mp);
+  }
   enc_mark(ctx, e, 4);
   OKV_HIP(hipGetLastError());
   return OKV_OK;

@@ -395,7 +395,8 @@ def run_encode(args, torch, okv, dist, world, rank, local, dev):
         "close_ms": round(close_ms, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "okv_enc_pack_kernel", "algorithmic_bytes_per_launch": int(alg)},
+                     "kernel": "okv_enc_pack_lds_kernel (pack + block XXH64)",
+                     "algorithmic_bytes_per_launch": int(alg)},
         "cpu_baseline": cpu,
     }
     if rank == 0:

@@ -256,3 +256,26 @@ def test_golden_synth_cases_match_oracle(golden):
         for k in ("row_start", "key_off", "key_len", "val_off", "val_len", "key_arena",
                   "val_arena", "key_base", "val_base", "status"):
             assert hashlib.sha256(o[k].tobytes()).hexdigest() == c["full"][k], (name, k)
+
+
+def test_encode_cpu_baseline_matches_writer():
+    """bench.py's C4 CPU leg (oref_encode_go) writes the oracle writer's bytes:
+    one shard = one segment; k shards = k key-range segments."""
+    import numpy as np
+    from objectkv_amd.sst import pack_rows
+    rows = [(b"key%05d" % i, b"v" * (i % 97)) for i in range(3001)]  # no shard ends a block (Q1)
+    soa = pack_rows(rows)
+
+    def seg_len(rs):
+        w = CO.Writer(3584, 4096)
+        for k, v in rs:
+            assert w.write_row(k, v) == 0
+        rc, data, _ = w.close()
+        assert rc == 0
+        return len(data)
+
+    assert CO.encode_go(soa, len(rows), 3584, 4096, False, 1) == seg_len(rows)
+    n = len(rows)
+    want = sum(seg_len(rows[n * t // 4:n * (t + 1) // 4]) for t in range(4))
+    assert CO.encode_go(soa, n, 3584, 4096, False, 4) == want
+    assert isinstance(soa["key_off"], np.ndarray)

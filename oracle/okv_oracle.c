@@ -7,6 +7,7 @@
  */
 #include "okv_oracle.h"
 
+#include <dlfcn.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -398,16 +399,65 @@ int oref_fetch_meta(const uint8_t *buf, uint64_t buf_len, int64_t file_bytes, or
 /* ======================================================================= */
 /* ReadBlockWithStat (segment_reader.go:295-355)                            */
 /* ======================================================================= */
-/* Shared bounds logic: the raw buffer is seg[off, off+block_size) (:309-316)
- * or, for LZ4, an empty buffer (:331-333).  Returns block status and sets
- * *buf and *buf_len. */
+/* zstd: zstd.NewReader(bytes.NewReader(rawBlockBytes[:CompressedSize])) and
+ * io.Copy (:320-330), klauspost/compress v1.17.9 = standard RFC 8878 decoding
+ * of every frame in the slice.  Checker: the system libzstd (dlopen, no
+ * headers needed), the RFC's reference implementation. */
+typedef size_t (*zstd_dec_fn)(void *, size_t, const void *, size_t);
+typedef unsigned (*zstd_iserr_fn)(size_t);
+typedef int (*zstd_code_fn)(size_t);
+static zstd_dec_fn z_dec;
+static zstd_iserr_fn z_iserr;
+static zstd_code_fn z_code;
+static pthread_once_t z_once = PTHREAD_ONCE_INIT;
+static void zstd_load(void) {
+  void *h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) return;
+  z_dec = (zstd_dec_fn)dlsym(h, "ZSTD_decompress");
+  z_iserr = (zstd_iserr_fn)dlsym(h, "ZSTD_isError");
+  z_code = (zstd_code_fn)dlsym(h, "ZSTD_getErrorCode");
+}
+static int zstd_block(const uint8_t *src, uint64_t n, uint64_t hint, uint8_t **out,
+                      uint64_t *out_len) {
+  pthread_once(&z_once, zstd_load);
+  if (!z_dec || !z_iserr || !z_code) return OREF_BLK_UNSUPPORTED;
+  uint64_t cap = hint + 65536;
+  for (;;) {
+    uint8_t *buf = (uint8_t *)malloc(cap);
+    size_t r = z_dec(buf, cap, n ? src : (const uint8_t *)"", n);
+    if (!z_iserr(r)) {
+      *out = buf;
+      *out_len = r;
+      return OREF_BLK_OK;
+    }
+    free(buf);
+    if (z_code(r) != 70 /* dstSize_tooSmall */ || cap > (1ull << 31)) return OREF_BLK_ZSTD;
+    cap *= 2;
+  }
+}
+
+/* Shared bounds logic: the raw buffer is seg[off, off+block_size) (:309-316),
+ * for LZ4 an empty buffer (:331-333), for zstd the decompressed frames (then
+ * *owned is set and the caller frees it).  Returns the block status. */
 static int block_buffer(const uint8_t *seg, uint64_t seg_len, const oref_block_desc *d,
-                        int compression, const uint8_t **buf, uint64_t *buf_len) {
+                        int compression, const uint8_t **buf, uint64_t *buf_len,
+                        uint8_t **owned) {
+  *owned = NULL;
   if ((int64_t)d->offset < 0) return OREF_BLK_EOF; /* Seek error :303-306 */
   if (d->offset >= seg_len) return OREF_BLK_EOF;   /* bytes.Reader.Read io.EOF :310-313 */
   uint64_t avail = seg_len - d->offset;
   if (avail < d->block_size) return OREF_BLK_SHORT; /* :314-316 */
-  if (compression == OREF_COMP_ZSTD) return OREF_BLK_UNSUPPORTED; /* :320-330 */
+  if (compression == OREF_COMP_ZSTD) {
+    if (d->compressed_size > d->block_size) return OREF_BLK_PANIC; /* slice bounds :321 */
+    uint8_t *o = NULL;
+    uint64_t n = 0;
+    int st = zstd_block(seg + d->offset, d->compressed_size, d->original_size, &o, &n);
+    if (st) return st;
+    *owned = o;
+    *buf = o;
+    *buf_len = n;
+    return OREF_BLK_OK;
+  }
   *buf = seg + d->offset;
   *buf_len = (compression == OREF_COMP_LZ4) ? 0 : d->block_size; /* :331-335 (Q7) */
   return OREF_BLK_OK;
@@ -456,11 +506,13 @@ int oref_read_block(const uint8_t *seg, uint64_t seg_len, const oref_block_desc 
   memset(out, 0, sizeof(*out));
   const uint8_t *buf = NULL;
   uint64_t len = 0;
-  int st = block_buffer(seg, seg_len, d, compression, &buf, &len);
+  uint8_t *owned = NULL;
+  int st = block_buffer(seg, seg_len, d, compression, &buf, &len, &owned);
   if (st) return st;
   /* rawBlockBytes := make([]byte, BlockSize); Read (:309-310) -- a copy */
   uint8_t *copy = (uint8_t *)malloc(len ? len : 1);
   if (len) memcpy(copy, buf, len);
+  free(owned);
   go_ctx g = {copy, out};
   st = walk_records(copy, len, d->original_size, go_row, &g);
   free(copy);
@@ -606,8 +658,10 @@ void oref_block_counts(const uint8_t *seg, uint64_t seg_len, const oref_block_de
     const uint8_t *buf = NULL;
     uint64_t len = 0;
     cnt_ctx c = {0, 0, 0};
-    int st = block_buffer(seg, seg_len, &d[b], compression, &buf, &len);
+    uint8_t *owned = NULL;
+    int st = block_buffer(seg, seg_len, &d[b], compression, &buf, &len, &owned);
     if (!st) st = walk_records(buf, len, d[b].original_size, cnt_row, &c);
+    free(owned);
     if (st) c = (cnt_ctx){0, 0, 0}; /* a failed block contributes no rows */
     status[b] = st;
     rows[b] = c.rows;
@@ -660,13 +714,20 @@ void oref_decode_soa(const uint8_t *seg, uint64_t seg_len, const oref_block_desc
     }
     const uint8_t *buf = NULL;
     uint64_t len = 0;
-    int st = block_buffer(seg, seg_len, &d[b], compression, &buf, &len);
+    uint8_t *owned = NULL;
+    int st = block_buffer(seg, seg_len, &d[b], compression, &buf, &len, &owned);
+    if (!st && index_only && compression == OREF_COMP_ZSTD)
+      st = OREF_BLK_UNSUPPORTED; /* spans into seg do not exist for zstd blocks */
     if (!st) st = walk_records(buf, len, d[b].original_size, NULL, NULL); /* validate first */
     status[b] = st;
-    if (st) continue;
+    if (st) {
+      free(owned);
+      continue;
+    }
     soa_ctx s = {buf, d[b].offset, index_only, g, kb, vb, key_off, val_off, key_len, val_len,
                  key_arena, val_arena};
     walk_records(buf, len, d[b].original_size, soa_row, &s);
+    free(owned);
     g = s.g;
     if (!index_only) {
       /* each block's arena region is padded with zeros to a 16-byte multiple */

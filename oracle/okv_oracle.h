@@ -48,7 +48,8 @@ extern "C" {
 #define OREF_BLK_EOF 1         /* reader.Read / Seek error (:303-313) */
 #define OREF_BLK_SHORT 2       /* ErrUnexpectedBytesRead error (:314-316) */
 #define OREF_BLK_PANIC 3       /* mustReadBytes panic in the record loop (:338-352, :506-512) */
-#define OREF_BLK_UNSUPPORTED 4 /* zstd block (decoder not restated here) */
+#define OREF_BLK_UNSUPPORTED 4 /* index-only spans of a zstd block; libzstd missing */
+#define OREF_BLK_ZSTD 6        /* zstd.NewReader / io.Copy error (:321-330) */
 
 #define OREF_COMP_NONE 0
 #define OREF_COMP_ZSTD 1

@@ -55,6 +55,7 @@ FATAL = {ErrInvalidMagicNumber, ErrUnknownSegmentVersion, ErrMismatchedMetaBlock
 
 # per-block status codes shared with include/okv_sst.h
 BLK_OK, BLK_EOF, BLK_SHORT, BLK_PANIC, BLK_UNSUPPORTED = 0, 1, 2, 3, 4
+BLK_ZSTD_ERROR = 6  # zstd.NewReader / io.Copy error (segment_reader.go:321-330)
 COMP_NONE, COMP_ZSTD, COMP_LZ4 = 0, 1, 2
 
 # ---- XXH64 (cespare/xxhash v2.2.0; segment_writer.go:185, :248) --------------
@@ -390,8 +391,18 @@ def read_block(seg: bytes, desc, compression: int):
     if len(seg) - off < bsize:
         return BLK_SHORT, None  # :314-316
     if compression == COMP_ZSTD:
-        return BLK_UNSUPPORTED, None
-    buf = b"" if compression == COMP_LZ4 else seg[off:off + bsize]  # :331-335 (Q7)
+        # zstd.NewReader(bytes.NewReader(rawBlockBytes[:stat.CompressedSize])) + io.Copy
+        # (:320-330); the decoder is klauspost v1.17.9 (standard RFC 8878 frames),
+        # checked here with libzstd (oracle/zstd_ref.py)
+        csize = desc[3] if len(desc) > 3 else 0
+        if csize > bsize:
+            return BLK_PANIC, None  # slice bounds out of range
+        from oracle import zstd_ref
+        buf = zstd_ref.decompress(seg[off:off + csize], orig)
+        if buf is None:
+            return BLK_ZSTD_ERROR, None
+    else:
+        buf = b"" if compression == COMP_LZ4 else seg[off:off + bsize]  # :331-335 (Q7)
     rows = None
     p = 0
     n = len(buf)
@@ -657,6 +668,8 @@ def decode_soa(seg: bytes, descs, compression: int, index_only: bool = False):
         out["key_base"].append(len(ka))
         out["val_base"].append(len(va))
         status, rows = read_block(seg, d, compression)
+        if index_only and compression == COMP_ZSTD and status == BLK_OK:
+            status, rows = BLK_UNSUPPORTED, None  # spans into seg do not exist for zstd
         out["status"].append(status)
         if status != BLK_OK:
             continue

@@ -279,3 +279,28 @@ def test_encode_cpu_baseline_matches_writer():
     want = sum(seg_len(rows[n * t // 4:n * (t + 1) // 4]) for t in range(4))
     assert CO.encode_go(soa, n, 3584, 4096, False, 4) == want
     assert isinstance(soa["key_off"], np.ndarray)
+
+
+def test_zstd_blocks_c_and_python_oracles_agree():
+    """zstd blocks (segment_reader.go:320-330) through both oracles' libzstd
+    checker: statuses, rows and arenas agree; full + index-only layouts."""
+    from tests import zstd_cases as ZC
+    for name, seg, descs, _note in ZC.cases():
+        for index_only in (False, True):
+            py = P.decode_soa(seg, descs, P.COMP_ZSTD, index_only)
+            c = CO.decode_soa(seg, CO.descs_array(descs), P.COMP_ZSTD, index_only)
+            assert list(c["status"]) == py["status"], name
+            if not index_only:
+                assert set(py["status"]) == {0}, name
+                assert c["key_arena"].tobytes() == py["key_arena"]
+                assert c["val_arena"].tobytes() == py["val_arena"]
+                assert list(c["key_len"]) == py["key_len"]
+                assert list(c["val_off"]) == py["val_off"]
+            else:
+                assert set(py["status"]) == {P.BLK_UNSUPPORTED}, name
+    want = {"payload_flip": P.BLK_ZSTD_ERROR, "truncated": P.BLK_ZSTD_ERROR,
+            "csize_gt_bsize": P.BLK_PANIC, "empty_ok": P.BLK_OK, "empty_panics": P.BLK_PANIC}
+    for name, seg, descs in ZC.corrupt_cases():
+        py = P.decode_soa(seg, descs, P.COMP_ZSTD)
+        c = CO.decode_soa(seg, CO.descs_array(descs), P.COMP_ZSTD)
+        assert py["status"] == [want[name]] and list(c["status"]) == py["status"], name

@@ -41,8 +41,10 @@ extern "C" {
 #define OKV_R_BLOCK_SHORT (-306)     /* ReadBlockWithStat: ErrUnexpectedBytesRead (:314-316) */
 #define OKV_R_PANIC (-307)           /* a Go panic: mustReadBytes (:506-512) or rows[0] of an
                                         empty block (segment_row_iter.go:95, :147) */
-#define OKV_R_UNSUPPORTED (-308)     /* zstd block (device zstd not implemented yet) */
+#define OKV_R_UNSUPPORTED (-308)     /* a block the device decode does not support */
 #define OKV_R_GPU (-309)             /* the GPU decode itself failed (okv_last_error) */
+#define OKV_R_ZSTD (-310)            /* zstd decoder error: ReadBlockWithStat's io.Copy error
+                                        (segment_reader.go:326-330) */
 
 /* ---- SegmentWriter ------------------------------------------------------- */
 typedef struct okv_writer okv_writer;

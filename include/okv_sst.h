@@ -57,12 +57,14 @@ extern "C" {
 #define OKV_BLK_EOF 1         /* Seek/Read error: offset >= segment length (:303-313) -> Go error */
 #define OKV_BLK_SHORT 2       /* short read, ErrUnexpectedBytesRead (:314-316) -> Go error */
 #define OKV_BLK_PANIC 3       /* record overruns the block buffer: mustReadBytes panics (:338-352, :506-512) */
-#define OKV_BLK_UNSUPPORTED 4 /* zstd block: not decoded on device yet (:320-330) */
-#define OKV_BLK_CAPACITY 5    /* output capacity exceeded (library-specific; never a Go outcome) */
+#define OKV_BLK_UNSUPPORTED 4 /* zstd block under OKV_F_INDEX_ONLY (no spans into seg exist) */
+#define OKV_BLK_CAPACITY 5    /* output capacity exceeded, or a zstd block decompressing past
+                                 its OriginalSize (library-specific; never a Go-written block) */
+#define OKV_BLK_ZSTD_ERROR 6  /* zstd.NewReader / io.Copy error (:321-330) -> Go error */
 
 /* ---- compression byte of the meta block (segment_reader.go:166-172) ----- */
 #define OKV_COMP_NONE 0
-#define OKV_COMP_ZSTD 1
+#define OKV_COMP_ZSTD 1 /* decoded on the device (okv_zstd.hip); not with OKV_F_INDEX_ONLY */
 #define OKV_COMP_LZ4 2 /* reference quirk Q7: decodes as an empty buffer */
 
 /* ---- flags ---------------------------------------------------------------- */

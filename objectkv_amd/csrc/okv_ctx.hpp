@@ -16,6 +16,14 @@ void enc_release(okv_ctx* ctx);
 // okv_decode.hip: enqueue XXH64 of each block's BlockSize bytes (device pointers).
 void launch_hash(hipStream_t stream, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
                  uint32_t nblk, uint64_t* out);
+// okv_zstd.hip: zstd block decompression into per-block scratch regions.
+void launch_zstd_cap(hipStream_t s, const Desc* descs, uint32_t nblk, uint64_t* cap_off);
+void launch_zstd(hipStream_t s, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
+                 uint32_t nblk, const uint64_t* cap_off, uint8_t* dec, uint64_t* dec_len,
+                 int32_t* zstatus, uint8_t* lit, uint32_t grid);
+void launch_zstd_desc(hipStream_t s, const Desc* descs, uint32_t nblk, const uint64_t* cap_off,
+                      const uint64_t* dec_len, Desc* out);
+constexpr uint32_t kZstdLitBytes = 1u << 17;  // per-wave literal scratch (Block_Maximum_Size)
 }  // namespace okv
 
 struct okv_ctx {
@@ -51,6 +59,16 @@ struct okv_ctx {
   double prof_ms[3] = {0, 0, 0};
   uint64_t prof_calls = 0;
   okv::EncScratch* enc = nullptr;  // encode scratch (okv_encode.hip)
+  // zstd decompression scratch (okv_zstd.hip)
+  uint64_t* z_cap_off = nullptr;  // [nblk + 1] decompressed-region offsets
+  uint64_t* z_dec_len = nullptr;  // [nblk]
+  int32_t* z_status = nullptr;    // [nblk]
+  okv::Desc* z_desc = nullptr;    // [nblk] descriptors of the decompressed blocks
+  size_t z_cap_blocks = 0;
+  uint8_t* z_dec = nullptr;       // decompressed blocks
+  size_t z_cap_dec = 0;
+  uint8_t* z_lit = nullptr;       // per-wave literal scratch
+  size_t z_cap_lit = 0;
 };
 
 namespace okv {

@@ -41,19 +41,22 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     const uint8_t* __restrict__ seg, uint64_t seg_bytes, const Desc* __restrict__ descs,
     uint32_t nblk, int comp, BlockCount* __restrict__ cnt, Prefix* __restrict__ lp,
     Prefix* __restrict__ tile_tot, uint32_t* __restrict__ rec_s, uint32_t* __restrict__ big_list,
-    uint32_t* __restrict__ big_count) {
+    uint32_t* __restrict__ big_count, const int32_t* __restrict__ pre_status) {
   const uint32_t tid = threadIdx.x;
   const uint32_t b = blockIdx.x * kTile + tid;
   uint64_t rows = 0, kb = 0, vb = 0, p = 0;
   int32_t st = OKV_BLK_OK;
   if (b < nblk) {
     const Desc d = descs[b];
-    if (int64_t(d.offset) < 0 || d.offset >= seg_bytes) {
+    const int32_t pre = pre_status ? pre_status[b] : int32_t(OKV_BLK_OK);
+    if (pre != OKV_BLK_OK) {
+      st = pre;  // outcome of the zstd stage (raw-block bounds, decoder error)
+    } else if (int64_t(d.offset) < 0 || d.offset >= seg_bytes) {
       st = OKV_BLK_EOF;  // Seek error / bytes.Reader io.EOF (:303-313)
     } else if (seg_bytes - d.offset < d.block_size) {
       st = OKV_BLK_SHORT;  // ErrUnexpectedBytesRead (:314-316)
     } else if (comp == OKV_COMP_ZSTD) {
-      st = OKV_BLK_UNSUPPORTED;  // :320-330 (device zstd: SURVEY §8f)
+      st = OKV_BLK_UNSUPPORTED;  // index-only spans cannot point into decompressed bytes
     } else {
       const uint64_t len = (comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
       const uint64_t orig = d.original_size;
@@ -824,18 +827,64 @@ void prof_mark(okv_ctx* ctx, int k) {
   if (e && k == 3) ctx->ev_used += 4;
 }
 
+// Working inputs of passes 1-3: the segment itself, or for zstd blocks the
+// decompressed bytes (okv_zstd.hip) with per-block statuses from that stage.
+struct Work {
+  const uint8_t* seg;
+  uint64_t seg_bytes;
+  const Desc* descs;
+  int comp;
+  const int32_t* pre;
+};
+
+int prepare(okv_ctx* ctx, const uint8_t* d_seg, uint64_t seg_bytes, const Desc* d_desc,
+            uint32_t nblk, int comp, bool index_only, Work* w) {
+  *w = Work{d_seg, seg_bytes, d_desc, comp, nullptr};
+  if (comp != OKV_COMP_ZSTD || index_only || nblk == 0) return OKV_OK;
+  int rc;
+  if (nblk + 1 > ctx->z_cap_blocks || !ctx->z_cap_off) {
+    OKV_HIP(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(ctx->z_cap_off);
+    (void)hipFree(ctx->z_dec_len);
+    (void)hipFree(ctx->z_status);
+    (void)hipFree(ctx->z_desc);
+    const size_t n = size_t(nblk) + 1;
+    OKV_HIP(hipMalloc(&ctx->z_cap_off, n * 8));
+    OKV_HIP(hipMalloc(&ctx->z_dec_len, n * 8));
+    OKV_HIP(hipMalloc(&ctx->z_status, n * 4));
+    OKV_HIP(hipMalloc(&ctx->z_desc, n * sizeof(Desc)));
+    ctx->z_cap_blocks = n;
+  }
+  launch_zstd_cap(ctx->stream, d_desc, nblk, ctx->z_cap_off);
+  uint64_t total = 0;
+  OKV_HIP(hipMemcpyAsync(&total, ctx->z_cap_off + nblk, 8, hipMemcpyDeviceToHost, ctx->stream));
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_dec), &ctx->z_cap_dec, total + 64)))
+    return rc;
+  const uint32_t grid = std::min<uint32_t>(nblk, 2048);
+  if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_lit), &ctx->z_cap_lit,
+                 size_t(grid) * kZstdLitBytes)))
+    return rc;
+  launch_zstd(ctx->stream, d_seg, seg_bytes, d_desc, nblk, ctx->z_cap_off, ctx->z_dec,
+              ctx->z_dec_len, ctx->z_status, ctx->z_lit, grid);
+  launch_zstd_desc(ctx->stream, d_desc, nblk, ctx->z_cap_off, ctx->z_dec_len, ctx->z_desc);
+  OKV_HIP(hipGetLastError());
+  // offsets <= total < seg_bytes, so no decompressed block reads as EOF
+  *w = Work{ctx->z_dec, total + 16, ctx->z_desc, OKV_COMP_NONE, ctx->z_status};
+  return OKV_OK;
+}
+
 // Launch passes 1 and 2 on device inputs.
-int launch_plan(okv_ctx* ctx, const uint8_t* d_seg, uint64_t seg_bytes, const Desc* d_desc,
-                uint32_t nblk, int comp, uint64_t* d_row_start, bool timed = false) {
+int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_start,
+                bool timed = false) {
   int rc = ensure_blocks(ctx, nblk);
   if (rc) return rc;
   const uint32_t ntiles = (nblk + kTile - 1) / kTile;
-  if (timed) prof_mark(ctx, 0);
   OKV_HIP(hipMemsetAsync(ctx->d_big + nblk, 0, sizeof(uint32_t), ctx->stream));
   if (ntiles)
-    hipLaunchKernelGGL(okv_count_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, d_seg,
-                       seg_bytes, d_desc, nblk, comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
-                       ctx->d_rec, ctx->d_big, ctx->d_big + nblk);
+    hipLaunchKernelGGL(okv_count_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, w.seg,
+                       w.seg_bytes, w.descs, nblk, w.comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
+                       ctx->d_rec, ctx->d_big, ctx->d_big + nblk, w.pre);
   if (timed) prof_mark(ctx, 1);
   hipLaunchKernelGGL(okv_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_tile_tot,
                      ntiles, ctx->d_tile_pre, ctx->d_tot, d_row_start, nblk);
@@ -859,14 +908,18 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   if (!aligned16(seg)) return set_err(ctx, OKV_E_ARG, "device seg must be 16-byte aligned");
   if (!index_only && (!aligned16(o->key_arena) || !aligned16(o->val_arena)))
     return set_err(ctx, OKV_E_ARG, "device arenas must be 16-byte aligned");
-  int rc = launch_plan(ctx, seg, seg_bytes, descs, nblk, comp, o->row_start, true);
+  prof_mark(ctx, 0);
+  Work w;
+  int rc = prepare(ctx, seg, seg_bytes, descs, nblk, comp, index_only, &w);
+  if (rc) return rc;
+  rc = launch_plan(ctx, w, nblk, o->row_start, true);
   if (rc) return rc;
   CopyParams P;
-  P.seg = seg;
-  P.seg_bytes = seg_bytes;
-  P.descs = descs;
+  P.seg = w.seg;
+  P.seg_bytes = w.seg_bytes;
+  P.descs = w.descs;
   P.nblk = nblk;
-  P.comp = comp;
+  P.comp = w.comp;
   P.index_only = index_only ? 1 : 0;
   P.rec_s = ctx->d_rec;
   P.big_list = ctx->d_big;
@@ -945,8 +998,10 @@ int decode_host(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv_
   rc = grow(ctx, &ctx->d_out, &ctx->cap_out, off_rows + 256);
   if (rc) return rc;
   uint8_t* base = static_cast<uint8_t*>(ctx->d_out);
-  rc = launch_plan(ctx, ctx->d_seg, seg_bytes, ctx->d_desc, nblk, comp,
-                   reinterpret_cast<uint64_t*>(base + off_rs));
+  Work w;
+  rc = prepare(ctx, ctx->d_seg, seg_bytes, ctx->d_desc, nblk, comp, index_only, &w);
+  if (rc) return rc;
+  rc = launch_plan(ctx, w, nblk, reinterpret_cast<uint64_t*>(base + off_rs));
   if (rc) return rc;
   Totals T;
   rc = read_totals(ctx, &T);
@@ -1054,6 +1109,12 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->d_desc);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_hash);
+  (void)hipFree(ctx->z_cap_off);
+  (void)hipFree(ctx->z_dec_len);
+  (void)hipFree(ctx->z_status);
+  (void)hipFree(ctx->z_desc);
+  (void)hipFree(ctx->z_dec);
+  (void)hipFree(ctx->z_lit);
   okv::enc_release(ctx);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -1092,7 +1153,11 @@ int okv_decode_plan(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes,
   } else if (!aligned16(seg)) {
     return set_err(ctx, OKV_E_ARG, "device seg must be 16-byte aligned");
   }
-  if ((rc = launch_plan(ctx, d_seg, seg_bytes, d_desc, nblk, compression, nullptr))) return rc;
+  Work w;
+  if ((rc = prepare(ctx, d_seg, seg_bytes, d_desc, nblk, compression,
+                    (flags & OKV_F_INDEX_ONLY) != 0, &w)))
+    return rc;
+  if ((rc = launch_plan(ctx, w, nblk, nullptr))) return rc;
   Totals T;
   if ((rc = read_totals(ctx, &T))) return rc;
   if (n_rows) *n_rows = T.rows;

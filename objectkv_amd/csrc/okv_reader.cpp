@@ -203,6 +203,7 @@ int read_block(okv_reader* r, const Entry& e, const std::vector<okv_row>** rows)
     case OKV_BLK_SHORT: return OKV_R_BLOCK_SHORT;
     case OKV_BLK_PANIC: return OKV_R_PANIC;
     case OKV_BLK_UNSUPPORTED: return OKV_R_UNSUPPORTED;
+    case OKV_BLK_ZSTD_ERROR: return OKV_R_ZSTD;
     default: return OKV_R_GPU;
   }
   if (!r->block_built[i]) {

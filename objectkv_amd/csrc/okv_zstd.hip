@@ -1,0 +1,867 @@
+// okv_zstd.hip -- zstd block decompression on the GPU (gfx950), for segments
+// whose meta compression byte is 1.
+//
+// The reference reads a zstd block as
+//   zstd.NewReader(bytes.NewReader(rawBlockBytes[:stat.CompressedSize])); io.Copy
+// (/root/reference/sst/segment_reader.go:320-330) with klauspost/compress
+// v1.17.9: every frame in the slice is decoded (RFC 8878), skippable frames are
+// skipped, content checksums and frame content sizes are verified, and any
+// failure is an error returned from ReadBlockWithStat.  This file restates that
+// decoding; the record walk then runs unchanged on the decompressed bytes.
+//
+// One wave (64 lanes) per segment block, persistent over the batch.  Entropy
+// decoding (FSE sequences, Huffman weights, headers) is sequential and runs
+// wave-uniform (every lane computes the same values: no broadcasts); Huffman
+// literal streams run one per lane (4 streams -> lanes 0..3); literal and match
+// copies run lane-parallel.  Output goes to a per-block scratch region in HBM;
+// a match whose source overlaps bytes written since the last commit point first
+// waits for this wave's stores (s_waitcnt vmcnt(0) + workgroup fence).
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "okv_ctx.hpp"
+#include "okv_kernels.hpp"
+#include "okv_sst.h"
+
+namespace okv {
+namespace zst {
+
+constexpr int kHufMaxBits = 11;          // Max_Number_of_Bits for literals (RFC 8878 4.2.1)
+constexpr uint32_t kBlockMax = 1u << 17;  // Block_Maximum_Size (128 KiB)
+constexpr int kLLMaxAL = 9, kMLMaxAL = 9, kOFMaxAL = 8;
+
+enum : int32_t { kOK = 0, kErr = 1, kCap = 2 };
+
+// Literals_Length and Match_Length baselines / extra bits (RFC 8878 3.1.1.3.2.1.1).
+__constant__ uint32_t LL_BASE[36] = {0,  1,  2,   3,   4,   5,    6,    7,    8,    9,     10,    11,
+                                     12, 13, 14,  15,  16,  18,   20,   22,   24,   28,    32,    40,
+                                     48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+__constant__ uint8_t LL_BITS[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  0,  0,  1,  1,
+                                    1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ uint32_t ML_BASE[53] = {3,  4,  5,  6,  7,  8,  9,  10,  11,  12,  13,   14,   15,   16,
+                                     17, 18, 19, 20, 21, 22, 23, 24,  25,  26,  27,   28,   29,   30,
+                                     31, 32, 33, 34, 35, 37, 39, 41,  43,  47,  51,   59,   67,   83,
+                                     99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
+__constant__ uint8_t ML_BITS[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                    0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1,
+                                    2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+// Predefined distributions (RFC 8878 3.1.1.3.2.2).
+__constant__ int16_t LL_DEF[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1,  1,  2,  2,
+                                   2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+__constant__ int16_t ML_DEF[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1,  1,  1,  1,  1,  1,  1,  1,
+                                   1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,  1,  1,  1,  1,  1,  1,  1,
+                                   1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+__constant__ int16_t OF_DEF[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1,  1,  1,  1,
+                                   1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+
+// FSE decoding table entry: symbol | nbBits << 8 | baseline << 16.
+__device__ __forceinline__ uint32_t fse_sym(uint32_t e) { return e & 0xff; }
+__device__ __forceinline__ uint32_t fse_nb(uint32_t e) { return (e >> 8) & 0xff; }
+__device__ __forceinline__ uint32_t fse_base(uint32_t e) { return e >> 16; }
+
+struct __align__(16) Smem {
+  uint32_t ll[1 << kLLMaxAL];
+  uint32_t ml[1 << kMLMaxAL];
+  uint32_t of[1 << kOFMaxAL];
+  uint32_t hw[1 << 6];         // FSE table of the Huffman weights (AL <= 6)
+  uint16_t huf[1 << kHufMaxBits];
+  uint16_t next[64];           // FSE build scratch (symbolNext)
+  int16_t norm[64];            // normalized counts
+  uint8_t wgt[256];            // Huffman weights
+  uint16_t hstart[256];        // first decoding-table entry of each symbol
+  uint32_t rank[kHufMaxBits + 2];
+};
+
+// ---- byte access -------------------------------------------------------------
+// Bytes [i, i+4) of p with every byte outside [0, n) read as 0; only aligned
+// dwords holding a byte of [0, n) are loaded.
+__device__ __forceinline__ uint32_t ld32z(const uint8_t* p, int64_t i, int64_t n) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p) + uintptr_t(i);
+  const uintptr_t base = reinterpret_cast<uintptr_t>(p);
+  const uintptr_t end = base + uintptr_t(n);
+  const uintptr_t w0 = a & ~uintptr_t(3), w1 = w0 + 4;
+  const uint32_t sh = uint32_t(a & 3);
+  uint32_t x = 0, y = 0;
+  if (int64_t(w0 + 4) > int64_t(base) && w0 < end) x = *reinterpret_cast<const uint32_t*>(w0);
+  if (sh && int64_t(w1 + 4) > int64_t(base) && w1 < end) y = *reinterpret_cast<const uint32_t*>(w1);
+  uint32_t v = sh ? __builtin_amdgcn_alignbyte(y, x, sh) : x;
+  // zero the bytes outside [0, n)
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (i + k < 0 || i + k >= n) v &= ~(0xffu << (8 * k));
+  return v;
+}
+__device__ __forceinline__ uint64_t ld64z(const uint8_t* p, int64_t i, int64_t n) {
+  return uint64_t(ld32z(p, i, n)) | (uint64_t(ld32z(p, i + 4, n)) << 32);
+}
+__device__ __forceinline__ uint32_t rd8(const uint8_t* p) { return *p; }
+
+// ---- backward bit reader (FSE / Huffman streams) --------------------------------
+// Stream bytes [0, n) of p; bit i of the stream = bit (i & 7) of byte i >> 3.
+// Reading consumes from the top: read(n) returns bits [pos - n, pos) and
+// lowers pos; bits below 0 read as 0 (the "overflow" tail of RFC 8878 4.2.1.2).
+struct BitR {
+  const uint8_t* p;
+  int64_t n;     // stream bytes
+  int64_t pos;   // remaining bits
+  int64_t lo;    // container holds bits [lo, lo + 64)
+  uint64_t c;
+};
+
+__device__ __forceinline__ bool bitr_init(BitR& b, const uint8_t* p, int64_t n) {
+  b.p = p;
+  b.n = n;
+  b.lo = INT64_MAX / 4;  // forces the first fill
+  b.c = 0;
+  b.pos = 0;
+  if (n <= 0) return false;
+  const uint32_t last = p[n - 1];
+  if (last == 0) return false;  // the final byte holds the end marker
+  b.pos = (n - 1) * 8 + (31 - __builtin_clz(last));
+  return true;
+}
+// Container = the 8 bytes ending at the byte boundary at or above bit `top`.
+__device__ __forceinline__ void bitr_fill(BitR& b, int64_t top) {
+  const int64_t top_byte = (top + 7) >> 3;  // floor division for negatives is fine here
+  const int64_t lo_byte = top_byte - 8;
+  b.lo = lo_byte * 8;
+  b.c = ld64z(b.p, lo_byte, b.n);
+}
+// Bits [pos - nb, pos) (nb <= 32), consumed.
+__device__ __forceinline__ uint32_t bitr_read(BitR& b, uint32_t nb) {
+  if (nb == 0) return 0;
+  b.pos -= nb;
+  if (b.pos < b.lo || b.pos + nb > b.lo + 64) bitr_fill(b, b.pos + nb);
+  return uint32_t((b.c >> (b.pos - b.lo)) & ((uint64_t(1) << nb) - 1));
+}
+// Bits [pos - nb, pos), not consumed.
+__device__ __forceinline__ uint32_t bitr_peek(BitR& b, uint32_t nb) {
+  const int64_t p0 = b.pos - nb;
+  if (p0 < b.lo || b.pos > b.lo + 64) bitr_fill(b, b.pos);
+  return uint32_t((b.c >> (p0 - b.lo)) & ((uint64_t(1) << nb) - 1));
+}
+__device__ __forceinline__ void bitr_skip(BitR& b, uint32_t nb) { b.pos -= nb; }
+
+// ---- FSE ---------------------------------------------------------------------
+// FSE_readNCount (RFC 8878 4.1.1): forward bitstream at p[0, n); fills norm[]
+// (max_sym + 1 entries), returns bytes consumed or -1.
+__device__ int32_t read_ncount(const uint8_t* p, int64_t n, int16_t* norm, uint32_t max_sym,
+                               uint32_t max_al, uint32_t& al_out, uint32_t& nsym_out) {
+  int64_t bit = 0;
+  auto peek = [&](uint32_t k) -> uint32_t {
+    const uint64_t v = ld64z(p, bit >> 3, n) >> (bit & 7);
+    return uint32_t(v & ((uint64_t(1) << k) - 1));
+  };
+  const uint32_t al = peek(4) + 5;
+  bit += 4;
+  if (al > max_al) return -1;
+  int32_t remaining = (1 << al) + 1;
+  int32_t threshold = 1 << al;
+  uint32_t nbits = al + 1;
+  uint32_t s = 0;
+  while (remaining > 1) {
+    if (s > max_sym) return -1;
+    const int32_t max = 2 * threshold - 1 - remaining;
+    int32_t count;
+    const uint32_t v = peek(nbits);
+    if (int32_t(v & uint32_t(threshold - 1)) < max) {
+      count = int32_t(v & uint32_t(threshold - 1));
+      bit += nbits - 1;
+    } else {
+      count = int32_t(v & uint32_t(2 * threshold - 1));
+      if (count >= threshold) count -= max;
+      bit += nbits;
+    }
+    count -= 1;  // probability; -1 = "less than 1"
+    remaining -= count < 0 ? -count : count;
+    norm[s++] = int16_t(count);
+    if (count == 0) {  // 2-bit repeat flags of zero probabilities
+      for (;;) {
+        const uint32_t r = peek(2);
+        bit += 2;
+        for (uint32_t k = 0; k < r; ++k) {
+          if (s > max_sym) return -1;
+          norm[s++] = 0;
+        }
+        if (r != 3) break;
+      }
+    }
+    while (remaining < threshold) {
+      --nbits;
+      threshold >>= 1;
+    }
+    if ((bit >> 3) > n) return -1;
+  }
+  if (remaining != 1) return -1;
+  al_out = al;
+  nsym_out = s;
+  return int32_t((bit + 7) >> 3);
+}
+
+// Build an FSE decoding table from normalized counts (RFC 8878 4.1.1).
+// Wave-uniform: every lane runs it, lane 0 writes.
+__device__ bool build_fse(uint32_t* table, const int16_t* norm, uint32_t nsym, uint32_t al,
+                          uint16_t* next) {
+  const uint32_t size = 1u << al;
+  const bool w = (threadIdx.x & 63) == 0;
+  int32_t high = int32_t(size) - 1;
+  for (uint32_t s = 0; s < nsym; ++s) {
+    if (norm[s] == -1) {
+      if (w) table[high] = s;
+      --high;
+      if (w) next[s] = 1;
+    } else {
+      if (w) next[s] = uint16_t(norm[s]);
+    }
+  }
+  __syncthreads();
+  const uint32_t step = (size >> 1) + (size >> 3) + 3, mask = size - 1;
+  uint32_t pos = 0;
+  for (uint32_t s = 0; s < nsym; ++s) {
+    for (int32_t i = 0; i < norm[s]; ++i) {
+      if (w) table[pos] = s;
+      do {
+        pos = (pos + step) & mask;
+      } while (int32_t(pos) > high);
+    }
+  }
+  if (pos != 0) return false;
+  __syncthreads();
+  // nbBits / baseline per state: lanes share the states (next[] updated in order by lane 0)
+  if (w) {
+    for (uint32_t u = 0; u < size; ++u) {
+      const uint32_t s = table[u] & 0xff;
+      const uint32_t x = next[s]++;
+      const uint32_t nb = al - (31 - __builtin_clz(x));
+      const uint32_t base = (x << nb) - size;
+      table[u] = s | (nb << 8) | (base << 16);
+    }
+  }
+  __syncthreads();
+  return true;
+}
+
+__device__ __forceinline__ void build_rle(uint32_t* table, uint32_t sym) {
+  if ((threadIdx.x & 63) == 0) table[0] = sym;  // AL 0: one state, no bits
+  __syncthreads();
+}
+
+// ---- Huffman -------------------------------------------------------------------
+// Huffman tree description (RFC 8878 4.2.1).  Returns bytes consumed or -1;
+// sets max_bits.
+__device__ int32_t read_huf_tree(Smem& sm, const uint8_t* p, int64_t n, uint32_t& max_bits) {
+  if (n < 1) return -1;
+  const uint32_t hb = p[0];
+  uint32_t nw;  // weights given explicitly (the last one is implied)
+  int32_t used;
+  const bool w0 = (threadIdx.x & 63) == 0;
+  if (hb >= 128) {  // direct 4-bit weights
+    nw = hb - 127;
+    used = 1 + int32_t((nw + 1) / 2);
+    if (used > n) return -1;
+    for (uint32_t i = 0; i < nw; ++i) {
+      const uint32_t byte = p[1 + i / 2];
+      const uint32_t v = (i & 1) ? (byte & 15) : (byte >> 4);
+      if (w0) sm.wgt[i] = uint8_t(v);
+    }
+  } else {  // FSE-compressed weights, two interleaved states
+    const int64_t csz = hb;
+    if (1 + csz > n) return -1;
+    uint32_t al, nsym;
+    const int32_t hlen = read_ncount(p + 1, csz, sm.norm, 15, 6, al, nsym);
+    if (hlen < 0) return -1;
+    if (!build_fse(sm.hw, sm.norm, nsym, al, sm.next)) return -1;
+    BitR br;
+    if (!bitr_init(br, p + 1 + hlen, csz - hlen)) return -1;
+    uint32_t s1 = bitr_read(br, al), s2 = bitr_read(br, al);
+    nw = 0;
+    for (;;) {
+      if (nw >= 255) return -1;
+      uint32_t e = sm.hw[s1];
+      if (w0) sm.wgt[nw] = uint8_t(fse_sym(e));
+      ++nw;
+      s1 = fse_base(e) + bitr_read(br, fse_nb(e));
+      if (br.pos < 0) {  // overflow: the other state's symbol ends the list
+        if (w0) sm.wgt[nw] = uint8_t(fse_sym(sm.hw[s2]));
+        ++nw;
+        break;
+      }
+      if (nw >= 255) return -1;
+      e = sm.hw[s2];
+      if (w0) sm.wgt[nw] = uint8_t(fse_sym(e));
+      ++nw;
+      s2 = fse_base(e) + bitr_read(br, fse_nb(e));
+      if (br.pos < 0) {
+        if (w0) sm.wgt[nw] = uint8_t(fse_sym(sm.hw[s1]));
+        ++nw;
+        break;
+      }
+    }
+    used = 1 + int32_t(csz);
+  }
+  __syncthreads();
+  // implied last weight: the weights' 2^(w-1) must sum to a power of two
+  uint32_t sum = 0;
+  for (uint32_t i = 0; i < nw; ++i) {
+    const uint32_t w = sm.wgt[i];
+    if (w > kHufMaxBits) return -1;
+    if (w) sum += 1u << (w - 1);
+  }
+  if (sum == 0) return -1;
+  const uint32_t mb = 32 - __builtin_clz(sum);  // highbit(sum) + 1
+  if (mb > kHufMaxBits) return -1;
+  const uint32_t left = (1u << mb) - sum;
+  if (left == 0 || (left & (left - 1))) return -1;
+  const uint32_t lastw = 31 - __builtin_clz(left) + 1;
+  if (w0) sm.wgt[nw] = uint8_t(lastw);
+  const uint32_t nsym = nw + 1;
+  __syncthreads();
+  // libzstd HUF_readStats: at least two weight-1 symbols, and an even count
+  {
+    uint32_t r1 = 0;
+    for (uint32_t i = 0; i < nsym; ++i) r1 += sm.wgt[i] == 1;
+    if (r1 < 2 || (r1 & 1)) return -1;
+  }
+  // decoding table: entries grouped by weight ascending, symbols ascending
+  // within a weight; symbol of weight w covers 2^(w-1) entries, nbBits = mb + 1 - w
+  if (w0) {
+    for (uint32_t w = 0; w <= kHufMaxBits + 1; ++w) sm.rank[w] = 0;
+    for (uint32_t i = 0; i < nsym; ++i) sm.rank[sm.wgt[i]]++;
+    uint32_t start = 0;
+    for (uint32_t w = 1; w <= mb; ++w) {
+      const uint32_t cnt = sm.rank[w];
+      sm.rank[w] = start;
+      start += cnt << (w - 1);
+    }
+    for (uint32_t i = 0; i < nsym; ++i) {
+      const uint32_t w = sm.wgt[i];
+      sm.hstart[i] = uint16_t(w ? sm.rank[w] : 0);
+      if (w) sm.rank[w] += 1u << (w - 1);
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  for (uint32_t i = 0; i < nsym; ++i) {
+    const uint32_t w = sm.wgt[i];
+    if (!w) continue;
+    const uint32_t len = 1u << (w - 1), st = sm.hstart[i];
+    const uint16_t ent = uint16_t(i | ((mb + 1 - w) << 8));
+    for (uint32_t k = lane; k < len; k += 64) sm.huf[st + k] = ent;
+  }
+  __syncthreads();
+  max_bits = mb;
+  return used;
+}
+
+// Decode one Huffman stream of `cnt` literals into out (this lane only).
+__device__ bool huf_stream(const Smem& sm, uint32_t mb, const uint8_t* p, int64_t n, uint8_t* out,
+                           uint32_t cnt) {
+  BitR br;
+  if (!bitr_init(br, p, n)) return cnt == 0 && n == 0;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const uint32_t idx = bitr_peek(br, mb);
+    const uint32_t e = sm.huf[idx];
+    out[i] = uint8_t(e & 0xff);
+    bitr_skip(br, e >> 8);
+  }
+  return br.pos == 0;
+}
+
+// ---- one zstd block -----------------------------------------------------------
+struct FrameState {
+  uint32_t rep0, rep1, rep2;  // repeat offsets (3.1.1.5)
+  bool huf_ok;       // a Huffman table is available for treeless literals
+  uint32_t huf_bits;
+  bool ll_ok, of_ok, ml_ok;  // tables available for Repeat mode
+  uint32_t ll_al, of_al, ml_al;
+};
+
+struct Out {
+  uint8_t* base;       // this segment block's decompressed region
+  uint64_t cap;
+  uint64_t pos;        // bytes written
+  uint64_t committed;  // bytes known visible to every lane
+  uint64_t frame0;     // first output byte of the current frame
+};
+
+__device__ __forceinline__ void commit(Out& o) {
+  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
+  __threadfence_block();
+  o.committed = o.pos;
+}
+
+// Lane-parallel byte copy of n bytes from src (global) to the output.
+__device__ __forceinline__ void out_copy(Out& o, const uint8_t* src, uint64_t n) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t j = lane; j < n; j += 64) o.base[o.pos + j] = src[j];
+  o.pos += n;
+}
+
+// Table for one of LL / OF / ML from the symbol compression mode.
+__device__ int32_t seq_table(Smem& sm, uint32_t* table, uint32_t mode, const int16_t* def,
+                             uint32_t def_al, uint32_t def_n, uint32_t max_sym, uint32_t max_al,
+                             const uint8_t* p, int64_t n, bool& ok, uint32_t& al) {
+  switch (mode) {
+    case 0: {  // Predefined_Mode
+      for (uint32_t s = 0; s < def_n; ++s) sm.norm[s] = def[s];
+      __syncthreads();
+      if (!build_fse(table, sm.norm, def_n, def_al, sm.next)) return -1;
+      ok = true;
+      al = def_al;
+      return 0;
+    }
+    case 1: {  // RLE_Mode
+      if (n < 1 || p[0] > max_sym) return -1;
+      build_rle(table, p[0]);
+      ok = true;
+      al = 0;
+      return 1;
+    }
+    case 2: {  // FSE_Compressed_Mode
+      uint32_t nsym;
+      const int32_t used = read_ncount(p, n, sm.norm, max_sym, max_al, al, nsym);
+      if (used < 0) return -1;
+      __syncthreads();
+      if (!build_fse(table, sm.norm, nsym, al, sm.next)) return -1;
+      ok = true;
+      return used;
+    }
+    default:  // Repeat_Mode
+      return ok ? 0 : -1;
+  }
+}
+
+// Decompress one compressed zstd block (RFC 8878 3.1.1.3) into the output.
+__device__ int32_t compressed_block(Smem& sm, FrameState& fs, Out& o, const uint8_t* p, int64_t n,
+                                    uint8_t* lit_buf) {
+  if (n < 1) return kErr;
+  // ---- literals section header (3.1.1.3.1.1)
+  const uint32_t b0 = p[0];
+  const uint32_t ltype = b0 & 3, sf = (b0 >> 2) & 3;
+  uint32_t regen = 0, csize = 0, hdr = 0, nstreams = 1;
+  if (ltype <= 1) {
+    if (sf == 0 || sf == 2) {
+      regen = b0 >> 3;
+      hdr = 1;
+    } else if (sf == 1) {
+      if (n < 2) return kErr;
+      regen = (b0 >> 4) + (uint32_t(p[1]) << 4);
+      hdr = 2;
+    } else {
+      if (n < 3) return kErr;
+      regen = (b0 >> 4) + (uint32_t(p[1]) << 4) + (uint32_t(p[2]) << 12);
+      hdr = 3;
+    }
+  } else {
+    if (sf <= 1) {
+      if (n < 3) return kErr;
+      const uint32_t h = b0 | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16);
+      regen = (h >> 4) & 0x3ff;
+      csize = (h >> 14) & 0x3ff;
+      hdr = 3;
+      nstreams = sf == 0 ? 1 : 4;
+    } else if (sf == 2) {
+      if (n < 4) return kErr;
+      const uint32_t h = b0 | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+      regen = (h >> 4) & 0x3fff;
+      csize = h >> 18;
+      hdr = 4;
+      nstreams = 4;
+    } else {
+      if (n < 5) return kErr;
+      const uint64_t h = uint64_t(b0) | (uint64_t(p[1]) << 8) | (uint64_t(p[2]) << 16) |
+                         (uint64_t(p[3]) << 24) | (uint64_t(p[4]) << 32);
+      regen = uint32_t((h >> 4) & 0x3ffff);
+      csize = uint32_t((h >> 22) & 0x3ffff);
+      hdr = 5;
+      nstreams = 4;
+    }
+  }
+  if (regen > kBlockMax) return kErr;
+  const uint8_t* lits = nullptr;  // literal source for the sequences
+  uint8_t rle_byte = 0;
+  bool rle = false;
+  int64_t at = hdr;
+  if (ltype == 0) {  // Raw_Literals_Block
+    if (at + regen > n) return kErr;
+    lits = p + at;
+    at += regen;
+  } else if (ltype == 1) {  // RLE_Literals_Block
+    if (at + 1 > n) return kErr;
+    rle_byte = p[at];
+    rle = true;
+    at += 1;
+  } else {  // Compressed / Treeless
+    if (at + csize > n) return kErr;
+    const uint8_t* q = p + at;
+    int64_t qn = csize;
+    if (ltype == 2) {
+      uint32_t mb;
+      const int32_t used = read_huf_tree(sm, q, qn, mb);
+      if (used < 0) return kErr;
+      fs.huf_ok = true;
+      fs.huf_bits = mb;
+      q += used;
+      qn -= used;
+    } else if (!fs.huf_ok) {
+      return kErr;
+    }
+    const int lane = threadIdx.x & 63;
+    bool good = true;
+    if (nstreams == 1) {
+      if (lane == 0) good = huf_stream(sm, fs.huf_bits, q, qn, lit_buf, regen);
+    } else {
+      if (qn < 6) return kErr;
+      const uint32_t s1 = q[0] | (uint32_t(q[1]) << 8), s2 = q[2] | (uint32_t(q[3]) << 8),
+                     s3 = q[4] | (uint32_t(q[5]) << 8);
+      const int64_t s4 = qn - 6 - int64_t(s1) - s2 - s3;
+      if (s4 < 0) return kErr;
+      const uint32_t seg = (regen + 3) / 4;
+      if (3 * seg > regen) return kErr;
+      if (lane < 4) {
+        const int64_t off = 6 + (lane > 0 ? s1 : 0) + (lane > 1 ? s2 : 0) + (lane > 2 ? s3 : 0);
+        const int64_t len = lane == 0 ? s1 : lane == 1 ? s2 : lane == 2 ? s3 : s4;
+        const uint32_t cnt = lane < 3 ? seg : regen - 3 * seg;
+        good = huf_stream(sm, fs.huf_bits, q + off, len, lit_buf + lane * seg, cnt);
+      }
+    }
+    // every lane must agree the streams decoded cleanly
+    if (__any(!good)) return kErr;
+    __builtin_amdgcn_s_waitcnt(0);
+    __threadfence_block();
+    lits = lit_buf;
+    at += csize;
+  }
+  // ---- sequences section (3.1.1.3.2)
+  if (at >= n) return kErr;
+  uint32_t nseq = p[at];
+  if (nseq < 128) {
+    at += 1;
+  } else if (nseq < 255) {
+    if (at + 2 > n) return kErr;
+    nseq = ((nseq - 128) << 8) + p[at + 1];
+    at += 2;
+  } else {
+    if (at + 3 > n) return kErr;
+    nseq = p[at + 1] + (uint32_t(p[at + 2]) << 8) + 0x7f00;
+    at += 3;
+  }
+  uint64_t lit_left = regen;
+  uint64_t lit_pos = 0;
+  auto emit_lits = [&](uint64_t ll) -> bool {
+    if (ll > lit_left) return false;
+    if (o.pos + ll > o.cap) return false;
+    if (rle) {
+      const int lane = threadIdx.x & 63;
+      for (uint64_t j = lane; j < ll; j += 64) o.base[o.pos + j] = rle_byte;
+      o.pos += ll;
+    } else {
+      out_copy(o, lits + lit_pos, ll);
+    }
+    lit_pos += ll;
+    lit_left -= ll;
+    return true;
+  };
+  if (nseq == 0) {  // literals only (bytes after the header are not read, as libzstd)
+    if (o.pos + lit_left > o.cap) return kCap;
+    emit_lits(lit_left);
+    return kOK;
+  }
+  if (at >= n) return kErr;
+  const uint32_t modes = p[at++];
+  if (modes & 3) return kErr;  // reserved bits
+  int32_t used;
+  used = seq_table(sm, sm.ll, modes >> 6, LL_DEF, 6, 36, 35, kLLMaxAL, p + at, n - at, fs.ll_ok,
+                   fs.ll_al);
+  if (used < 0) return kErr;
+  at += used;
+  used = seq_table(sm, sm.of, (modes >> 4) & 3, OF_DEF, 5, 29, 31, kOFMaxAL, p + at, n - at,
+                   fs.of_ok, fs.of_al);
+  if (used < 0) return kErr;
+  at += used;
+  used = seq_table(sm, sm.ml, (modes >> 2) & 3, ML_DEF, 6, 53, 52, kMLMaxAL, p + at, n - at,
+                   fs.ml_ok, fs.ml_al);
+  if (used < 0) return kErr;
+  at += used;
+  BitR br;
+  if (!bitr_init(br, p + at, n - at)) return kErr;
+  uint32_t sll = bitr_read(br, fs.ll_al);
+  uint32_t sof = bitr_read(br, fs.of_al);
+  uint32_t sml = bitr_read(br, fs.ml_al);
+  const int lane = threadIdx.x & 63;
+  for (uint32_t i = 0; i < nseq; ++i) {
+    if (br.pos < 0) return kErr;  // libzstd: the stream overflowed before this sequence
+    const uint32_t ell = sm.ll[sll], eof = sm.of[sof], eml = sm.ml[sml];
+    const uint32_t llc = fse_sym(ell), ofc = fse_sym(eof), mlc = fse_sym(eml);
+    if (llc > 35 || mlc > 52 || ofc > 31) return kErr;
+    // extra bits: offset, then match length, then literals length
+    uint64_t ofv = (uint64_t(1) << ofc) + bitr_read(br, ofc);
+    const uint32_t ml = ML_BASE[mlc] + bitr_read(br, ML_BITS[mlc]);
+    const uint32_t ll = LL_BASE[llc] + bitr_read(br, LL_BITS[llc]);
+    // repeat offsets (3.1.1.5), as libzstd's ZSTD_decodeSequence
+    uint64_t off;
+    if (ofv > 3) {
+      off = ofv - 3;
+      fs.rep2 = fs.rep1;
+      fs.rep1 = fs.rep0;
+      fs.rep0 = uint32_t(off);
+    } else {
+      const uint32_t idx = uint32_t(ofv) - 1 + (ll == 0 ? 1 : 0);  // 0..3
+      if (idx == 0) {
+        off = fs.rep0;
+      } else {
+        uint64_t t = idx == 3 ? uint64_t(fs.rep0) - 1 : (idx == 1 ? fs.rep1 : fs.rep2);
+        t += t == 0;  // libzstd: offset 0 is corrupt input, forced to 1
+        if (idx != 1) fs.rep2 = fs.rep1;
+        fs.rep1 = fs.rep0;
+        fs.rep0 = uint32_t(t);
+        off = t;
+      }
+    }
+    if (i + 1 < nseq) {  // state updates: literals length, match length, offset
+      sll = fse_base(ell) + bitr_read(br, fse_nb(ell));
+      sml = fse_base(eml) + bitr_read(br, fse_nb(eml));
+      sof = fse_base(eof) + bitr_read(br, fse_nb(eof));
+    }
+    // execute (3.1.1.4): literals, then the match
+    if (!emit_lits(ll)) return (o.pos + ll > o.cap) ? kCap : kErr;
+    if (off > o.pos - o.frame0) return kErr;  // before the frame start (no dictionary)
+    if (o.pos + ml > o.cap) return kCap;
+    const uint64_t q = o.pos - off;
+    if (q + (ml < off ? ml : off) > o.committed) commit(o);
+    for (uint64_t j = lane; j < ml; j += 64) o.base[o.pos + j] = o.base[q + (j % off)];
+    o.pos += ml;
+  }
+  if (br.pos > 0) return kErr;  // unread bits: corrupt (an over-read on the last one passes)
+  if (o.pos + lit_left > o.cap) return kCap;
+  emit_lits(lit_left);
+  return kOK;
+}
+
+// XXH64 of out[a, b) by lanes 0..3 (the four accumulators), result on every lane.
+__device__ uint64_t xxh64_out(const uint8_t* base, uint64_t len) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t q = lane & 3;
+  uint64_t acc = (q == 0) ? XP1 + XP2 : (q == 1) ? XP2 : (q == 2) ? 0 : 0 - XP1;
+  const uint64_t nstripe = len / 32;
+  if (lane < 4)
+    for (uint64_t s = 0; s < nstripe; ++s) acc = xround(acc, ld64u(base + s * 32 + q * 8));
+  const uint64_t a1 = __shfl(acc, 1, 64), a2 = __shfl(acc, 2, 64), a3 = __shfl(acc, 3, 64);
+  const uint64_t a0 = __shfl(acc, 0, 64);
+  uint64_t h;
+  if (len >= 32) {
+    h = rotl64(a0, 1) + rotl64(a1, 7) + rotl64(a2, 12) + rotl64(a3, 18);
+    h = (h ^ xround(0, a0)) * XP1 + XP4;
+    h = (h ^ xround(0, a1)) * XP1 + XP4;
+    h = (h ^ xround(0, a2)) * XP1 + XP4;
+    h = (h ^ xround(0, a3)) * XP1 + XP4;
+  } else {
+    h = XP5;
+  }
+  h += len;
+  uint64_t t = nstripe * 32;
+  for (; t + 8 <= len; t += 8) {
+    h ^= xround(0, ld64u(base + t));
+    h = rotl64(h, 27) * XP1 + XP4;
+  }
+  if (t + 4 <= len) {
+    const uint32_t v = uint32_t(base[t]) | (uint32_t(base[t + 1]) << 8) |
+                       (uint32_t(base[t + 2]) << 16) | (uint32_t(base[t + 3]) << 24);
+    h ^= uint64_t(v) * XP1;
+    h = rotl64(h, 23) * XP2 + XP3;
+    t += 4;
+  }
+  for (; t < len; ++t) {
+    h ^= uint64_t(base[t]) * XP5;
+    h = rotl64(h, 11) * XP1;
+  }
+  h ^= h >> 33;
+  h *= XP2;
+  h ^= h >> 29;
+  h *= XP3;
+  h ^= h >> 32;
+  return h;
+}
+
+// Every frame of src[0, n) (zstd.NewReader + io.Copy semantics).
+__device__ int32_t decode_frames(Smem& sm, const uint8_t* src, int64_t n, Out& o,
+                                 uint8_t* lit_buf) {
+  int64_t at = 0;
+  while (at < n) {
+    if (n - at < 4) return kErr;
+    const uint32_t magic = ld32z(src, at, n);
+    if ((magic & 0xfffffff0u) == 0x184d2a50u) {  // skippable frame (3.1.2)
+      if (n - at < 8) return kErr;
+      const uint64_t sz = ld32z(src, at + 4, n);
+      if (uint64_t(n - at - 8) < sz) return kErr;
+      at += 8 + int64_t(sz);
+      continue;
+    }
+    if (magic != 0xfd2fb528u) return kErr;
+    at += 4;
+    if (at >= n) return kErr;
+    const uint32_t fhd = src[at++];
+    const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, reserved = (fhd >> 3) & 1;
+    const uint32_t has_csum = (fhd >> 2) & 1, did_flag = fhd & 3;
+    if (reserved) return kErr;
+    if (!single) {
+      if (at >= n) return kErr;
+      at += 1;  // Window_Descriptor
+    }
+    const uint32_t did_size = did_flag == 0 ? 0 : did_flag == 1 ? 1 : did_flag == 2 ? 2 : 4;
+    if (at + did_size > n) return kErr;
+    uint32_t did = 0;
+    for (uint32_t k = 0; k < did_size; ++k) did |= uint32_t(src[at + k]) << (8 * k);
+    at += did_size;
+    if (did != 0) return kErr;  // no dictionaries are registered with the reader
+    const uint32_t fcs_size = fcs_flag == 0 ? (single ? 1 : 0) : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8;
+    if (at + fcs_size > n) return kErr;
+    uint64_t fcs = 0;
+    for (uint32_t k = 0; k < fcs_size; ++k) fcs |= uint64_t(src[at + k]) << (8 * k);
+    if (fcs_size == 2) fcs += 256;
+    at += fcs_size;
+    FrameState fs;
+    fs.rep0 = 1;
+    fs.rep1 = 4;
+    fs.rep2 = 8;
+    fs.huf_ok = fs.ll_ok = fs.of_ok = fs.ml_ok = false;
+    fs.huf_bits = 0;
+    fs.ll_al = fs.of_al = fs.ml_al = 0;
+    o.frame0 = o.pos;
+    for (;;) {  // blocks (3.1.1.2)
+      if (n - at < 3) return kErr;
+      const uint32_t bh = src[at] | (uint32_t(src[at + 1]) << 8) | (uint32_t(src[at + 2]) << 16);
+      at += 3;
+      const uint32_t last = bh & 1, btype = (bh >> 1) & 3, bsize = bh >> 3;
+      if (btype == 0) {  // Raw_Block
+        if (int64_t(bsize) > n - at) return kErr;
+        if (o.pos + bsize > o.cap) return kCap;
+        out_copy(o, src + at, bsize);
+        at += bsize;
+      } else if (btype == 1) {  // RLE_Block
+        if (at >= n) return kErr;
+        if (o.pos + bsize > o.cap) return kCap;
+        const uint8_t v = src[at];
+        const int lane = threadIdx.x & 63;
+        for (uint64_t j = lane; j < bsize; j += 64) o.base[o.pos + j] = v;
+        o.pos += bsize;
+        at += 1;
+      } else if (btype == 2) {  // Compressed_Block (libzstd: < 128 KiB)
+        if (int64_t(bsize) > n - at || bsize >= kBlockMax) return kErr;
+        const int32_t r = compressed_block(sm, fs, o, src + at, bsize, lit_buf);
+        if (r != kOK) return r;
+        at += bsize;
+      } else {
+        return kErr;  // reserved block type
+      }
+      if (last) break;
+    }
+    if (fcs_size && o.pos - o.frame0 != fcs) return kErr;  // Frame_Content_Size check
+    if (has_csum) {
+      if (n - at < 4) return kErr;
+      commit(o);
+      const uint32_t want = ld32z(src, at, n);
+      const uint64_t h = xxh64_out(o.base + o.frame0, o.pos - o.frame0);
+      if (uint32_t(h) != want) return kErr;
+      at += 4;
+    }
+  }
+  return kOK;
+}
+
+}  // namespace zst
+
+// One wave per segment block, persistent over the batch.  Inputs: the raw
+// descriptors; outputs: decompressed bytes at dec + cap_off[b], their length,
+// and a per-block status (OKV_BLK_*).  lit = per-wave literal scratch.
+__global__ __launch_bounds__(64) void okv_zstd_kernel(const uint8_t* __restrict__ seg,
+                                                      uint64_t seg_bytes, const Desc* __restrict__ descs,
+                                                      uint32_t nblk, const uint64_t* __restrict__ cap_off,
+                                                      uint8_t* __restrict__ dec, uint64_t* __restrict__ dec_len,
+                                                      int32_t* __restrict__ zstatus,
+                                                      uint8_t* __restrict__ lit) {
+  __shared__ zst::Smem sm;
+  uint8_t* lit_buf = lit + uint64_t(blockIdx.x) * zst::kBlockMax;
+  for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const Desc d = descs[b];
+    int32_t st = OKV_BLK_OK;
+    zst::Out o;
+    o.base = dec + cap_off[b];
+    o.cap = cap_off[b + 1] - cap_off[b];
+    o.pos = o.committed = o.frame0 = 0;
+    if (int64_t(d.offset) < 0 || d.offset >= seg_bytes) {
+      st = OKV_BLK_EOF;  // :303-313
+    } else if (seg_bytes - d.offset < d.block_size) {
+      st = OKV_BLK_SHORT;  // :314-316
+    } else if (d.compressed_size > d.block_size) {
+      st = OKV_BLK_PANIC;  // rawBlockBytes[:CompressedSize] out of range (:321)
+    } else {
+      const int32_t r = zst::decode_frames(sm, seg + d.offset, int64_t(d.compressed_size), o, lit_buf);
+      st = r == zst::kOK ? OKV_BLK_OK : r == zst::kCap ? OKV_BLK_CAPACITY : OKV_BLK_ZSTD_ERROR;
+    }
+    if ((threadIdx.x & 63) == 0) {
+      zstatus[b] = st;
+      dec_len[b] = st == OKV_BLK_OK ? o.pos : 0;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+  }
+}
+
+// Exclusive scan of per-block decompressed capacities (round16(OriginalSize)).
+__global__ __launch_bounds__(1024) void okv_zstd_cap_kernel(const Desc* __restrict__ descs,
+                                                            uint32_t nblk,
+                                                            uint64_t* __restrict__ cap_off) {
+  __shared__ uint64_t sm[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint64_t v = i < nblk ? round16(descs[i].original_size) : 0;
+    const uint64_t inc = wave_incl_scan(v, lane);
+    if (lane == 63) sm[wave] = inc;
+    __syncthreads();
+    uint64_t before = 0, tot = 0;
+    for (int w = 0; w < 16; ++w) {
+      before += w < wave ? sm[w] : 0;
+      tot += sm[w];
+    }
+    if (i < nblk) cap_off[i] = carry + before + inc - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) cap_off[nblk] = carry;
+}
+
+// Descriptors of the decompressed blocks for the record walk (passes 1-3):
+// offset into the scratch, BlockSize = decompressed length.
+__global__ void okv_zstd_desc_kernel(const Desc* __restrict__ descs, uint32_t nblk,
+                                     const uint64_t* __restrict__ cap_off,
+                                     const uint64_t* __restrict__ dec_len,
+                                     Desc* __restrict__ out) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblk) return;
+  Desc d;
+  d.offset = cap_off[b];
+  d.block_size = dec_len[b];
+  d.original_size = descs[b].original_size;
+  d.compressed_size = 0;
+  out[b] = d;
+}
+
+void launch_zstd(hipStream_t s, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
+                 uint32_t nblk, const uint64_t* cap_off, uint8_t* dec, uint64_t* dec_len,
+                 int32_t* zstatus, uint8_t* lit, uint32_t grid) {
+  hipLaunchKernelGGL(okv_zstd_kernel, dim3(grid), dim3(64), 0, s, seg, seg_bytes, descs, nblk,
+                     cap_off, dec, dec_len, zstatus, lit);
+}
+void launch_zstd_cap(hipStream_t s, const Desc* descs, uint32_t nblk, uint64_t* cap_off) {
+  hipLaunchKernelGGL(okv_zstd_cap_kernel, dim3(1), dim3(1024), 0, s, descs, nblk, cap_off);
+}
+void launch_zstd_desc(hipStream_t s, const Desc* descs, uint32_t nblk, const uint64_t* cap_off,
+                      const uint64_t* dec_len, Desc* out) {
+  hipLaunchKernelGGL(okv_zstd_desc_kernel, dim3((nblk + 255) / 256), dim3(256), 0, s, descs, nblk,
+                     cap_off, dec_len, out);
+}
+
+}  // namespace okv

@@ -190,6 +190,9 @@ def decode_soa(seg, descs: np.ndarray, compression=0, index_only=False):
                           _ptr(o["key_off"]), _ptr(o["key_len"]), _ptr(o["val_off"]),
                           _ptr(o["val_len"]), _ptr(o["key_arena"]), _ptr(o["val_arena"]),
                           _ptr(o["status"]))
+    rows_out = int(out["row_start"][-1])  # index-only zstd blocks yield no rows
+    for k in ("key_off", "key_len", "val_off", "val_len"):
+        out[k] = out[k][:rows_out]
     return out
 
 

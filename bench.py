@@ -39,6 +39,9 @@ CONFIGS = {
     "c2": (0, 1, 256, 3584, 4096, "C2: 256 x 4 KiB blocks, fixed 16 B key / 64 B value"),
     "c5": (1, 3, 16384, 57344, 65536,
            "C5: 1 GiB segment per GPU (16384 x 64 KiB C3-style blocks)"),
+    # zstd: 1 GiB of text-like rows in 64 KiB blocks, one libzstd level-3 frame per block
+    "cz": ("zstd", 5, 16384, 57344, 65536,
+           "CZ: 16384 x 64 KiB-raw blocks, zstd level 3 frames (text-like values 0-4096 B)"),
     # encode: total rows (split across ranks by key range), key/value bytes
     "c4": ("encode", 1, 100_000_000, 3584, 4096,
            "C4: encode 100 M sorted pairs (16 B key / 64 B value) into 4 KiB blocks + "
@@ -104,9 +107,17 @@ def main():
     kind, seed0, nblk, th, bs, desc = CONFIGS[args.config]
     seed = seed0 + rank
     t0 = time.time()
-    w = okv.synth_segment(kind, seed, nblocks=nblk, threshold=th, block_size=bs)
-    seg = w.data_view()
-    descs = w.descs()[:nblk]
+    comp = 0
+    if kind == "zstd":
+        from tools.zstd_gen import text_zstd_segment
+        seg, descs, _ = text_zstd_segment(nblk, seed, 3, th, bs)
+        comp = okv.sst.COMP_ZSTD
+        if args.mode == "index":
+            raise SystemExit("index-only decode does not apply to zstd blocks")
+    else:
+        w = okv.synth_segment(kind, seed, nblocks=nblk, threshold=th, block_size=bs)
+        seg = w.data_view()
+        descs = w.descs()[:nblk]
     log(f"[rank {rank}] generated {seg.nbytes / 2**30:.2f} GiB segment "
         f"({nblk} blocks) in {time.time() - t0:.1f}s")
     in_bytes = int(descs[:, 1].sum())  # sum BlockSize (headline GiB/s numerator)
@@ -119,7 +130,8 @@ def main():
     seg_t[:seg.nbytes].copy_(torch.from_numpy(seg))
     d_t = torch.from_numpy(descs.view(np.int64).copy()).to(dev)
     index_only = args.mode == "index"
-    rows, kb, vb = dec.plan_device(seg_t, seg.nbytes, d_t, nblk, index_only=index_only)
+    rows, kb, vb = dec.plan_device(seg_t, seg.nbytes, d_t, nblk, compression=comp,
+                                   index_only=index_only)
     out = dict(row_start=torch.empty(nblk + 1, dtype=torch.int64, device=dev),
                key_base=torch.empty(nblk, dtype=torch.int64, device=dev),
                val_base=torch.empty(nblk, dtype=torch.int64, device=dev),
@@ -133,8 +145,8 @@ def main():
     payload = int(kb + vb)  # padded arena bytes written
 
     def step(sync=False):
-        return dec.decode_device(seg_t, seg.nbytes, d_t, nblk, out, index_only=index_only,
-                                 sync=sync)
+        return dec.decode_device(seg_t, seg.nbytes, d_t, nblk, out, compression=comp,
+                                 index_only=index_only, sync=sync)
 
     # correctness guard on the bench path itself (totals + statuses)
     o = step(sync=True)
@@ -192,13 +204,13 @@ def main():
         res = {}
         for nth in (1, threads):
             # bounded sample: whole passes over the first blocks until the budget is spent
-            sample = nblk if args.config != "c3" else 4096 * nth
+            sample = nblk if args.config not in ("c3", "cz") else 4096 * nth
             sample = min(sample, nblk)
             n_pass, t_cpu, nrows_cpu = 0, 0.0, 0
             budget = args.cpu_seconds / 2
             while t_cpu < budget:
                 t1 = time.perf_counter()
-                r_, _pay = coracle.decode_go(seg, cd[:sample], 0, nth)
+                r_, _pay = coracle.decode_go(seg, cd[:sample], comp, nth)
                 t_cpu += time.perf_counter() - t1
                 n_pass += 1
                 nrows_cpu += r_
@@ -220,7 +232,7 @@ def main():
         t1 = time.perf_counter()
         n_e2e = 3
         for _ in range(n_e2e):
-            got = dec.decode(seg, descs, index_only=index_only)
+            got = dec.decode(seg, descs, compression=comp, index_only=index_only)
         t_e2e = (time.perf_counter() - t1) / n_e2e
         e2e = {"GiB_s": round(in_bytes / t_e2e / 2**30, 3), "ms": round(t_e2e * 1e3, 2),
                "note": "pageable host buffers, H2D + plan + decode + D2H, synchronous"}

@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <cstdio>
+#include <cstdlib>
 
 #include "okv_ctx.hpp"
 #include "okv_kernels.hpp"
@@ -30,6 +32,8 @@ namespace zst {
 constexpr int kHufMaxBits = 11;          // Max_Number_of_Bits for literals (RFC 8878 4.2.1)
 constexpr uint32_t kBlockMax = 1u << 17;  // Block_Maximum_Size (128 KiB)
 constexpr int kLLMaxAL = 9, kMLMaxAL = 9, kOFMaxAL = 8;
+constexpr uint32_t kSeqChunk = 256;      // sequences decoded before a parallel execution pass
+constexpr uint32_t kChunkOut = 4096;     // output bytes per chunk covered by the byte map
 
 enum : int32_t { kOK = 0, kErr = 1, kCap = 2 };
 
@@ -61,9 +65,12 @@ __device__ __forceinline__ uint32_t fse_nb(uint32_t e) { return (e >> 8) & 0xff;
 __device__ __forceinline__ uint32_t fse_base(uint32_t e) { return e >> 16; }
 
 struct __align__(16) Smem {
-  uint32_t ll[1 << kLLMaxAL];
+  uint32_t ll[1 << kLLMaxAL];   // FSE states (symbol | nbBits | nextState baseline)
   uint32_t ml[1 << kMLMaxAL];
   uint32_t of[1 << kOFMaxAL];
+  uint32_t llv[1 << kLLMaxAL];  // per state: baseValue << 5 | extra bits (libzstd's seqSymbol)
+  uint32_t mlv[1 << kMLMaxAL];
+  uint32_t ofv[1 << kOFMaxAL];
   uint32_t hw[1 << 6];         // FSE table of the Huffman weights (AL <= 6)
   uint16_t huf[1 << kHufMaxBits];
   uint16_t next[64];           // FSE build scratch (symbolNext)
@@ -71,6 +78,12 @@ struct __align__(16) Smem {
   uint8_t wgt[256];            // Huffman weights
   uint16_t hstart[256];        // first decoding-table entry of each symbol
   uint32_t rank[kHufMaxBits + 2];
+  // one chunk of decoded sequences (phase A) for parallel execution (phase B)
+  uint32_t s_ll[kSeqChunk], s_ml[kSeqChunk], s_off[kSeqChunk];
+  uint32_t s_lpre[kSeqChunk + 1];  // exclusive prefix of literal lengths
+  uint32_t s_opre[kSeqChunk + 1];  // exclusive prefix of ll + ml (output offsets)
+  uint32_t s_mpre[kSeqChunk + 1];  // exclusive prefix of match lengths
+  uint8_t s_map[kChunkOut];        // chunk output byte -> its sequence (low 8 bits)
 };
 
 // ---- byte access -------------------------------------------------------------
@@ -96,6 +109,13 @@ __device__ __forceinline__ uint64_t ld64z(const uint8_t* p, int64_t i, int64_t n
   return uint64_t(ld32z(p, i, n)) | (uint64_t(ld32z(p, i + 4, n)) << 32);
 }
 __device__ __forceinline__ uint32_t rd8(const uint8_t* p) { return *p; }
+
+// Wave-uniform values into scalar registers: the sequential decode then runs
+// on the SALU instead of 4-cycle wave64 VALU instructions.
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
+  return uint64_t(rfl(uint32_t(x))) | (uint64_t(rfl(uint32_t(x >> 32))) << 32);
+}
 
 // ---- backward bit reader (FSE / Huffman streams) --------------------------------
 // Stream bytes [0, n) of p; bit i of the stream = bit (i & 7) of byte i >> 3.
@@ -133,6 +153,18 @@ __device__ __forceinline__ uint32_t bitr_read(BitR& b, uint32_t nb) {
   if (nb == 0) return 0;
   b.pos -= nb;
   if (b.pos < b.lo || b.pos + nb > b.lo + 64) bitr_fill(b, b.pos + nb);
+  return uint32_t((b.c >> (b.pos - b.lo)) & ((uint64_t(1) << nb) - 1));
+}
+// Wave-uniform variant (sequence streams): container and positions in SGPRs.
+__device__ __forceinline__ uint32_t bitr_read_u(BitR& b, uint32_t nb) {
+  if (nb == 0) return 0;
+  b.pos -= nb;
+  if (b.pos < b.lo || b.pos + nb > b.lo + 64) {
+    const int64_t top_byte = (b.pos + nb + 7) >> 3;
+    const int64_t lo_byte = top_byte - 8;
+    b.lo = lo_byte * 8;
+    b.c = rfl64(ld64z(b.p, lo_byte, b.n));
+  }
   return uint32_t((b.c >> (b.pos - b.lo)) & ((uint64_t(1) << nb) - 1));
 }
 // Bits [pos - nb, pos), not consumed.
@@ -378,6 +410,7 @@ struct FrameState {
 };
 
 struct Out {
+  unsigned long long* prof;  // diagnostic phase counters (OKV_ZSTD_PROF), or null
   uint8_t* base;       // this segment block's decompressed region
   uint64_t cap;
   uint64_t pos;        // bytes written
@@ -385,7 +418,12 @@ struct Out {
   uint64_t frame0;     // first output byte of the current frame
 };
 
+__device__ __forceinline__ void prof_add(const Out& o, int k, unsigned long long v) {
+  if (o.prof && (threadIdx.x & 63) == 0) atomicAdd(o.prof + k, v);
+}
+
 __device__ __forceinline__ void commit(Out& o) {
+  prof_add(o, 5, 1);
   __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
   __threadfence_block();
   o.committed = o.pos;
@@ -396,6 +434,28 @@ __device__ __forceinline__ void out_copy(Out& o, const uint8_t* src, uint64_t n)
   const int lane = threadIdx.x & 63;
   for (uint64_t j = lane; j < n; j += 64) o.base[o.pos + j] = src[j];
   o.pos += n;
+}
+
+// Per-state (baseValue, extra bits) for one sequence table, so the decode loop
+// reads one LDS word per state instead of constant-memory lookups.  kind: 0 LL, 1 OF, 2 ML.
+__device__ void seq_values(const uint32_t* table, uint32_t* vals, uint32_t al, int kind) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t u = lane; u < (1u << al); u += 64) {
+    const uint32_t c = fse_sym(table[u]);
+    uint32_t base, bits;
+    if (kind == 0) {
+      base = LL_BASE[c < 36 ? c : 0];
+      bits = LL_BITS[c < 36 ? c : 0];
+    } else if (kind == 1) {
+      base = c < 32 ? (1u << c) : 0;
+      bits = c;
+    } else {
+      base = ML_BASE[c < 53 ? c : 0];
+      bits = ML_BITS[c < 53 ? c : 0];
+    }
+    vals[u] = (base << 5) | bits;
+  }
+  __syncthreads();
 }
 
 // Table for one of LL / OF / ML from the symbol compression mode.
@@ -436,6 +496,7 @@ __device__ int32_t seq_table(Smem& sm, uint32_t* table, uint32_t mode, const int
 __device__ int32_t compressed_block(Smem& sm, FrameState& fs, Out& o, const uint8_t* p, int64_t n,
                                     uint8_t* lit_buf) {
   if (n < 1) return kErr;
+  const long long t0 = o.prof ? clock64() : 0;
   // ---- literals section header (3.1.1.3.1.1)
   const uint32_t b0 = p[0];
   const uint32_t ltype = b0 & 3, sf = (b0 >> 2) & 3;
@@ -533,6 +594,8 @@ __device__ int32_t compressed_block(Smem& sm, FrameState& fs, Out& o, const uint
     lits = lit_buf;
     at += csize;
   }
+  const long long t1 = o.prof ? clock64() : 0;
+  prof_add(o, 0, t1 - t0);
   // ---- sequences section (3.1.1.3.2)
   if (at >= n) return kErr;
   uint32_t nseq = p[at];
@@ -576,64 +639,171 @@ __device__ int32_t compressed_block(Smem& sm, FrameState& fs, Out& o, const uint
                    fs.ll_al);
   if (used < 0) return kErr;
   at += used;
+  if ((modes >> 6) != 3) seq_values(sm.ll, sm.llv, fs.ll_al, 0);
   used = seq_table(sm, sm.of, (modes >> 4) & 3, OF_DEF, 5, 29, 31, kOFMaxAL, p + at, n - at,
                    fs.of_ok, fs.of_al);
   if (used < 0) return kErr;
   at += used;
+  if (((modes >> 4) & 3) != 3) seq_values(sm.of, sm.ofv, fs.of_al, 1);
   used = seq_table(sm, sm.ml, (modes >> 2) & 3, ML_DEF, 6, 53, 52, kMLMaxAL, p + at, n - at,
                    fs.ml_ok, fs.ml_al);
   if (used < 0) return kErr;
   at += used;
+  if (((modes >> 2) & 3) != 3) seq_values(sm.ml, sm.mlv, fs.ml_al, 2);
   BitR br;
   if (!bitr_init(br, p + at, n - at)) return kErr;
-  uint32_t sll = bitr_read(br, fs.ll_al);
-  uint32_t sof = bitr_read(br, fs.of_al);
-  uint32_t sml = bitr_read(br, fs.ml_al);
+  uint32_t sll = bitr_read_u(br, fs.ll_al);
+  uint32_t sof = bitr_read_u(br, fs.of_al);
+  uint32_t sml = bitr_read_u(br, fs.ml_al);
   const int lane = threadIdx.x & 63;
-  for (uint32_t i = 0; i < nseq; ++i) {
-    if (br.pos < 0) return kErr;  // libzstd: the stream overflowed before this sequence
-    const uint32_t ell = sm.ll[sll], eof = sm.of[sof], eml = sm.ml[sml];
-    const uint32_t llc = fse_sym(ell), ofc = fse_sym(eof), mlc = fse_sym(eml);
-    if (llc > 35 || mlc > 52 || ofc > 31) return kErr;
-    // extra bits: offset, then match length, then literals length
-    uint64_t ofv = (uint64_t(1) << ofc) + bitr_read(br, ofc);
-    const uint32_t ml = ML_BASE[mlc] + bitr_read(br, ML_BITS[mlc]);
-    const uint32_t ll = LL_BASE[llc] + bitr_read(br, LL_BITS[llc]);
-    // repeat offsets (3.1.1.5), as libzstd's ZSTD_decodeSequence
-    uint64_t off;
-    if (ofv > 3) {
-      off = ofv - 3;
-      fs.rep2 = fs.rep1;
-      fs.rep1 = fs.rep0;
-      fs.rep0 = uint32_t(off);
-    } else {
-      const uint32_t idx = uint32_t(ofv) - 1 + (ll == 0 ? 1 : 0);  // 0..3
-      if (idx == 0) {
-        off = fs.rep0;
-      } else {
-        uint64_t t = idx == 3 ? uint64_t(fs.rep0) - 1 : (idx == 1 ? fs.rep1 : fs.rep2);
-        t += t == 0;  // libzstd: offset 0 is corrupt input, forced to 1
-        if (idx != 1) fs.rep2 = fs.rep1;
+  const bool w0 = lane == 0;
+  // largest k < cnt with arr[k] <= x (arr[0] == 0 <= x)
+  auto find = [](const uint32_t* arr, uint32_t cnt, uint32_t x) {
+    uint32_t lo = 0, hi = cnt;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (arr[mid] <= x)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    return lo;
+  };
+  for (uint32_t i = 0; i < nseq;) {
+    // ---- phase A: decode up to kSeqChunk sequences (wave-uniform) ----
+    const long long ta = o.prof ? clock64() : 0;
+    uint32_t cnt = 0, lsum = 0, osum = 0, msum = 0;
+    for (; cnt < kSeqChunk && i < nseq && (cnt == 0 || osum < kChunkOut / 2); ++cnt, ++i) {
+      if (br.pos < 0) return kErr;  // libzstd: the stream overflowed before this sequence
+      const uint32_t ell = rfl(sm.ll[sll]), eof = rfl(sm.of[sof]), eml = rfl(sm.ml[sml]);
+      const uint32_t vll = rfl(sm.llv[sll]), vof = rfl(sm.ofv[sof]), vml = rfl(sm.mlv[sml]);
+      if (fse_sym(ell) > 35 || fse_sym(eml) > 52 || fse_sym(eof) > 31) return kErr;
+      // extra bits: offset, then match length, then literals length
+      const uint64_t ofv = uint64_t(vof >> 5) + bitr_read_u(br, vof & 31);
+      const uint32_t ml = (vml >> 5) + bitr_read_u(br, vml & 31);
+      const uint32_t ll = (vll >> 5) + bitr_read_u(br, vll & 31);
+      // repeat offsets (3.1.1.5), as libzstd's ZSTD_decodeSequence
+      uint64_t off;
+      if (ofv > 3) {
+        off = ofv - 3;
+        fs.rep2 = fs.rep1;
         fs.rep1 = fs.rep0;
-        fs.rep0 = uint32_t(t);
-        off = t;
+        fs.rep0 = uint32_t(off);
+      } else {
+        const uint32_t idx = uint32_t(ofv) - 1 + (ll == 0 ? 1 : 0);  // 0..3
+        if (idx == 0) {
+          off = fs.rep0;
+        } else {
+          uint64_t t = idx == 3 ? uint64_t(fs.rep0) - 1 : (idx == 1 ? fs.rep1 : fs.rep2);
+          t += t == 0;  // libzstd: offset 0 is corrupt input, forced to 1
+          if (idx != 1) fs.rep2 = fs.rep1;
+          fs.rep1 = fs.rep0;
+          fs.rep0 = uint32_t(t);
+          off = t;
+        }
       }
+      if (i + 1 < nseq) {  // state updates: literals length, match length, offset
+        sll = fse_base(ell) + bitr_read_u(br, fse_nb(ell));
+        sml = fse_base(eml) + bitr_read_u(br, fse_nb(eml));
+        sof = fse_base(eof) + bitr_read_u(br, fse_nb(eof));
+      }
+      // execution checks (3.1.1.4): literals available, match inside the frame
+      if (uint64_t(lsum) + ll > lit_left) return kErr;
+      const uint64_t mstart = o.pos + osum + ll;
+      if (mstart + ml > o.cap) return kCap;
+      if (off > mstart - o.frame0) return kErr;  // before the frame start (no dictionary)
+      if (w0) {
+        sm.s_ll[cnt] = ll;
+        sm.s_ml[cnt] = ml;
+        sm.s_off[cnt] = uint32_t(off);
+        sm.s_lpre[cnt] = lsum;
+        sm.s_opre[cnt] = osum;
+        sm.s_mpre[cnt] = msum;
+      }
+      lsum += ll;
+      osum += ll + ml;
+      msum += ml;
     }
-    if (i + 1 < nseq) {  // state updates: literals length, match length, offset
-      sll = fse_base(ell) + bitr_read(br, fse_nb(ell));
-      sml = fse_base(eml) + bitr_read(br, fse_nb(eml));
-      sof = fse_base(eof) + bitr_read(br, fse_nb(eof));
+    if (w0) {
+      sm.s_lpre[cnt] = lsum;
+      sm.s_opre[cnt] = osum;
+      sm.s_mpre[cnt] = msum;
     }
-    // execute (3.1.1.4): literals, then the match
-    if (!emit_lits(ll)) return (o.pos + ll > o.cap) ? kCap : kErr;
-    if (off > o.pos - o.frame0) return kErr;  // before the frame start (no dictionary)
-    if (o.pos + ml > o.cap) return kCap;
-    const uint64_t q = o.pos - off;
-    if (q + (ml < off ? ml : off) > o.committed) commit(o);
-    for (uint64_t j = lane; j < ml; j += 64) o.base[o.pos + j] = o.base[q + (j % off)];
-    o.pos += ml;
+    __syncthreads();
+    const long long tb = o.prof ? clock64() : 0;
+    prof_add(o, 2, tb - ta);
+    commit(o);  // output before this chunk is visible to every lane
+    // ---- phase B: every literal byte and match byte of the chunk in parallel ----
+    const uint64_t O = o.pos;
+    const bool mapped = osum <= kChunkOut && cnt <= 256;
+    if (mapped) {  // byte map: sequence k owns chunk output [opre[k], opre[k+1])
+      for (uint32_t k = lane; k < cnt; k += 64)
+        for (uint32_t x = sm.s_opre[k]; x < sm.s_opre[k + 1]; ++x) sm.s_map[x] = uint8_t(k);
+      __syncthreads();
+    }
+    auto seq_of = [&](uint32_t rel) -> uint32_t {
+      return mapped ? uint32_t(sm.s_map[rel]) : find(sm.s_opre, cnt, rel);
+    };
+    for (uint32_t j = lane; j < lsum; j += 64) {
+      const uint32_t k = find(sm.s_lpre, cnt, j);
+      const uint8_t v = rle ? rle_byte : lits[lit_pos + j];
+      o.base[O + sm.s_opre[k] + (j - sm.s_lpre[k])] = v;
+    }
+    // match bytes, in output order so a lane's items resolve through the map;
+    // four items per lane resolve their sources before any load is issued
+    const uint32_t tot = osum;
+    for (uint32_t r0 = lane; r0 < tot; r0 += 64 * 4) {
+      const uint8_t* srcp[4];
+      uint64_t dst[4];
+      bool live[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t rel0 = r0 + 64 * u;
+        live[u] = false;
+        srcp[u] = o.base;
+        dst[u] = 0;
+        if (rel0 >= tot) continue;
+        uint32_t k = seq_of(rel0);
+        uint32_t in = rel0 - sm.s_opre[k];
+        if (in < sm.s_ll[k]) continue;  // a literal byte: written above
+        live[u] = true;
+        dst[u] = O + rel0;
+        // follow the copy back until it lands on a literal or on earlier output
+        uint32_t t = in - sm.s_ll[k];
+        for (;;) {
+          const uint32_t off = sm.s_off[k];
+          const uint64_t src = O + sm.s_opre[k] + sm.s_ll[k] - off + (t % off);
+          if (src < O) {
+            srcp[u] = o.base + src;
+            break;
+          }
+          const uint32_t rel = uint32_t(src - O);
+          const uint32_t k2 = seq_of(rel);
+          const uint32_t in2 = rel - sm.s_opre[k2];
+          if (in2 < sm.s_ll[k2]) {
+            srcp[u] = rle ? nullptr : lits + lit_pos + sm.s_lpre[k2] + in2;
+            break;
+          }
+          k = k2;
+          t = in2 - sm.s_ll[k2];
+        }
+      }
+      uint8_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = (live[u] && srcp[u]) ? *srcp[u] : rle_byte;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (live[u]) o.base[dst[u]] = v[u];
+    }
+    o.pos += osum;
+    lit_pos += lsum;
+    lit_left -= lsum;
+    __syncthreads();  // the chunk arrays are rewritten by the next phase A
+    if (o.prof) prof_add(o, 6, clock64() - tb);
   }
   if (br.pos > 0) return kErr;  // unread bits: corrupt (an over-read on the last one passes)
+  if (o.prof) prof_add(o, 1, clock64() - t1);
+  prof_add(o, 4, nseq);
   if (o.pos + lit_left > o.cap) return kCap;
   emit_lits(lit_left);
   return kOK;
@@ -645,8 +815,17 @@ __device__ uint64_t xxh64_out(const uint8_t* base, uint64_t len) {
   const uint32_t q = lane & 3;
   uint64_t acc = (q == 0) ? XP1 + XP2 : (q == 1) ? XP2 : (q == 2) ? 0 : 0 - XP1;
   const uint64_t nstripe = len / 32;
-  if (lane < 4)
-    for (uint64_t s = 0; s < nstripe; ++s) acc = xround(acc, ld64u(base + s * 32 + q * 8));
+  if (lane < 4) {
+    uint64_t s = 0;
+    for (; s + 8 <= nstripe; s += 8) {  // eight loads in flight ahead of the chain
+      uint64_t x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = ld64u(base + (s + u) * 32 + q * 8);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = xround(acc, x[u]);
+    }
+    for (; s < nstripe; ++s) acc = xround(acc, ld64u(base + s * 32 + q * 8));
+  }
   const uint64_t a1 = __shfl(acc, 1, 64), a2 = __shfl(acc, 2, 64), a3 = __shfl(acc, 3, 64);
   const uint64_t a0 = __shfl(acc, 0, 64);
   uint64_t h;
@@ -761,8 +940,10 @@ __device__ int32_t decode_frames(Smem& sm, const uint8_t* src, int64_t n, Out& o
     if (has_csum) {
       if (n - at < 4) return kErr;
       commit(o);
+      const long long tc = o.prof ? clock64() : 0;
       const uint32_t want = ld32z(src, at, n);
       const uint64_t h = xxh64_out(o.base + o.frame0, o.pos - o.frame0);
+      (void)tc;
       if (uint32_t(h) != want) return kErr;
       at += 4;
     }
@@ -775,18 +956,24 @@ __device__ int32_t decode_frames(Smem& sm, const uint8_t* src, int64_t n, Out& o
 // One wave per segment block, persistent over the batch.  Inputs: the raw
 // descriptors; outputs: decompressed bytes at dec + cap_off[b], their length,
 // and a per-block status (OKV_BLK_*).  lit = per-wave literal scratch.
+
 __global__ __launch_bounds__(64) void okv_zstd_kernel(const uint8_t* __restrict__ seg,
                                                       uint64_t seg_bytes, const Desc* __restrict__ descs,
                                                       uint32_t nblk, const uint64_t* __restrict__ cap_off,
                                                       uint8_t* __restrict__ dec, uint64_t* __restrict__ dec_len,
                                                       int32_t* __restrict__ zstatus,
-                                                      uint8_t* __restrict__ lit) {
+                                                      uint8_t* __restrict__ lit,
+                                                      unsigned long long* __restrict__ prof,
+                                                      int stage_on) {
   __shared__ zst::Smem sm;
   uint8_t* lit_buf = lit + uint64_t(blockIdx.x) * zst::kBlockMax;
+
   for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
     const Desc d = descs[b];
     int32_t st = OKV_BLK_OK;
     zst::Out o;
+    o.prof = prof;
+    const long long tb = prof ? clock64() : 0;
     o.base = dec + cap_off[b];
     o.cap = cap_off[b + 1] - cap_off[b];
     o.pos = o.committed = o.frame0 = 0;
@@ -797,12 +984,19 @@ __global__ __launch_bounds__(64) void okv_zstd_kernel(const uint8_t* __restrict_
     } else if (d.compressed_size > d.block_size) {
       st = OKV_BLK_PANIC;  // rawBlockBytes[:CompressedSize] out of range (:321)
     } else {
-      const int32_t r = zst::decode_frames(sm, seg + d.offset, int64_t(d.compressed_size), o, lit_buf);
+      const uint8_t* src = seg + d.offset;
+      (void)stage_on;  // LDS staging of the frames measured no gain (refills hit L2)
+      const int32_t r = zst::decode_frames(sm, src, int64_t(d.compressed_size), o, lit_buf);
+      __syncthreads();
       st = r == zst::kOK ? OKV_BLK_OK : r == zst::kCap ? OKV_BLK_CAPACITY : OKV_BLK_ZSTD_ERROR;
     }
     if ((threadIdx.x & 63) == 0) {
       zstatus[b] = st;
       dec_len[b] = st == OKV_BLK_OK ? o.pos : 0;
+    }
+    if (prof) {
+      zst::prof_add(o, 3, clock64() - tb);
+      zst::prof_add(o, 7, 1);
     }
     __builtin_amdgcn_s_waitcnt(0);
   }
@@ -852,8 +1046,24 @@ __global__ void okv_zstd_desc_kernel(const Desc* __restrict__ descs, uint32_t nb
 void launch_zstd(hipStream_t s, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
                  uint32_t nblk, const uint64_t* cap_off, uint8_t* dec, uint64_t* dec_len,
                  int32_t* zstatus, uint8_t* lit, uint32_t grid) {
+  // OKV_ZSTD_PROF=1: per-phase clock64 totals printed to stderr (diagnostics only)
+  static unsigned long long* prof = nullptr;
+  const bool want = getenv("OKV_ZSTD_PROF") != nullptr;
+  if (want && !prof) (void)hipMalloc(&prof, 8 * sizeof(unsigned long long));
+  if (want) (void)hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), s);
   hipLaunchKernelGGL(okv_zstd_kernel, dim3(grid), dim3(64), 0, s, seg, seg_bytes, descs, nblk,
-                     cap_off, dec, dec_len, zstatus, lit);
+                     cap_off, dec, dec_len, zstatus, lit, want ? prof : nullptr,
+                     getenv("OKV_ZSTD_STAGE") ? atoi(getenv("OKV_ZSTD_STAGE")) : 1);
+  if (want) {
+    unsigned long long h[8];
+    (void)hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    fprintf(stderr,
+            "[zstd prof] blocks %llu cycles/block: total %.0f literals %.0f sequences %.0f "
+            "(phase A %.0f, phase B %.0f) | seqs/block %.0f commits/block %.0f\n",
+            h[7], double(h[3]) / h[7], double(h[0]) / h[7], double(h[1]) / h[7],
+            double(h[2]) / h[7], double(h[6]) / h[7], double(h[4]) / h[7], double(h[5]) / h[7]);
+  }
 }
 void launch_zstd_cap(hipStream_t s, const Desc* descs, uint32_t nblk, uint64_t* cap_off) {
   hipLaunchKernelGGL(okv_zstd_cap_kernel, dim3(1), dim3(1024), 0, s, descs, nblk, cap_off);

@@ -1,0 +1,26 @@
+"""zstd decode diagnostics on the CZ workload: phase cycle counters
+(OKV_ZSTD_PROF) and an A/B of LDS staging (OKV_ZSTD_STAGE)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import objectkv_amd as okv  # noqa: E402
+from tools.zstd_gen import text_zstd_segment  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+seg, descs, orig = text_zstd_segment(n, 5)
+dec = okv.Decoder(0)
+for stage in ("1",):
+    os.environ["OKV_ZSTD_STAGE"] = stage
+    os.environ.pop("OKV_ZSTD_PROF", None)
+    dec.profile(True)
+    got = dec.decode(seg, descs, compression=okv.sst.COMP_ZSTD)
+    ms, calls = dec.profile_read()
+    assert int(got.status.max()) == 0
+    print(f"stage={stage}: zstd+count {ms['count']:.2f} ms, gather {ms['copy']:.2f} ms, "
+          f"{orig / ms['count'] / 1e6:.1f} GB/s decompressed", flush=True)
+for stage in ("1",):
+    os.environ["OKV_ZSTD_STAGE"] = stage
+    os.environ["OKV_ZSTD_PROF"] = "1"
+    print("stage", stage, flush=True)
+    dec.decode(seg, descs, compression=okv.sst.COMP_ZSTD)

@@ -791,7 +791,10 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_region_kernel(PackParam
 // padding), then each lane ORs its records' header / key / value bytes in
 // (16-byte source windows realigned to the destination, all loads of a field
 // issued together), then the image is stored with aligned 16-byte stores.
-constexpr uint32_t kImage = 32768;
+// 16 KiB: 8 workgroups per CU, so one's XXH64 tail overlaps the others' copies
+// (C4 pack + hash: 32 KiB 5.2 ms, 16 KiB 4.3 ms)
+constexpr uint32_t kImage = 16384;
+constexpr uint32_t kMetaImage = 32768;
 
 // OR the first nbytes (<= 16; higher bytes of w must be zero) of w into the
 // LDS byte image at byte address d.
@@ -852,9 +855,10 @@ __device__ __forceinline__ void lds_copy_field(uint32_t* img, uint32_t d, const 
   }
 }
 
+template <uint32_t IMG>
 __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb,
                                                                     uint32_t G) {
-  __shared__ uint4 img4[kImage / 16];
+  __shared__ uint4 img4[IMG / 16];
   __shared__ uint64_t bfirst[kMaxRegion + 1], brel[kMaxRegion], bbase[kMaxRegion];
   uint32_t* img = reinterpret_cast<uint32_t*>(img4);
   const uint64_t k0 = uint64_t(blockIdx.x) * G;
@@ -1062,12 +1066,12 @@ __global__ __launch_bounds__(kThreads) void okv_enc_meta_kernel(MetaParams P) {
 }
 
 // E12 via LDS: one workgroup builds the entries of kThreads consecutive blocks
-// (one contiguous byte range of the meta block, <= kImage bytes) in an LDS
+// (one contiguous byte range of the meta block, <= kMetaImage bytes) in an LDS
 // image and stores it with aligned 16-byte stores; the range's unaligned head
 // and tail bytes (shared with neighbouring workgroups) are stored bytewise.
 __global__ __launch_bounds__(kThreads) void okv_enc_meta_lds_kernel(MetaParams P,
                                                                     uint64_t meta_bytes) {
-  __shared__ uint4 img4[kImage / 16 + 2];
+  __shared__ uint4 img4[kMetaImage / 16 + 2];
   __shared__ int big;
   uint32_t* img = reinterpret_cast<uint32_t*>(img4);
   const uint64_t k0 = uint64_t(blockIdx.x) * kThreads;
@@ -1076,7 +1080,7 @@ __global__ __launch_bounds__(kThreads) void okv_enc_meta_lds_kernel(MetaParams P
   const uint64_t hi = k1 < P.nb ? P.moff[k1] : meta_bytes;
   const uint64_t a0 = lo & ~uint64_t(15);  // image byte 0 = meta byte a0
   const uint32_t nq = uint32_t((hi - a0 + 15) >> 4);
-  if (threadIdx.x == 0) big = (hi - a0 + 15) > kImage;
+  if (threadIdx.x == 0) big = (hi - a0 + 15) > kMetaImage;
   __syncthreads();
   const uint64_t k = k0 + threadIdx.x;
   if (big) {  // long first keys: byte stores
@@ -1395,13 +1399,19 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
        uint64_t(kMaxChunks) * 16 / std::max<uint64_t>(pl.bmax, 1)});
   // record-major LDS assembly pays off for small records (most chunks would
   // mix fields); large records take the chunk-major kernels
-  const uint64_t GL = std::min<uint64_t>(kMaxRegion, kImage / std::max<uint64_t>(pl.bmax, 1));
+  const char* eimg = getenv("OKV_ENC_IMAGE");  // diagnostic: LDS image bytes (16384 / 32768)
+  const uint32_t img = (eimg && atoi(eimg) == 32768) ? 32768u : kImage;
+  const uint64_t GL = std::min<uint64_t>(kMaxRegion, img / std::max<uint64_t>(pl.bmax, 1));
   const bool aligned = o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0;
   const char* evar = getenv("OKV_ENC_VARIANT");
   const int EV = evar ? atoi(evar) : 0;
   if (aligned && GL >= 1 && pl.avg_rec <= 512 && EV != 3) {
-    hipLaunchKernelGGL(okv_enc_pack_lds_kernel, dim3(ceil_div(pl.nb, GL)), dim3(kThreads), 0,
-                       ctx->stream, pp, pl.nb, uint32_t(GL));
+    if (img == 32768)
+      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<32768>, dim3(ceil_div(pl.nb, GL)),
+                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
+    else
+      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<kImage>, dim3(ceil_div(pl.nb, GL)),
+                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
     hashed = true;
   } else if (aligned && G >= 1) {
     const int V = EV;

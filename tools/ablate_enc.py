@@ -15,6 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=100_000_000)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--variants", default="0,1,2")
+ap.add_argument("--images", default="32768", help="OKV_ENC_IMAGE values to interleave")
 args = ap.parse_args()
 n = args.rows
 dev = torch.device("cuda", 0)
@@ -28,11 +29,12 @@ rows = dict(key_arena=torch.empty(n * 16, dtype=torch.uint8, device=dev),
 enc.synth_fixed_device(1, 0, n, 16, 64, rows)
 nb = -(-n // 42) + 1
 out = dict(seg=torch.empty(nb * 4096 + nb * 60 + 4096, dtype=torch.uint8, device=dev))
-variants = [int(v) for v in args.variants.split(",")]
+variants = [(int(v), int(i)) for v in args.variants.split(",") for i in args.images.split(",")]
 res = {v: [] for v in variants}
 for rep in range(args.reps):
     for v in variants:
-        os.environ["OKV_ENC_VARIANT"] = str(v)
+        os.environ["OKV_ENC_VARIANT"] = str(v[0])
+        os.environ["OKV_ENC_IMAGE"] = str(v[1])
         enc.profile(True)
         enc.profile_reset_encode()
         enc.encode_device(rows, n, out, strict_go=False, close=False)

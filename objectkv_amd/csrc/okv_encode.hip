@@ -12,7 +12,9 @@
 // The greedy cut is a chain: the block starting at row a ends at the first
 // row b with P(b) - P(a-1) >= T (P = inclusive prefix of record sizes), and
 // the next block starts at b+1.  Launches (DESIGN.md "Encode"):
-//   E1 okv_enc_size_kernel   record sizes, 2048-row tile scans, empty-key check
+//   E1 okv_enc_size_next_kernel  record sizes, 2048-row tile scans, empty-key
+//                            check, and next(a) from a 256-row lookahead (E3 below
+//                            only when a block is longer than that)
 //   E2 okv_enc_scan_kernel   tile totals -> tile prefixes (one workgroup)
 //   E3 okv_enc_next_kernel   next(a) - a for every row: 2048-row tiles stage
 //                            P over the tile + 2048 rows of lookahead in LDS and
@@ -68,7 +70,8 @@ struct EncTotals {
   unsigned long long head;        // meta head bytes (keys, bloom, compression, count)
   unsigned long long fault;       // a chain-table invariant failed (never expected)
   unsigned long long bmax;        // largest BlockSize
-  unsigned long long pad[5];
+  unsigned long long far;         // a block longer than the fused lookahead
+  unsigned long long pad[4];
 };
 
 struct EncScratch {
@@ -167,6 +170,8 @@ __device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
   return v;
 }
 
+__global__ void okv_enc_init_wmax_kernel(EncTotals* t) { t->wmax = 0; }
+
 __global__ void okv_enc_init_kernel(EncTotals* t) {
   t->min_size = kNone;
   t->bad_row = kNone;
@@ -179,58 +184,123 @@ __global__ void okv_enc_init_kernel(EncTotals* t) {
   t->head = 0;
   t->fault = 0;
   t->bmax = 0;
+  t->far = 0;
 }
 
 // ---------------------------------------------------------------------------
-// E1: record sizes (WriteRow :121-125 frames 6 + len(key) + len(val) bytes),
-// tile-local inclusive scan, empty-key check (:89-91), smallest record.
+// E1 (with E3 fused): record sizes (WriteRow :121-125 frames 6 + len(key) +
+// len(val) bytes), empty-key check (:89-91), tile-local prefix AND next(a).  next(a) only
+// depends on differences of P, so a tile that stages the record sizes of its
+// rows plus kFuseLook lookahead rows computes it without the global prefix.
+// A block longer than the lookahead sets tot->far; the host then reruns E3
+// (okv_enc_next_kernel) over global P for every row.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void okv_enc_size_kernel(
+constexpr uint32_t kFuseLook = 256;
+constexpr uint32_t kFuseWin = kETile + kFuseLook;  // staged rows
+constexpr int kFuseItems = kFuseWin / kThreads;    // 9
+
+__global__ __launch_bounds__(kThreads) void okv_enc_size_next_kernel(
     const uint16_t* __restrict__ key_len, const uint32_t* __restrict__ val_len, uint64_t n,
-    uint64_t* __restrict__ pl, uint64_t* __restrict__ tile_tot, EncTotals* __restrict__ tot) {
-  __shared__ uint64_t sz[kETile];  // striped in/out, blocked compute
+    uint64_t T, uint64_t* __restrict__ pl, uint64_t* __restrict__ tile_tot,
+    uint32_t* __restrict__ nx, EncTotals* __restrict__ tot) {
+  __shared__ uint64_t W[kFuseWin + 1];  // W[m] = sum of sizes of window rows [0, m)
   __shared__ uint64_t sm[kThreads / 64 + 1];
-  const uint64_t tb = uint64_t(blockIdx.x) * kETile;
+  const uint64_t cs = uint64_t(blockIdx.x) * kETile;
+  const uint64_t nwin = std::min<uint64_t>(n - cs, kFuseWin);
   uint64_t mn = kNone, bad = kNone;
-#pragma unroll
-  for (int i = 0; i < kEItems; ++i) {  // coalesced loads
+  for (int i = 0; i < kFuseItems; ++i) {  // coalesced loads
     const uint32_t j = i * kThreads + threadIdx.x;
-    const uint64_t r = tb + j;
-    uint64_t s = 0;
-    if (r < n) {
+    uint64_t sz = 0;
+    if (j < nwin) {
+      const uint64_t r = cs + j;
       const uint32_t kl = key_len[r];
-      s = 6u + uint64_t(kl) + uint64_t(val_len[r]);
-      if (kl == 0 && r < bad) bad = r;
-      mn = s < mn ? s : mn;
+      sz = 6u + uint64_t(kl) + uint64_t(val_len[r]);
+      if (j < kETile) {
+        if (kl == 0 && r < bad) bad = r;
+        mn = sz < mn ? sz : mn;
+      }
     }
-    sz[j] = s;
+    W[j + 1] = sz;
   }
   __syncthreads();
-  uint64_t loc[kEItems], sum = 0;
+  uint64_t loc[kFuseItems], sum = 0;
 #pragma unroll
-  for (int i = 0; i < kEItems; ++i) {
-    sum += sz[threadIdx.x * kEItems + i];
+  for (int i = 0; i < kFuseItems; ++i) {
+    sum += W[1 + threadIdx.x * kFuseItems + i];
     loc[i] = sum;
   }
   uint64_t total;
   const uint64_t ex = wg_excl_scan(sum, sm, total);
 #pragma unroll
-  for (int i = 0; i < kEItems; ++i) sz[threadIdx.x * kEItems + i] = ex + loc[i];
+  for (int i = 0; i < kFuseItems; ++i) W[1 + threadIdx.x * kFuseItems + i] = ex + loc[i];
+  if (threadIdx.x == 0) W[0] = 0;
   __syncthreads();
-#pragma unroll
-  for (int i = 0; i < kEItems; ++i) {  // coalesced stores
+  const uint32_t rows = uint32_t(std::min<uint64_t>(n - cs, kETile));
+  for (int i = 0; i < kEItems; ++i) {  // tile-local inclusive prefix, coalesced stores
     const uint32_t j = i * kThreads + threadIdx.x;
-    if (tb + j < n) pl[tb + j] = sz[j];
+    if (j < rows) pl[cs + j] = W[j + 1];
   }
-  if (threadIdx.x == 0) tile_tot[blockIdx.x] = total;
-  // one same-address atomic per wave would serialise in L2: only issue it
-  // when this wave improves on the value already there (values move one way)
+  if (threadIdx.x == 0) tile_tot[blockIdx.x] = W[rows];
+  // next(a): first m > a - cs with W[m] >= W[a - cs] + T  (b = cs + m - 1)
+  const uint32_t M = uint32_t(nwin) + 1;
+  const bool complete = cs + nwin == n;
+  const uint32_t a0 = threadIdx.x * kEItems;
+  uint64_t wmax = 0;
+  bool far = false;
+  uint32_t mb = 0;
+  uint32_t dv[kEItems];
+#pragma unroll
+  for (int i = 0; i < kEItems; ++i) dv[i] = 0;
+  for (int i = 0; i < kEItems; ++i) {
+    const uint32_t ar = a0 + i;
+    if (ar >= rows) break;
+    const uint64_t target = W[ar] + T;
+    if (i == 0) {
+      uint32_t L = ar + 1, H = M;
+      while (L < H) {
+        const uint32_t m = (L + H) >> 1;
+        if (W[m] >= target)
+          H = m;
+        else
+          L = m + 1;
+      }
+      mb = L;
+    } else {
+      mb = std::max(mb, ar + 1);
+      while (mb < M && W[mb] < target) ++mb;
+    }
+    uint64_t next;
+    if (mb < M)
+      next = cs + mb;
+    else if (complete)
+      next = n;
+    else {
+      far = true;
+      next = cs + ar + 1;
+    }
+    const uint64_t d = next - (cs + ar);
+    dv[i] = uint32_t(d);
+    wmax = d > wmax ? d : wmax;
+  }
+  if (cs + a0 + kEItems <= n) {
+    uint4* q = reinterpret_cast<uint4*>(nx + cs + a0);
+    q[0] = make_uint4(dv[0], dv[1], dv[2], dv[3]);
+    q[1] = make_uint4(dv[4], dv[5], dv[6], dv[7]);
+  } else {
+    for (int i = 0; i < kEItems; ++i)
+      if (cs + a0 + i < n) nx[cs + a0 + i] = dv[i];
+  }
   mn = wave_min64(mn);
   bad = wave_min64(bad);
+  wmax = wave_max64(wmax);
+  const bool anyfar = __any(far);
   if ((threadIdx.x & 63) == 0) {
     if (mn < __atomic_load_n(&tot->min_size, __ATOMIC_RELAXED))
       atomicMin(&tot->min_size, (unsigned long long)mn);
     if (bad != kNone) atomicMin(&tot->bad_row, (unsigned long long)bad);
+    if (wmax > __atomic_load_n(&tot->wmax, __ATOMIC_RELAXED))
+      atomicMax(&tot->wmax, (unsigned long long)wmax);
+    if (anyfar) atomicOr(&tot->far, 1ull);
   }
 }
 
@@ -1297,14 +1367,19 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   if ((rc = ensure_rows(ctx, e, n))) return rc;
   enc_mark(ctx, e, 0);
   hipLaunchKernelGGL(okv_enc_init_kernel, dim3(1), dim3(1), 0, ctx->stream, e->d_tot);
-  hipLaunchKernelGGL(okv_enc_size_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, R.kl,
-                     R.vl, n, e->pl, e->tile_tot, e->d_tot);
+  hipLaunchKernelGGL(okv_enc_size_next_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream,
+                     R.kl, R.vl, n, T, e->pl, e->tile_tot, e->nx, e->d_tot);
   hipLaunchKernelGGL(okv_enc_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, e->tile_tot,
                      uint64_t(ntiles), e->tile_pre, &e->d_tot->total_raw);
-  hipLaunchKernelGGL(okv_enc_next_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, e->pl,
-                     e->tile_pre, n, T, e->nx, e->d_tot);
   OKV_HIP(hipGetLastError());
   if ((rc = read_enc_totals(ctx, e))) return rc;
+  if (e->h_tot->far) {  // some block holds more rows than the fused lookahead: E3 over global P
+    hipLaunchKernelGGL(okv_enc_init_wmax_kernel, dim3(1), dim3(1), 0, ctx->stream, e->d_tot);
+    hipLaunchKernelGGL(okv_enc_next_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, e->pl,
+                       e->tile_pre, n, T, e->nx, e->d_tot);
+    OKV_HIP(hipGetLastError());
+    if ((rc = read_enc_totals(ctx, e))) return rc;
+  }
   if (e->h_tot->bad_row != kNone) {
     *bad_row = e->h_tot->bad_row;
     return set_err(ctx, OKV_W_INVALID_KEY, "key cannot be empty (ErrInvalidKey)");

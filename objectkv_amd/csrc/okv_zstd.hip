@@ -34,6 +34,7 @@ constexpr uint32_t kBlockMax = 1u << 17;  // Block_Maximum_Size (128 KiB)
 constexpr int kLLMaxAL = 9, kMLMaxAL = 9, kOFMaxAL = 8;
 constexpr uint32_t kSeqChunk = 256;      // sequences decoded before a parallel execution pass
 constexpr uint32_t kChunkOut = 4096;     // output bytes per chunk covered by the byte map
+constexpr uint32_t kChunkClose = 3072;   // a chunk takes no more sequences past this output
 
 enum : int32_t { kOK = 0, kErr = 1, kCap = 2 };
 
@@ -62,15 +63,14 @@ __constant__ int16_t OF_DEF[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1,  1,  1,  
 // FSE decoding table entry: symbol | nbBits << 8 | baseline << 16.
 __device__ __forceinline__ uint32_t fse_sym(uint32_t e) { return e & 0xff; }
 __device__ __forceinline__ uint32_t fse_nb(uint32_t e) { return (e >> 8) & 0xff; }
-__device__ __forceinline__ uint32_t fse_base(uint32_t e) { return e >> 16; }
+__device__ __forceinline__ uint32_t fse_base(uint32_t e) { return (e >> 16) & 0x1ff; }
+__device__ __forceinline__ uint32_t fse_xb(uint32_t e) { return e >> 25; }
 
 struct __align__(16) Smem {
-  uint32_t ll[1 << kLLMaxAL];   // FSE states (symbol | nbBits | nextState baseline)
+  // FSE states: symbol | nbBits << 8 | nextState baseline << 16 (9 bits) | extra bits << 25
+  uint32_t ll[1 << kLLMaxAL];
   uint32_t ml[1 << kMLMaxAL];
   uint32_t of[1 << kOFMaxAL];
-  uint32_t llv[1 << kLLMaxAL];  // per state: baseValue << 5 | extra bits (libzstd's seqSymbol)
-  uint32_t mlv[1 << kMLMaxAL];
-  uint32_t ofv[1 << kOFMaxAL];
   uint32_t hw[1 << 6];         // FSE table of the Huffman weights (AL <= 6)
   uint16_t huf[1 << kHufMaxBits];
   uint16_t next[64];           // FSE build scratch (symbolNext)
@@ -78,12 +78,11 @@ struct __align__(16) Smem {
   uint8_t wgt[256];            // Huffman weights
   uint16_t hstart[256];        // first decoding-table entry of each symbol
   uint32_t rank[kHufMaxBits + 2];
-  // one chunk of decoded sequences (phase A) for parallel execution (phase B)
-  uint32_t s_ll[kSeqChunk], s_ml[kSeqChunk], s_off[kSeqChunk];
-  uint32_t s_lpre[kSeqChunk + 1];  // exclusive prefix of literal lengths
-  uint32_t s_opre[kSeqChunk + 1];  // exclusive prefix of ll + ml (output offsets)
-  uint32_t s_mpre[kSeqChunk + 1];  // exclusive prefix of match lengths
-  uint8_t s_map[kChunkOut];        // chunk output byte -> its sequence (low 8 bits)
+  // one chunk of decoded sequences (phase A) for parallel execution (phase B):
+  // phase A writes {ll, ml, off, -}; the scan rewrites {opre, ll, off, lpre}
+  // (output / literal prefix of the chunk); rec[cnt] = {osum, 0, 0, lsum}
+  uint4 rec[kSeqChunk + 1];
+  uint8_t map[kChunkOut];      // chunk output byte -> its sequence (low 8 bits)
 };
 
 // ---- byte access -------------------------------------------------------------
@@ -115,6 +114,13 @@ __device__ __forceinline__ uint32_t rd8(const uint8_t* p) { return *p; }
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
   return uint64_t(rfl(uint32_t(x))) | (uint64_t(rfl(uint32_t(x >> 32))) << 32);
+}
+// Values the compiler cannot prove wave-uniform (anything derived from a flat
+// load) are re-declared uniform, so the serial decode stays in SGPRs / SALU.
+__device__ __forceinline__ int64_t rfls64(int64_t x) { return int64_t(rfl64(uint64_t(x))); }
+template <class T>
+__device__ __forceinline__ T* rflp(T* p) {
+  return reinterpret_cast<T*>(rfl64(reinterpret_cast<uint64_t>(p)));
 }
 
 // ---- backward bit reader (FSE / Huffman streams) --------------------------------
@@ -436,26 +442,98 @@ __device__ __forceinline__ void out_copy(Out& o, const uint8_t* src, uint64_t n)
   o.pos += n;
 }
 
-// Per-state (baseValue, extra bits) for one sequence table, so the decode loop
-// reads one LDS word per state instead of constant-memory lookups.  kind: 0 LL, 1 OF, 2 ML.
-__device__ void seq_values(const uint32_t* table, uint32_t* vals, uint32_t al, int kind) {
+// Extra-bits count of each state's symbol into bits 25..29 of its entry, so the
+// sequence loop reads one LDS word per state.  kind: 0 LL, 1 OF, 2 ML.
+__device__ void seq_xbits(uint32_t* table, uint32_t al, int kind) {
   const int lane = threadIdx.x & 63;
   for (uint32_t u = lane; u < (1u << al); u += 64) {
-    const uint32_t c = fse_sym(table[u]);
-    uint32_t base, bits;
-    if (kind == 0) {
-      base = LL_BASE[c < 36 ? c : 0];
-      bits = LL_BITS[c < 36 ? c : 0];
-    } else if (kind == 1) {
-      base = c < 32 ? (1u << c) : 0;
-      bits = c;
-    } else {
-      base = ML_BASE[c < 53 ? c : 0];
-      bits = ML_BITS[c < 53 ? c : 0];
-    }
-    vals[u] = (base << 5) | bits;
+    const uint32_t e = table[u] & 0x1ffffffu, c = fse_sym(e);
+    const uint32_t bits = kind == 0 ? LL_BITS[c < 36 ? c : 0] : kind == 1 ? c : ML_BITS[c < 53 ? c : 0];
+    table[u] = e | (bits << 25);
   }
   __syncthreads();
+}
+
+// ---- wave-uniform backward bit reader of the sequence stream ------------------
+// The container (64 bits) and positions live in SGPRs; refills read a 256-byte
+// window held in one VGPR (lane l = aligned dword wdw + l) with v_readlane, so
+// the serial sequence loop touches memory once per ~256 stream bytes.  A refill
+// leaves >= 57 bits in the container; a sequence reads at most 89 bits, so the
+// loop refills twice per sequence and the reads themselves are shift + mask.
+// Streams are < 128 KiB, so positions fit in 32 bits.
+struct SeqBits {
+  const uint8_t* abase;  // stream start rounded down to 4 bytes
+  int32_t s0;            // stream start - abase (0..3)
+  int32_t n;             // stream bytes
+  int32_t pos;           // remaining bits (relative to the stream start)
+  int32_t lo;            // container holds bits [lo, lo + 64)
+  uint64_t c;
+  int32_t wdw;           // first dword (from abase) of the window
+  uint32_t win;
+};
+
+__device__ __forceinline__ void seqwin_load(SeqBits& b, int32_t top_dw) {
+  const int lane = threadIdx.x & 63;
+  b.wdw = top_dw - 63;
+  const int32_t d = b.wdw + lane;
+  const int32_t lo = 4 * d, hi = lo + 4;  // this lane's bytes, relative to abase
+  uint32_t v = 0;
+  if (hi > b.s0 && lo < b.s0 + b.n) {
+    v = *reinterpret_cast<const uint32_t*>(b.abase + lo);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (lo + k < b.s0 || lo + k >= b.s0 + b.n) v &= ~(0xffu << (8 * k));
+  }
+  b.win = v;
+}
+
+__device__ __forceinline__ void seqbits_fill(SeqBits& b) {
+  const int32_t lb = ((b.pos + 7) >> 3) - 8;  // container = stream bytes [lb, lb + 8)
+  const int32_t A = b.s0 + lb;
+  const int32_t d0 = A >> 2;
+  const uint32_t sh = uint32_t(A & 3);
+  if (d0 < b.wdw || d0 + 2 > b.wdw + 63) seqwin_load(b, d0 + 2);
+  const int i0 = d0 - b.wdw;
+  const uint32_t x0 = __builtin_amdgcn_readlane(b.win, i0);
+  const uint32_t x1 = __builtin_amdgcn_readlane(b.win, i0 + 1);
+  const uint32_t x2 = __builtin_amdgcn_readlane(b.win, i0 + 2);
+  const uint64_t w = uint64_t(x0) | (uint64_t(x1) << 32);
+  b.c = sh ? (w >> (8 * sh)) | (uint64_t(x2) << (64 - 8 * sh)) : w;
+  b.lo = lb * 8;
+}
+
+// Refill when fewer than `need` (<= 57) bits are left.
+__device__ __forceinline__ void seqbits_reload(SeqBits& b, int32_t need) {
+  if (b.pos - b.lo < need) seqbits_fill(b);
+}
+
+__device__ __forceinline__ bool seqbits_init(SeqBits& b, const uint8_t* p, int32_t n) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  b.abase = reinterpret_cast<const uint8_t*>(a & ~uintptr_t(3));
+  b.s0 = int32_t(a & 3);
+  b.n = n;
+  b.wdw = INT32_MIN / 8;
+  b.pos = 0;
+  b.lo = 0;
+  b.c = 0;
+  b.win = 0;
+  if (n <= 0) return false;
+  const uint32_t last = rfl(p[n - 1]);
+  if (last == 0) return false;  // the final byte holds the end marker
+  b.pos = (n - 1) * 8 + (31 - __builtin_clz(last));
+  seqbits_fill(b);
+  return true;
+}
+
+// Bits [pos - nb, pos) (nb <= 31, already in the container), consumed; bits
+// below the stream read as 0.
+__device__ __forceinline__ uint32_t seqbits_take(SeqBits& b, uint32_t nb) {
+  b.pos -= int32_t(nb);
+  return uint32_t(b.c >> uint32_t(b.pos - b.lo)) & uint32_t((uint64_t(1) << nb) - 1);
+}
+__device__ __forceinline__ uint32_t seqbits_read(SeqBits& b, uint32_t nb) {
+  if (b.pos - b.lo < int32_t(nb)) seqbits_fill(b);
+  return seqbits_take(b, nb);
 }
 
 // Table for one of LL / OF / ML from the symbol compression mode.
@@ -495,6 +573,11 @@ __device__ int32_t seq_table(Smem& sm, uint32_t* table, uint32_t mode, const int
 // Decompress one compressed zstd block (RFC 8878 3.1.1.3) into the output.
 __device__ int32_t compressed_block(Smem& sm, FrameState& fs, Out& o, const uint8_t* p, int64_t n,
                                     uint8_t* lit_buf) {
+  p = rflp(p);
+  n = rfls64(n);
+  o.pos = rfl64(o.pos);
+  o.cap = rfl64(o.cap);
+  o.frame0 = rfl64(o.frame0);
   if (n < 1) return kErr;
   const long long t0 = o.prof ? clock64() : 0;
   // ---- literals section header (3.1.1.3.1.1)
@@ -639,168 +722,231 @@ __device__ int32_t compressed_block(Smem& sm, FrameState& fs, Out& o, const uint
                    fs.ll_al);
   if (used < 0) return kErr;
   at += used;
-  if ((modes >> 6) != 3) seq_values(sm.ll, sm.llv, fs.ll_al, 0);
+  if ((modes >> 6) != 3) seq_xbits(sm.ll, fs.ll_al, 0);
   used = seq_table(sm, sm.of, (modes >> 4) & 3, OF_DEF, 5, 29, 31, kOFMaxAL, p + at, n - at,
                    fs.of_ok, fs.of_al);
   if (used < 0) return kErr;
   at += used;
-  if (((modes >> 4) & 3) != 3) seq_values(sm.of, sm.ofv, fs.of_al, 1);
+  if (((modes >> 4) & 3) != 3) seq_xbits(sm.of, fs.of_al, 1);
   used = seq_table(sm, sm.ml, (modes >> 2) & 3, ML_DEF, 6, 53, 52, kMLMaxAL, p + at, n - at,
                    fs.ml_ok, fs.ml_al);
   if (used < 0) return kErr;
   at += used;
-  if (((modes >> 2) & 3) != 3) seq_values(sm.ml, sm.mlv, fs.ml_al, 2);
-  BitR br;
-  if (!bitr_init(br, p + at, n - at)) return kErr;
-  uint32_t sll = bitr_read_u(br, fs.ll_al);
-  uint32_t sof = bitr_read_u(br, fs.of_al);
-  uint32_t sml = bitr_read_u(br, fs.ml_al);
+  if (((modes >> 2) & 3) != 3) seq_xbits(sm.ml, fs.ml_al, 2);
+  at = rfls64(at);
+  nseq = rfl(nseq);
+  lit_left = rfl64(lit_left);
+  lit_pos = rfl64(lit_pos);
+  fs.ll_al = rfl(fs.ll_al);
+  fs.of_al = rfl(fs.of_al);
+  fs.ml_al = rfl(fs.ml_al);
+  fs.rep0 = rfl(fs.rep0);
+  fs.rep1 = rfl(fs.rep1);
+  fs.rep2 = rfl(fs.rep2);
+  SeqBits br;
+  if (!seqbits_init(br, p + at, n - at)) return kErr;
+  uint32_t sll = seqbits_read(br, fs.ll_al);
+  uint32_t sof = seqbits_read(br, fs.of_al);
+  uint32_t sml = seqbits_read(br, fs.ml_al);
   const int lane = threadIdx.x & 63;
   const bool w0 = lane == 0;
-  // largest k < cnt with arr[k] <= x (arr[0] == 0 <= x)
-  auto find = [](const uint32_t* arr, uint32_t cnt, uint32_t x) {
+  // largest k < cnt with rec[k].x <= x (rec[0].x == 0 <= x)
+  auto find = [&](uint32_t cnt, uint32_t x) {
     uint32_t lo = 0, hi = cnt;
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
-      if (arr[mid] <= x)
+      if (sm.rec[mid].x <= x)
         lo = mid;
       else
         hi = mid;
     }
     return lo;
   };
+  uint32_t rep0 = fs.rep0, rep1 = fs.rep1, rep2 = fs.rep2;
+  // 32-bit forms of the execution checks (blocks are < 2^31 bytes):
+  // literals left, output capacity left, output since the frame start
+  const uint32_t lit_lim = uint32_t(min<uint64_t>(lit_left, 0x7fffffffu));
   for (uint32_t i = 0; i < nseq;) {
-    // ---- phase A: decode up to kSeqChunk sequences (wave-uniform) ----
+    // ---- phase A: decode up to kSeqChunk sequences (wave-uniform, SALU) ----
     const long long ta = o.prof ? clock64() : 0;
-    uint32_t cnt = 0, lsum = 0, osum = 0, msum = 0;
-    for (; cnt < kSeqChunk && i < nseq && (cnt == 0 || osum < kChunkOut / 2); ++cnt, ++i) {
+    const uint32_t cap_lim = uint32_t(min<uint64_t>(o.cap - o.pos, 0x7fffffffu));
+    const uint32_t back = uint32_t(min<uint64_t>(o.pos - o.frame0, 0x7fffffffu));
+    const uint32_t lit_done = uint32_t(lit_pos);
+    uint32_t cnt = 0, lsum = 0, osum = 0;
+    for (; cnt < kSeqChunk && i < nseq && osum < kChunkClose; ++cnt, ++i) {
       if (br.pos < 0) return kErr;  // libzstd: the stream overflowed before this sequence
       const uint32_t ell = rfl(sm.ll[sll]), eof = rfl(sm.of[sof]), eml = rfl(sm.ml[sml]);
-      const uint32_t vll = rfl(sm.llv[sll]), vof = rfl(sm.ofv[sof]), vml = rfl(sm.mlv[sml]);
-      if (fse_sym(ell) > 35 || fse_sym(eml) > 52 || fse_sym(eof) > 31) return kErr;
       // extra bits: offset, then match length, then literals length
-      const uint64_t ofv = uint64_t(vof >> 5) + bitr_read_u(br, vof & 31);
-      const uint32_t ml = (vml >> 5) + bitr_read_u(br, vml & 31);
-      const uint32_t ll = (vll >> 5) + bitr_read_u(br, vll & 31);
+      seqbits_reload(br, 47);  // offset (<= 31) + match length (<= 16) extra bits
+      const uint32_t ofs = fse_sym(eof);
+      const uint32_t ofv = (1u << ofs) + seqbits_take(br, ofs);
+      const uint32_t mls = fse_sym(eml), lls = fse_sym(ell);
+      const uint32_t mlx = seqbits_take(br, fse_xb(eml));
+      seqbits_reload(br, 42);  // literals length (<= 16) + three states (<= 26)
+      const uint32_t ml = (mls < 32 ? mls + 3 : ML_BASE[mls]) + mlx;
+      const uint32_t ll = (lls < 16 ? lls : LL_BASE[lls]) + seqbits_take(br, fse_xb(ell));
       // repeat offsets (3.1.1.5), as libzstd's ZSTD_decodeSequence
-      uint64_t off;
+      uint32_t off;
       if (ofv > 3) {
         off = ofv - 3;
-        fs.rep2 = fs.rep1;
-        fs.rep1 = fs.rep0;
-        fs.rep0 = uint32_t(off);
+        rep2 = rep1;
+        rep1 = rep0;
+        rep0 = off;
       } else {
-        const uint32_t idx = uint32_t(ofv) - 1 + (ll == 0 ? 1 : 0);  // 0..3
+        const uint32_t idx = ofv - 1 + (ll == 0 ? 1 : 0);  // 0..3
         if (idx == 0) {
-          off = fs.rep0;
+          off = rep0;
         } else {
-          uint64_t t = idx == 3 ? uint64_t(fs.rep0) - 1 : (idx == 1 ? fs.rep1 : fs.rep2);
+          uint32_t t = idx == 3 ? rep0 - 1 : (idx == 1 ? rep1 : rep2);
           t += t == 0;  // libzstd: offset 0 is corrupt input, forced to 1
-          if (idx != 1) fs.rep2 = fs.rep1;
-          fs.rep1 = fs.rep0;
-          fs.rep0 = uint32_t(t);
+          if (idx != 1) rep2 = rep1;
+          rep1 = rep0;
+          rep0 = t;
           off = t;
         }
       }
       if (i + 1 < nseq) {  // state updates: literals length, match length, offset
-        sll = fse_base(ell) + bitr_read_u(br, fse_nb(ell));
-        sml = fse_base(eml) + bitr_read_u(br, fse_nb(eml));
-        sof = fse_base(eof) + bitr_read_u(br, fse_nb(eof));
+        sll = fse_base(ell) + seqbits_take(br, fse_nb(ell));
+        sml = fse_base(eml) + seqbits_take(br, fse_nb(eml));
+        sof = fse_base(eof) + seqbits_take(br, fse_nb(eof));
       }
       // execution checks (3.1.1.4): literals available, match inside the frame
-      if (uint64_t(lsum) + ll > lit_left) return kErr;
-      const uint64_t mstart = o.pos + osum + ll;
-      if (mstart + ml > o.cap) return kCap;
-      if (off > mstart - o.frame0) return kErr;  // before the frame start (no dictionary)
-      if (w0) {
-        sm.s_ll[cnt] = ll;
-        sm.s_ml[cnt] = ml;
-        sm.s_off[cnt] = uint32_t(off);
-        sm.s_lpre[cnt] = lsum;
-        sm.s_opre[cnt] = osum;
-        sm.s_mpre[cnt] = msum;
-      }
+      if (lsum + ll > lit_lim - lit_done) return kErr;
+      const uint32_t mstart = osum + ll;  // relative to o.pos
+      if (mstart + ml > cap_lim) return kCap;
+      if (off > back + mstart) return kErr;  // before the frame start (no dictionary)
+      if (w0) sm.rec[cnt] = make_uint4(ll, ml, uint32_t(off), 0);
       lsum += ll;
       osum += ll + ml;
-      msum += ml;
     }
-    if (w0) {
-      sm.s_lpre[cnt] = lsum;
-      sm.s_opre[cnt] = osum;
-      sm.s_mpre[cnt] = msum;
-    }
-    __syncthreads();
     const long long tb = o.prof ? clock64() : 0;
     prof_add(o, 2, tb - ta);
     commit(o);  // output before this chunk is visible to every lane
-    // ---- phase B: every literal byte and match byte of the chunk in parallel ----
+    __syncthreads();
+    // ---- phase B: prefixes by a wave scan, byte -> sequence map, then every
+    // literal byte and match byte of the chunk in parallel ----
+    {
+      uint4 r[4];
+      uint32_t lt = 0, ot = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t k = 4 * lane + u;
+        r[u] = k < cnt ? sm.rec[k] : make_uint4(0, 0, 0, 0);
+        lt += r[u].x;
+        ot += r[u].x + r[u].y;
+      }
+      uint32_t lp = wave_incl_scan32(lt, lane) - lt, op = wave_incl_scan32(ot, lane) - ot;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t k = 4 * lane + u;
+        if (k < cnt) sm.rec[k] = make_uint4(op, r[u].x, r[u].z, lp);
+        lp += r[u].x;
+        op += r[u].x + r[u].y;
+      }
+      if (w0) sm.rec[cnt] = make_uint4(osum, 0, 0, lsum);
+    }
+    __syncthreads();
     const uint64_t O = o.pos;
-    const bool mapped = osum <= kChunkOut && cnt <= 256;
-    if (mapped) {  // byte map: sequence k owns chunk output [opre[k], opre[k+1])
-      for (uint32_t k = lane; k < cnt; k += 64)
-        for (uint32_t x = sm.s_opre[k]; x < sm.s_opre[k + 1]; ++x) sm.s_map[x] = uint8_t(k);
+    const bool mapped = osum <= kChunkOut;
+    if (mapped) {  // map[x] = k on [opre[k], opre[k+1]): markers, then a running max
+      uint4* m4 = reinterpret_cast<uint4*>(sm.map);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) m4[4 * lane + u] = make_uint4(0, 0, 0, 0);
+      __syncthreads();
+      for (uint32_t k = lane + 1; k < cnt; k += 64) sm.map[sm.rec[k].x] = uint8_t(k);
+      __syncthreads();
+      uint4 v[4];
+      uint32_t mx = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = m4[4 * lane + u];
+        const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) mx = max(mx, (w4[q] >> (8 * t)) & 0xffu);
+      }
+      // exclusive max-scan over lanes
+      uint32_t run = mx;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(run, d, 64);
+        if (lane >= d) run = max(run, y);
+      }
+      run = __shfl_up(run, 1, 64);
+      if (lane == 0) run = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t outw = 0;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            run = max(run, (w4[q] >> (8 * t)) & 0xffu);
+            outw |= run << (8 * t);
+          }
+          w4[q] = outw;
+        }
+        m4[4 * lane + u] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
       __syncthreads();
     }
-    auto seq_of = [&](uint32_t rel) -> uint32_t {
-      return mapped ? uint32_t(sm.s_map[rel]) : find(sm.s_opre, cnt, rel);
-    };
-    for (uint32_t j = lane; j < lsum; j += 64) {
-      const uint32_t k = find(sm.s_lpre, cnt, j);
-      const uint8_t v = rle ? rle_byte : lits[lit_pos + j];
-      o.base[O + sm.s_opre[k] + (j - sm.s_lpre[k])] = v;
-    }
-    // match bytes, in output order so a lane's items resolve through the map;
-    // four items per lane resolve their sources before any load is issued
-    const uint32_t tot = osum;
-    for (uint32_t r0 = lane; r0 < tot; r0 += 64 * 4) {
+    const uint8_t* lsrc = rle ? nullptr : lits + lit_pos;
+    const long long tr = o.prof ? clock64() : 0;
+    uint32_t hops = 0;
+    for (uint32_t r0 = lane; r0 < osum; r0 += 64 * 4) {
       const uint8_t* srcp[4];
-      uint64_t dst[4];
       bool live[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const uint32_t rel0 = r0 + 64 * u;
-        live[u] = false;
-        srcp[u] = o.base;
-        dst[u] = 0;
-        if (rel0 >= tot) continue;
-        uint32_t k = seq_of(rel0);
-        uint32_t in = rel0 - sm.s_opre[k];
-        if (in < sm.s_ll[k]) continue;  // a literal byte: written above
-        live[u] = true;
-        dst[u] = O + rel0;
-        // follow the copy back until it lands on a literal or on earlier output
-        uint32_t t = in - sm.s_ll[k];
+        live[u] = rel0 < osum;
+        srcp[u] = nullptr;
+        if (!live[u]) continue;
+        uint32_t rel = rel0;
+        // follow copies back until a literal byte or output before the chunk
         for (;;) {
-          const uint32_t off = sm.s_off[k];
-          const uint64_t src = O + sm.s_opre[k] + sm.s_ll[k] - off + (t % off);
-          if (src < O) {
-            srcp[u] = o.base + src;
+          const uint32_t k = mapped ? uint32_t(sm.map[rel]) : find(cnt, rel);
+          const uint4 R = sm.rec[k];
+          const uint32_t in = rel - R.x;
+          if (in < R.y) {
+            srcp[u] = lsrc ? lsrc + R.w + in : nullptr;
             break;
           }
-          const uint32_t rel = uint32_t(src - O);
-          const uint32_t k2 = seq_of(rel);
-          const uint32_t in2 = rel - sm.s_opre[k2];
-          if (in2 < sm.s_ll[k2]) {
-            srcp[u] = rle ? nullptr : lits + lit_pos + sm.s_lpre[k2] + in2;
+          const uint32_t t = in - R.y, off = R.z;
+          const uint32_t mo = t < off ? t : t % off;
+          const int64_t s = int64_t(R.x) + R.y + mo - int64_t(off);
+          if (s < 0) {
+            srcp[u] = o.base + (int64_t(O) + s);
             break;
           }
-          k = k2;
-          t = in2 - sm.s_ll[k2];
+          rel = uint32_t(s);
+          ++hops;
         }
       }
       uint8_t v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = (live[u] && srcp[u]) ? *srcp[u] : rle_byte;
+      for (int u = 0; u < 4; ++u) v[u] = srcp[u] ? *srcp[u] : rle_byte;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (live[u]) o.base[dst[u]] = v[u];
+        if (live[u]) o.base[O + r0 + 64 * u] = v[u];
     }
     o.pos += osum;
     lit_pos += lsum;
     lit_left -= lsum;
     __syncthreads();  // the chunk arrays are rewritten by the next phase A
-    if (o.prof) prof_add(o, 6, clock64() - tb);
+    if (o.prof) {
+      prof_add(o, 6, clock64() - tb);
+      prof_add(o, 8, clock64() - tr);
+      unsigned long long h = hops;
+      for (int d = 32; d; d >>= 1) h += __shfl_xor(h, d, 64);
+      prof_add(o, 9, h);
+    }
   }
+  fs.rep0 = rep0;
+  fs.rep1 = rep1;
+  fs.rep2 = rep2;
   if (br.pos > 0) return kErr;  // unread bits: corrupt (an over-read on the last one passes)
   if (o.prof) prof_add(o, 1, clock64() - t1);
   prof_add(o, 4, nseq);
@@ -1049,20 +1195,22 @@ void launch_zstd(hipStream_t s, const uint8_t* seg, uint64_t seg_bytes, const De
   // OKV_ZSTD_PROF=1: per-phase clock64 totals printed to stderr (diagnostics only)
   static unsigned long long* prof = nullptr;
   const bool want = getenv("OKV_ZSTD_PROF") != nullptr;
-  if (want && !prof) (void)hipMalloc(&prof, 8 * sizeof(unsigned long long));
-  if (want) (void)hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), s);
+  if (want && !prof) (void)hipMalloc(&prof, 16 * sizeof(unsigned long long));
+  if (want) (void)hipMemsetAsync(prof, 0, 16 * sizeof(unsigned long long), s);
   hipLaunchKernelGGL(okv_zstd_kernel, dim3(grid), dim3(64), 0, s, seg, seg_bytes, descs, nblk,
                      cap_off, dec, dec_len, zstatus, lit, want ? prof : nullptr,
                      getenv("OKV_ZSTD_STAGE") ? atoi(getenv("OKV_ZSTD_STAGE")) : 1);
   if (want) {
-    unsigned long long h[8];
+    unsigned long long h[16];
     (void)hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s);
     (void)hipStreamSynchronize(s);
     fprintf(stderr,
             "[zstd prof] blocks %llu cycles/block: total %.0f literals %.0f sequences %.0f "
-            "(phase A %.0f, phase B %.0f) | seqs/block %.0f commits/block %.0f\n",
+            "(phase A %.0f, phase B %.0f of which resolve %.0f) | seqs/block %.0f commits/block "
+            "%.0f hops/block %.0f\n",
             h[7], double(h[3]) / h[7], double(h[0]) / h[7], double(h[1]) / h[7],
-            double(h[2]) / h[7], double(h[6]) / h[7], double(h[4]) / h[7], double(h[5]) / h[7]);
+            double(h[2]) / h[7], double(h[6]) / h[7], double(h[8]) / h[7], double(h[4]) / h[7],
+            double(h[5]) / h[7], double(h[9]) / h[7]);
   }
 }
 void launch_zstd_cap(hipStream_t s, const Desc* descs, uint32_t nblk, uint64_t* cap_off) {

@@ -18,9 +18,8 @@ void launch_hash(hipStream_t stream, const uint8_t* seg, uint64_t seg_bytes, con
                  uint32_t nblk, uint64_t* out);
 // okv_zstd.hip: zstd block decompression into per-block scratch regions.
 void launch_zstd_cap(hipStream_t s, const Desc* descs, uint32_t nblk, uint64_t* cap_off);
-void launch_zstd(hipStream_t s, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
-                 uint32_t nblk, const uint64_t* cap_off, uint8_t* dec, uint64_t* dec_len,
-                 int32_t* zstatus, uint8_t* lit, uint32_t grid);
+int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
+             uint32_t nblk, uint64_t total);
 void launch_zstd_desc(hipStream_t s, const Desc* descs, uint32_t nblk, const uint64_t* cap_off,
                       const uint64_t* dec_len, Desc* out);
 constexpr uint32_t kZstdLitBytes = 1u << 17;  // per-wave literal scratch (Block_Maximum_Size)
@@ -67,8 +66,18 @@ struct okv_ctx {
   size_t z_cap_blocks = 0;
   uint8_t* z_dec = nullptr;       // decompressed blocks
   size_t z_cap_dec = 0;
-  uint8_t* z_lit = nullptr;       // per-wave literal scratch
+  uint8_t* z_lit = nullptr;       // per-wave literal scratch (general kernel)
   size_t z_cap_lit = 0;
+  uint8_t* z_blit = nullptr;      // per-block literal scratch (prologue -> executor)
+  size_t z_cap_blit = 0;
+  uint32_t* z_tabs = nullptr;     // per-block FSE tables (prologue -> sequence stage)
+  size_t z_cap_tabs = 0;
+  void* z_zb = nullptr;           // per-block zst::ZBlk
+  size_t z_cap_zb = 0;
+  uint64_t* z_seq_off = nullptr;  // [nblk + 1] sequence offsets
+  size_t z_cap_seq_off = 0;
+  uint64_t* z_seqs = nullptr;     // packed sequences
+  size_t z_cap_seqs = 0;
 };
 
 namespace okv {

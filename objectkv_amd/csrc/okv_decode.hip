@@ -861,12 +861,7 @@ int prepare(okv_ctx* ctx, const uint8_t* d_seg, uint64_t seg_bytes, const Desc* 
   OKV_HIP(hipStreamSynchronize(ctx->stream));
   if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_dec), &ctx->z_cap_dec, total + 64)))
     return rc;
-  const uint32_t grid = std::min<uint32_t>(nblk, 2048);
-  if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_lit), &ctx->z_cap_lit,
-                 size_t(grid) * kZstdLitBytes)))
-    return rc;
-  launch_zstd(ctx->stream, d_seg, seg_bytes, d_desc, nblk, ctx->z_cap_off, ctx->z_dec,
-              ctx->z_dec_len, ctx->z_status, ctx->z_lit, grid);
+  if ((rc = zstd_run(ctx, d_seg, seg_bytes, d_desc, nblk, total))) return rc;
   launch_zstd_desc(ctx->stream, d_desc, nblk, ctx->z_cap_off, ctx->z_dec_len, ctx->z_desc);
   OKV_HIP(hipGetLastError());
   // offsets <= total < seg_bytes, so no decompressed block reads as EOF
@@ -1115,6 +1110,11 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->z_desc);
   (void)hipFree(ctx->z_dec);
   (void)hipFree(ctx->z_lit);
+  (void)hipFree(ctx->z_blit);
+  (void)hipFree(ctx->z_tabs);
+  (void)hipFree(ctx->z_zb);
+  (void)hipFree(ctx->z_seq_off);
+  (void)hipFree(ctx->z_seqs);
   okv::enc_release(ctx);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;

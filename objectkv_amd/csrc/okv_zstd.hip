@@ -36,7 +36,10 @@ constexpr uint32_t kSeqChunk = 256;      // sequences decoded before a parallel 
 constexpr uint32_t kChunkOut = 4096;     // output bytes per chunk covered by the byte map
 constexpr uint32_t kChunkClose = 3072;   // a chunk takes no more sequences past this output
 
-enum : int32_t { kOK = 0, kErr = 1, kCap = 2 };
+enum : int32_t { kOK = 0, kErr = 1, kCap = 2, kSlow = 3, kDefer = 4 };
+// kSlow: the prologue stage hands the block to the general kernel; kDefer: its
+// sequences are decoded by the lane-per-block stage and executed by the
+// parallel executor (okv_zstd_seq_kernel, okv_zstd_exec_kernel).
 
 // Literals_Length and Match_Length baselines / extra bits (RFC 8878 3.1.1.3.2.1.1).
 __constant__ uint32_t LL_BASE[36] = {0,  1,  2,   3,   4,   5,    6,    7,    8,    9,     10,    11,
@@ -66,7 +69,7 @@ __device__ __forceinline__ uint32_t fse_nb(uint32_t e) { return (e >> 8) & 0xff;
 __device__ __forceinline__ uint32_t fse_base(uint32_t e) { return (e >> 16) & 0x1ff; }
 __device__ __forceinline__ uint32_t fse_xb(uint32_t e) { return e >> 25; }
 
-struct __align__(16) Smem {
+struct __align__(16) SmemCore {
   // FSE states: symbol | nbBits << 8 | nextState baseline << 16 (9 bits) | extra bits << 25
   uint32_t ll[1 << kLLMaxAL];
   uint32_t ml[1 << kMLMaxAL];
@@ -78,6 +81,8 @@ struct __align__(16) Smem {
   uint8_t wgt[256];            // Huffman weights
   uint16_t hstart[256];        // first decoding-table entry of each symbol
   uint32_t rank[kHufMaxBits + 2];
+};
+struct __align__(16) Smem : SmemCore {
   // one chunk of decoded sequences (phase A) for parallel execution (phase B):
   // phase A writes {ll, ml, off, -}; the scan rewrites {opre, ll, off, lpre}
   // (output / literal prefix of the chunk); rec[cnt] = {osum, 0, 0, lsum}
@@ -288,7 +293,7 @@ __device__ __forceinline__ void build_rle(uint32_t* table, uint32_t sym) {
 // ---- Huffman -------------------------------------------------------------------
 // Huffman tree description (RFC 8878 4.2.1).  Returns bytes consumed or -1;
 // sets max_bits.
-__device__ int32_t read_huf_tree(Smem& sm, const uint8_t* p, int64_t n, uint32_t& max_bits) {
+__device__ int32_t read_huf_tree(SmemCore& sm, const uint8_t* p, int64_t n, uint32_t& max_bits) {
   if (n < 1) return -1;
   const uint32_t hb = p[0];
   uint32_t nw;  // weights given explicitly (the last one is implied)
@@ -393,7 +398,7 @@ __device__ int32_t read_huf_tree(Smem& sm, const uint8_t* p, int64_t n, uint32_t
 }
 
 // Decode one Huffman stream of `cnt` literals into out (this lane only).
-__device__ bool huf_stream(const Smem& sm, uint32_t mb, const uint8_t* p, int64_t n, uint8_t* out,
+__device__ bool huf_stream(const SmemCore& sm, uint32_t mb, const uint8_t* p, int64_t n, uint8_t* out,
                            uint32_t cnt) {
   BitR br;
   if (!bitr_init(br, p, n)) return cnt == 0 && n == 0;
@@ -422,6 +427,36 @@ struct Out {
   uint64_t pos;        // bytes written
   uint64_t committed;  // bytes known visible to every lane
   uint64_t frame0;     // first output byte of the current frame
+};
+
+// Per segment block, written by the prologue (okv_zstd_pro_kernel) for the
+// sequence stage and the executor.
+enum : int32_t { kKindDone = 0, kKindSeq = 1, kKindSlow = 2 };
+enum : uint32_t { kFlagFcs = 1, kFlagCsum = 2, kFlagRle = 4 };
+constexpr uint32_t kTabWords = 1280;  // LL [0, 512), OF [512, 768), ML [768, 1280)
+struct ZBlk {
+  const uint8_t* stream;  // sequence bitstream
+  const uint8_t* lits;    // literal bytes (unused with kFlagRle)
+  uint64_t fcs;           // Frame_Content_Size (kFlagFcs)
+  uint32_t stream_len, nseq, lit_total, cap;
+  uint32_t csum;          // stored content checksum (kFlagCsum)
+  uint32_t flags;
+  uint32_t ll_al, of_al, ml_al, rle_byte;
+  int32_t kind;           // kKindDone / kKindSeq / kKindSlow
+  int32_t st;             // kOK / kErr / kCap of the stage that owns the block
+  uint32_t out_len;       // decompressed bytes
+  uint32_t lsum;          // literals consumed by the sequences (sequence stage)
+};
+
+// Prologue context of one block: per-block literal scratch and table slots.
+struct Pro {
+  uint8_t* lit_blk;   // literal scratch of this segment block (lit_cap bytes)
+  uint64_t lit_cap;
+  uint32_t* tabs;     // kTabWords table words of this block
+  ZBlk* zb;
+  bool deferrable;    // the compressed block being decoded may be deferred
+  uint64_t fcs;
+  uint32_t fcs_on, csum_on;
 };
 
 __device__ __forceinline__ void prof_add(const Out& o, int k, unsigned long long v) {
@@ -537,7 +572,7 @@ __device__ __forceinline__ uint32_t seqbits_read(SeqBits& b, uint32_t nb) {
 }
 
 // Table for one of LL / OF / ML from the symbol compression mode.
-__device__ int32_t seq_table(Smem& sm, uint32_t* table, uint32_t mode, const int16_t* def,
+__device__ int32_t seq_table(SmemCore& sm, uint32_t* table, uint32_t mode, const int16_t* def,
                              uint32_t def_al, uint32_t def_n, uint32_t max_sym, uint32_t max_al,
                              const uint8_t* p, int64_t n, bool& ok, uint32_t& al) {
   switch (mode) {
@@ -571,8 +606,9 @@ __device__ int32_t seq_table(Smem& sm, uint32_t* table, uint32_t mode, const int
 }
 
 // Decompress one compressed zstd block (RFC 8878 3.1.1.3) into the output.
-__device__ int32_t compressed_block(Smem& sm, FrameState& fs, Out& o, const uint8_t* p, int64_t n,
-                                    uint8_t* lit_buf) {
+template <bool PRO, class SM>
+__device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_t* p, int64_t n,
+                                    uint8_t* lit_buf, Pro* pro) {
   p = rflp(p);
   n = rfls64(n);
   o.pos = rfl64(o.pos);
@@ -638,6 +674,10 @@ __device__ int32_t compressed_block(Smem& sm, FrameState& fs, Out& o, const uint
     at += 1;
   } else {  // Compressed / Treeless
     if (at + csize > n) return kErr;
+    if constexpr (PRO) {
+      if (regen > pro->lit_cap) return kSlow;  // per-block scratch too small: general kernel
+      lit_buf = pro->lit_blk;
+    }
     const uint8_t* q = p + at;
     int64_t qn = csize;
     if (ltype == 2) {
@@ -714,6 +754,9 @@ __device__ int32_t compressed_block(Smem& sm, FrameState& fs, Out& o, const uint
     emit_lits(lit_left);
     return kOK;
   }
+  if constexpr (PRO) {
+    if (!pro->deferrable) return kSlow;
+  }
   if (at >= n) return kErr;
   const uint32_t modes = p[at++];
   if (modes & 3) return kErr;  // reserved bits
@@ -733,6 +776,29 @@ __device__ int32_t compressed_block(Smem& sm, FrameState& fs, Out& o, const uint
   if (used < 0) return kErr;
   at += used;
   if (((modes >> 2) & 3) != 3) seq_xbits(sm.ml, fs.ml_al, 2);
+  if constexpr (PRO) {
+    // hand the sequences to the lane-per-block stage: tables to HBM, setup to zb
+    const int lane = threadIdx.x & 63;
+    for (uint32_t u = lane; u < (1u << fs.ll_al); u += 64) pro->tabs[u] = sm.ll[u];
+    for (uint32_t u = lane; u < (1u << fs.of_al); u += 64) pro->tabs[512 + u] = sm.of[u];
+    for (uint32_t u = lane; u < (1u << fs.ml_al); u += 64) pro->tabs[768 + u] = sm.ml[u];
+    if (lane == 0) {
+      ZBlk& z = *pro->zb;
+      z.stream = p + at;
+      z.stream_len = uint32_t(n - at);
+      z.lits = rle ? nullptr : lits;
+      z.nseq = nseq;
+      z.lit_total = regen;
+      z.cap = uint32_t(min<uint64_t>(o.cap, 0x7fffffffu));
+      z.fcs = pro->fcs;
+      z.flags = (pro->fcs_on ? kFlagFcs : 0) | (pro->csum_on ? kFlagCsum : 0) | (rle ? kFlagRle : 0);
+      z.ll_al = fs.ll_al;
+      z.of_al = fs.of_al;
+      z.ml_al = fs.ml_al;
+      z.rle_byte = rle_byte;
+    }
+    return kDefer;
+  } else {
   at = rfls64(at);
   nseq = rfl(nseq);
   lit_left = rfl64(lit_left);
@@ -953,6 +1019,7 @@ __device__ int32_t compressed_block(Smem& sm, FrameState& fs, Out& o, const uint
   if (o.pos + lit_left > o.cap) return kCap;
   emit_lits(lit_left);
   return kOK;
+  }  // !PRO
 }
 
 // XXH64 of out[a, b) by lanes 0..3 (the four accumulators), result on every lane.
@@ -1010,9 +1077,11 @@ __device__ uint64_t xxh64_out(const uint8_t* base, uint64_t len) {
 }
 
 // Every frame of src[0, n) (zstd.NewReader + io.Copy semantics).
-__device__ int32_t decode_frames(Smem& sm, const uint8_t* src, int64_t n, Out& o,
-                                 uint8_t* lit_buf) {
+template <bool PRO, class SM>
+__device__ int32_t decode_frames(SM& sm, const uint8_t* src, int64_t n, Out& o, uint8_t* lit_buf,
+                                 Pro* pro) {
   int64_t at = 0;
+  bool first_frame = true;
   while (at < n) {
     if (n - at < 4) return kErr;
     const uint32_t magic = ld32z(src, at, n);
@@ -1054,6 +1123,7 @@ __device__ int32_t decode_frames(Smem& sm, const uint8_t* src, int64_t n, Out& o
     fs.huf_bits = 0;
     fs.ll_al = fs.of_al = fs.ml_al = 0;
     o.frame0 = o.pos;
+    bool first_block = true;
     for (;;) {  // blocks (3.1.1.2)
       if (n - at < 3) return kErr;
       const uint32_t bh = src[at] | (uint32_t(src[at + 1]) << 8) | (uint32_t(src[at + 2]) << 16);
@@ -1074,14 +1144,26 @@ __device__ int32_t decode_frames(Smem& sm, const uint8_t* src, int64_t n, Out& o
         at += 1;
       } else if (btype == 2) {  // Compressed_Block (libzstd: < 128 KiB)
         if (int64_t(bsize) > n - at || bsize >= kBlockMax) return kErr;
-        const int32_t r = compressed_block(sm, fs, o, src + at, bsize, lit_buf);
+        if constexpr (PRO) {
+          // deferrable: the input is exactly one frame holding this one block
+          pro->deferrable = first_frame && first_block && last &&
+                            at + int64_t(bsize) + (has_csum ? 4 : 0) == n;
+          pro->fcs = fcs;
+          pro->fcs_on = fcs_size != 0;
+          pro->csum_on = has_csum;
+          if (pro->deferrable && has_csum && (threadIdx.x & 63) == 0)
+            pro->zb->csum = ld32z(src, at + bsize, n);
+        }
+        const int32_t r = compressed_block<PRO>(sm, fs, o, src + at, bsize, lit_buf, pro);
         if (r != kOK) return r;
         at += bsize;
       } else {
         return kErr;  // reserved block type
       }
+      first_block = false;
       if (last) break;
     }
+    first_frame = false;
     if (fcs_size && o.pos - o.frame0 != fcs) return kErr;  // Frame_Content_Size check
     if (has_csum) {
       if (n - at < 4) return kErr;
@@ -1110,11 +1192,12 @@ __global__ __launch_bounds__(64) void okv_zstd_kernel(const uint8_t* __restrict_
                                                       int32_t* __restrict__ zstatus,
                                                       uint8_t* __restrict__ lit,
                                                       unsigned long long* __restrict__ prof,
-                                                      int stage_on) {
+                                                      const zst::ZBlk* __restrict__ zb) {
   __shared__ zst::Smem sm;
   uint8_t* lit_buf = lit + uint64_t(blockIdx.x) * zst::kBlockMax;
 
   for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    if (zb && zst::rfl(uint32_t(zb[b].kind)) != zst::kKindSlow) continue;
     const Desc d = descs[b];
     int32_t st = OKV_BLK_OK;
     zst::Out o;
@@ -1131,8 +1214,8 @@ __global__ __launch_bounds__(64) void okv_zstd_kernel(const uint8_t* __restrict_
       st = OKV_BLK_PANIC;  // rawBlockBytes[:CompressedSize] out of range (:321)
     } else {
       const uint8_t* src = seg + d.offset;
-      (void)stage_on;  // LDS staging of the frames measured no gain (refills hit L2)
-      const int32_t r = zst::decode_frames(sm, src, int64_t(d.compressed_size), o, lit_buf);
+      const int32_t r = zst::decode_frames<false>(sm, src, int64_t(d.compressed_size), o, lit_buf,
+                                                         nullptr);
       __syncthreads();
       st = r == zst::kOK ? OKV_BLK_OK : r == zst::kCap ? OKV_BLK_CAPACITY : OKV_BLK_ZSTD_ERROR;
     }
@@ -1146,6 +1229,630 @@ __global__ __launch_bounds__(64) void okv_zstd_kernel(const uint8_t* __restrict_
     }
     __builtin_amdgcn_s_waitcnt(0);
   }
+}
+
+// ---- stage 1: prologue, one wave per segment block -------------------------------
+// Frame / block headers, Huffman literals into the block's literal scratch, FSE
+// tables into HBM.  Raw / RLE / literals-only blocks finish here; a block whose
+// input is one frame holding one compressed block with sequences is deferred to
+// stages 2-3; anything else goes to okv_zstd_kernel (kKindSlow).
+__global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
+    const uint8_t* __restrict__ seg, uint64_t seg_bytes, const Desc* __restrict__ descs,
+    uint32_t nblk, const uint64_t* __restrict__ cap_off, uint8_t* __restrict__ dec,
+    uint64_t* __restrict__ dec_len, int32_t* __restrict__ zstatus, uint8_t* __restrict__ lits,
+    uint32_t* __restrict__ tabs, zst::ZBlk* __restrict__ zb) {
+  __shared__ zst::SmemCore sm;
+  const int lane = threadIdx.x & 63;
+  for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const Desc d = descs[b];
+    int32_t st = OKV_BLK_OK;
+    int32_t kind = zst::kKindDone;
+    zst::Out o;
+    o.prof = nullptr;
+    o.base = dec + cap_off[b];
+    o.cap = cap_off[b + 1] - cap_off[b];
+    o.pos = o.committed = o.frame0 = 0;
+    if (int64_t(d.offset) < 0 || d.offset >= seg_bytes) {
+      st = OKV_BLK_EOF;  // :303-313
+    } else if (seg_bytes - d.offset < d.block_size) {
+      st = OKV_BLK_SHORT;  // :314-316
+    } else if (d.compressed_size > d.block_size) {
+      st = OKV_BLK_PANIC;  // rawBlockBytes[:CompressedSize] out of range (:321)
+    } else {
+      zst::Pro pro;
+      pro.lit_blk = lits + cap_off[b];
+      pro.lit_cap = o.cap;
+      pro.tabs = tabs + uint64_t(b) * zst::kTabWords;
+      pro.zb = zb + b;
+      pro.deferrable = false;
+      pro.fcs = 0;
+      pro.fcs_on = pro.csum_on = 0;
+      const int32_t r = zst::decode_frames<true>(sm, seg + d.offset, int64_t(d.compressed_size), o,
+                                                 nullptr, &pro);
+      __syncthreads();
+      if (r == zst::kDefer) {
+        kind = zst::kKindSeq;
+      } else if (r == zst::kSlow) {
+        kind = zst::kKindSlow;
+      } else {
+        st = r == zst::kOK ? OKV_BLK_OK : r == zst::kCap ? OKV_BLK_CAPACITY : OKV_BLK_ZSTD_ERROR;
+      }
+    }
+    if (lane == 0) {
+      zb[b].kind = kind;
+      zb[b].st = zst::kOK;
+      if (kind == zst::kKindDone) {
+        zstatus[b] = st;
+        dec_len[b] = st == OKV_BLK_OK ? o.pos : 0;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+  }
+}
+
+// Exclusive scan of the deferred blocks' sequence counts -> seq_off[nblk + 1].
+__global__ __launch_bounds__(1024) void okv_zstd_seqoff_kernel(const zst::ZBlk* __restrict__ zb,
+                                                               uint32_t nblk,
+                                                               uint64_t* __restrict__ seq_off) {
+  __shared__ uint64_t sm[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t carry = 0;
+  for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint64_t v = (i < nblk && zb[i].kind == zst::kKindSeq) ? zb[i].nseq : 0;
+    const uint64_t inc = wave_incl_scan(v, lane);
+    if (lane == 63) sm[wave] = inc;
+    __syncthreads();
+    uint64_t before = 0, tot = 0;
+    for (int w = 0; w < 16; ++w) {
+      before += w < wave ? sm[w] : 0;
+      tot += sm[w];
+    }
+    if (i < nblk) seq_off[i] = carry + before + inc - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) seq_off[nblk] = carry;
+}
+
+namespace zst {
+// Per-lane backward bit reader over aligned dwords, two dwords prefetched, so a
+// lane's serial decode rarely waits on memory.  Bit positions are relative to
+// the aligned base ab; stream bytes outside [s0, s0 + n) read as 0.
+struct LaneBits {
+  const uint8_t* ab;
+  int32_t s0, n;
+  int32_t P;       // remaining bits, as ab-relative position
+  int32_t acc_lo;  // acc holds bits [acc_lo, acc_lo + 64)
+  uint64_t acc;
+  uint32_t nx0, nx1;  // raw dwords acc_lo / 32 - 1 and - 2 (masked when shifted in)
+  int32_t nd;         // dword index loaded into nx1 next
+};
+// Raw aligned dword d (clamped into the buffer): an unconditional load whose
+// value is only used when it is shifted in, so prefetches do not stall.
+__device__ __forceinline__ uint32_t lb_raw(const LaneBits& b, int32_t d) {
+  const int32_t lim = (b.s0 + b.n - 1) >> 2;
+  const int32_t dc = d < 0 ? 0 : (d > lim ? lim : d);
+  // a global (not flat) load: it counts in vmcnt only, so LDS waits do not drain it
+  return *(const __attribute__((address_space(1))) uint32_t*)(b.ab + 4 * dc);
+}
+// Bytes of dword d outside the stream [s0, s0 + n) read as 0.
+__device__ __forceinline__ uint32_t lb_fix(const LaneBits& b, uint32_t v, int32_t d) {
+  const int32_t lo = 4 * d;
+  if (d < 0 || lo >= b.s0 + b.n) return 0;
+  if (lo < b.s0) v &= 0xffffffffu << (8 * (b.s0 - lo));
+  const int32_t hi = b.s0 + b.n - lo;
+  if (hi < 4) v &= (1u << (8 * hi)) - 1;
+  return v;
+}
+__device__ __forceinline__ uint32_t lb_dw(const LaneBits& b, int32_t d) {
+  return lb_fix(b, lb_raw(b, d), d);
+}
+// Ensure k (<= 32) bits are in the container.
+__device__ __forceinline__ void lb_ensure(LaneBits& b, int32_t k) {
+  if (b.P - b.acc_lo < k) {
+    const int32_t d = (b.acc_lo >> 5) - 1;  // the dword held in nx0
+    b.acc = (b.acc << 32) | lb_fix(b, b.nx0, d);
+    b.acc_lo -= 32;
+    b.nx0 = b.nx1;
+    b.nx1 = lb_raw(b, b.nd);
+    --b.nd;
+  }
+}
+__device__ __forceinline__ uint32_t lb_take(LaneBits& b, uint32_t k) {
+  b.P -= int32_t(k);
+  return uint32_t(b.acc >> uint32_t(b.P - b.acc_lo)) & uint32_t((uint64_t(1) << k) - 1);
+}
+
+// 128-bit window reader for the sequence stage.  The window holds aligned
+// dwords [wd, wd + 4); the three dwords below it are loaded unconditionally at
+// the end of every sequence and only read at the end of the next one, after the
+// next table gathers have drained the load queue -- so the stream never stalls
+// the lane chain.  One sequence reads <= 89 bits; the window always holds > 96.
+struct WinBits {
+  LaneBits f;             // ab / s0 / n (masking), P
+  int32_t wd;
+  uint64_t lo, hi;        // dwords wd+1:wd, wd+3:wd+2 (masked)
+  uint32_t l0, l1, l2;    // raw dwords wd-1, wd-2, wd-3 (in flight)
+};
+__device__ __forceinline__ void wb_issue(WinBits& w) {
+  w.l0 = lb_raw(w.f, w.wd - 1);
+  w.l1 = lb_raw(w.f, w.wd - 2);
+  w.l2 = lb_raw(w.f, w.wd - 3);
+}
+__device__ __forceinline__ uint32_t wb_take(WinBits& w, uint32_t k) {
+  w.f.P -= int32_t(k);
+  const uint32_t pos = uint32_t(w.f.P - 32 * w.wd);  // 0 .. 128 - k
+  uint64_t v;
+  if (pos >= 64) {
+    v = w.hi >> (pos - 64);
+  } else {
+    v = w.lo >> pos;
+    if (pos) v |= w.hi << (64 - pos);
+  }
+  return uint32_t(v) & uint32_t((uint64_t(1) << k) - 1);
+}
+// Slide the window down so its top dword holds bit P - 1; by 0..3 dwords.
+__device__ __forceinline__ void wb_slide(WinBits& w) {
+  const int32_t dtop = ((w.f.P + 31) >> 5) - 1;
+  int32_t sft = w.wd + 3 - dtop;
+  sft = sft < 0 ? 0 : (sft > 3 ? 3 : sft);
+  const uint32_t c0 = lb_fix(w.f, w.l2, w.wd - 3), c1 = lb_fix(w.f, w.l1, w.wd - 2),
+                 c2 = lb_fix(w.f, w.l0, w.wd - 1);
+  const uint32_t w0 = uint32_t(w.lo), w1 = uint32_t(w.lo >> 32), w2 = uint32_t(w.hi),
+                 w3 = uint32_t(w.hi >> 32);
+  // C = [c0 c1 c2 w0 w1 w2 w3]; new window k = C[k + 3 - sft]
+  const uint32_t n0 = sft == 0 ? w0 : sft == 1 ? c2 : sft == 2 ? c1 : c0;
+  const uint32_t n1 = sft == 0 ? w1 : sft == 1 ? w0 : sft == 2 ? c2 : c1;
+  const uint32_t n2 = sft == 0 ? w2 : sft == 1 ? w1 : sft == 2 ? w0 : c2;
+  const uint32_t n3 = sft == 0 ? w3 : sft == 1 ? w2 : sft == 2 ? w1 : w0;
+  w.lo = uint64_t(n0) | (uint64_t(n1) << 32);
+  w.hi = uint64_t(n2) | (uint64_t(n3) << 32);
+  w.wd -= sft;
+  wb_issue(w);
+}
+
+// Packed sequence: ll (18 bits) | ml (18 bits) << 18 | offset (28 bits) << 36;
+// the executor re-derives nothing, so the checks of stage 2 bound every field.
+__device__ __forceinline__ uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t off) {
+  return uint64_t(ll) | (uint64_t(ml) << 18) | (uint64_t(off) << 36);
+}
+}  // namespace zst
+
+// ---- stage 2: sequences, one lane per segment block --------------------------------
+// RFC 8878 3.1.1.3.2 / libzstd ZSTD_decodeSequence for every deferred block at
+// once: each lane owns a block's FSE states and bitstream (tables gathered from
+// HBM), checks each sequence exactly as the general kernel does and writes it
+// packed.  64 blocks advance per wave instruction.
+__global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict__ zb, uint32_t nblk,
+                                                          const uint32_t* __restrict__ tabs,
+                                                          const uint64_t* __restrict__ seq_off,
+                                                          uint64_t* __restrict__ seqs) {
+  // Tables stay in HBM / L2: 64 blocks' tables (320 KiB) do not fit LDS, and
+  // 16 blocks per workgroup with LDS tables measured slower at C5 scale (half
+  // the blocks in flight; the lane chain is instruction-bound, not table-bound).
+  __shared__ uint32_t llb[36], mlb[53];
+  const int lane = threadIdx.x & 63;
+  if (lane < 36) llb[lane] = zst::LL_BASE[lane];
+  if (lane < 53) mlb[lane] = zst::ML_BASE[lane];
+  __syncthreads();
+  const uint32_t b = blockIdx.x * 64 + lane;
+  if (b >= nblk || zb[b].kind != zst::kKindSeq) return;
+  const zst::ZBlk z = zb[b];
+  const uint32_t* T = tabs + uint64_t(b) * zst::kTabWords;
+  uint64_t* S = seqs + seq_off[b];
+  int32_t st = zst::kOK;
+  uint32_t lsum = 0, osum = 0;
+  zst::WinBits br;
+  {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(z.stream);
+    br.f.ab = reinterpret_cast<const uint8_t*>(a & ~uintptr_t(3));
+    br.f.s0 = int32_t(a & 3);
+    br.f.n = int32_t(z.stream_len);
+  }
+  const uint32_t last = br.f.n > 0 ? z.stream[br.f.n - 1] : 0;
+  if (last == 0) {
+    st = zst::kErr;  // no end marker
+  } else {
+    br.f.P = 8 * br.f.s0 + (br.f.n - 1) * 8 + (31 - __builtin_clz(last));
+    const int32_t dtop = (br.f.s0 + br.f.n - 1) >> 2;
+    br.wd = dtop - 3;
+    br.lo = uint64_t(zst::lb_dw(br.f, dtop - 3)) | (uint64_t(zst::lb_dw(br.f, dtop - 2)) << 32);
+    br.hi = uint64_t(zst::lb_dw(br.f, dtop - 1)) | (uint64_t(zst::lb_dw(br.f, dtop)) << 32);
+    zst::wb_issue(br);
+    uint32_t sll = zst::wb_take(br, z.ll_al);
+    uint32_t sof = zst::wb_take(br, z.of_al);
+    uint32_t sml = zst::wb_take(br, z.ml_al);
+    zst::wb_slide(br);
+    uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
+    const int32_t P0 = 8 * br.f.s0;
+    for (uint32_t i = 0; i < z.nseq; ++i) {
+      if (br.f.P < P0) {  // libzstd: the stream overflowed before this sequence
+        st = zst::kErr;
+        break;
+      }
+      const uint32_t ell = T[sll], eof = T[512 + sof], eml = T[768 + sml];
+      const uint32_t ofs = zst::fse_sym(eof);
+      const uint32_t ofv = (1u << ofs) + zst::wb_take(br, ofs);
+      const uint32_t mlx = zst::wb_take(br, zst::fse_xb(eml));
+      const uint32_t llx = zst::wb_take(br, zst::fse_xb(ell));
+      const uint32_t ml = mlb[zst::fse_sym(eml)] + mlx;
+      const uint32_t ll = llb[zst::fse_sym(ell)] + llx;
+      uint32_t off;
+      if (ofv > 3) {
+        off = ofv - 3;
+        rep2 = rep1;
+        rep1 = rep0;
+        rep0 = off;
+      } else {
+        const uint32_t idx = ofv - 1 + (ll == 0 ? 1 : 0);  // 0..3
+        if (idx == 0) {
+          off = rep0;
+        } else {
+          uint32_t t = idx == 3 ? rep0 - 1 : (idx == 1 ? rep1 : rep2);
+          t += t == 0;  // libzstd: offset 0 is corrupt input, forced to 1
+          if (idx != 1) rep2 = rep1;
+          rep1 = rep0;
+          rep0 = t;
+          off = t;
+        }
+      }
+      if (i + 1 < z.nseq) {  // state updates: literals length, match length, offset
+        sll = zst::fse_base(ell) + zst::wb_take(br, zst::fse_nb(ell));
+        sml = zst::fse_base(eml) + zst::wb_take(br, zst::fse_nb(eml));
+        sof = zst::fse_base(eof) + zst::wb_take(br, zst::fse_nb(eof));
+      }
+      zst::wb_slide(br);
+      // execution checks (3.1.1.4), in the general kernel's order
+      if (uint64_t(lsum) + ll > z.lit_total) {
+        st = zst::kErr;
+        break;
+      }
+      const uint64_t mstart = uint64_t(osum) + ll;
+      if (mstart + ml > z.cap) {
+        st = zst::kCap;
+        break;
+      }
+      if (off > mstart) {  // before the frame start (no dictionary)
+        st = zst::kErr;
+        break;
+      }
+      S[i] = zst::seq_pack(ll, ml, off);
+      lsum += ll;
+      osum += ll + ml;
+    }
+    if (st == zst::kOK && br.f.P > P0) st = zst::kErr;  // unread bits
+    if (st == zst::kOK && uint64_t(osum) + (z.lit_total - lsum) > z.cap) st = zst::kCap;
+    if (st == zst::kOK && (z.flags & zst::kFlagFcs) && uint64_t(osum) + (z.lit_total - lsum) != z.fcs)
+      st = zst::kErr;  // Frame_Content_Size check
+  }
+  zb[b].st = st;
+  zb[b].lsum = lsum;
+  zb[b].out_len = osum + (z.lit_total - lsum);
+}
+
+// ---- stage 3: execution, one wave per segment block --------------------------------
+// Sequences in chunks of <= 256 sequences / 4 KiB of output.  For each output
+// byte of a chunk the wave records its source -- a literal, output before the
+// chunk, or an earlier byte of the chunk -- then resolves in-chunk chains by
+// pointer jumping in LDS (sources always lie before the byte, so there are no
+// cycles), and gathers every byte independently.
+// Diagnostics (OKV_ZSTD_PROF): per-phase cycles accumulated in registers and
+// added to this workgroup's own slot, so profiling adds no shared atomics.
+#define PMARK(k)                  \
+  do {                            \
+    if (prof) {                   \
+      const long long tq = clock64(); \
+      pacc[(k)] += tq - tp0;      \
+      tp0 = tq;                   \
+    }                             \
+  } while (0)
+namespace zst {
+constexpr uint32_t kTerm = 0x80000000u, kLit = 0x40000000u, kIdx = 0x3fffffffu;
+}
+
+__global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
+    const zst::ZBlk* __restrict__ zb, uint32_t nblk, const uint64_t* __restrict__ seq_off,
+    const uint64_t* __restrict__ seqs, const uint64_t* __restrict__ cap_off,
+    uint8_t* __restrict__ dec, uint64_t* __restrict__ dec_len, int32_t* __restrict__ zstatus,
+    unsigned long long* __restrict__ prof) {
+  __shared__ uint4 rec[zst::kSeqChunk + 1];
+  __shared__ uint32_t srcx[zst::kChunkOut];
+  __shared__ uint8_t map[zst::kChunkOut];
+  const int lane = threadIdx.x & 63;
+  unsigned long long pacc[10] = {};
+  for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const int32_t kind = zst::rfl(uint32_t(zb[b].kind));
+    if (kind != zst::kKindSeq) continue;
+    const int32_t st0 = zst::rfl(uint32_t(zb[b].st));
+    if (st0 != zst::kOK) {
+      if (lane == 0) {
+        zstatus[b] = st0 == zst::kCap ? OKV_BLK_CAPACITY : OKV_BLK_ZSTD_ERROR;
+        dec_len[b] = 0;
+      }
+      continue;
+    }
+    const uint32_t nseq = zst::rfl(zb[b].nseq), lit_total = zst::rfl(zb[b].lit_total);
+    const uint32_t flags = zst::rfl(zb[b].flags);
+    const bool rle = flags & zst::kFlagRle;
+    const uint8_t rle_byte = uint8_t(zst::rfl(zb[b].rle_byte));
+    const uint8_t* lits = zst::rflp(zb[b].lits);
+    uint8_t* out = dec + zst::rfl64(cap_off[b]);
+    const uint64_t* S = seqs + zst::rfl64(seq_off[b]);
+    uint32_t O = 0, lp = 0;
+    for (uint32_t i0 = 0; i0 < nseq;) {
+      long long tp0 = prof ? clock64() : 0;
+      const uint32_t nrem = nseq - i0;
+      // up to 256 sequences: lane holds sequences 4 lane .. 4 lane + 3
+      uint32_t ll[4], ml[4], of[4];
+      uint32_t lt = 0, ot = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t k = 4 * lane + u;
+        const uint64_t vr = S[i0 + (k < nrem ? k : 0)];
+        const uint64_t v = k < nrem ? vr : 0;
+        ll[u] = uint32_t(v) & 0x3ffff;
+        ml[u] = uint32_t(v >> 18) & 0x3ffff;
+        of[u] = uint32_t(v >> 36);
+        lt += ll[u];
+        ot += ll[u] + ml[u];
+      }
+      uint32_t lpx = wave_incl_scan32(lt, lane) - lt, opx = wave_incl_scan32(ot, lane) - ot;
+      uint32_t fit = 0;  // sequences of this lane that end within the byte map
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t k = 4 * lane + u;
+        rec[k] = make_uint4(opx, ll[u], of[u], lpx);
+        lpx += ll[u];
+        opx += ll[u] + ml[u];
+        fit += (k < nrem && opx <= zst::kChunkOut) ? 1u : 0u;
+      }
+      if (lane == 63) rec[256] = make_uint4(opx, 0, 0, lpx);
+      for (int d = 32; d; d >>= 1) fit += __shfl_xor(fit, d, 64);
+      const uint32_t cnt = fit ? fit : 1;  // a single long sequence when none fits
+      __syncthreads();
+      const uint32_t osum = zst::rfl(rec[cnt].x), lsum = zst::rfl(rec[cnt].w);
+      PMARK(0);
+      if (fit) {
+        // byte -> sequence map: markers, then a running max
+        uint4* m4 = reinterpret_cast<uint4*>(map);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) m4[4 * lane + u] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        for (uint32_t k = lane + 1; k < cnt; k += 64) map[rec[k].x] = uint8_t(k);
+        __syncthreads();
+        uint4 v[4];
+        uint32_t mx = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[u] = m4[4 * lane + u];
+          const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) mx = max(mx, (w4[q] >> (8 * t)) & 0xffu);
+        }
+        uint32_t run = mx;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(run, d, 64);
+          if (lane >= d) run = max(run, y);
+        }
+        run = __shfl_up(run, 1, 64);
+        if (lane == 0) run = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            uint32_t outw = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              run = max(run, (w4[q] >> (8 * t)) & 0xffu);
+              outw |= run << (8 * t);
+            }
+            w4[q] = outw;
+          }
+          m4[4 * lane + u] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+        __syncthreads();
+        PMARK(1);
+        // each byte's immediate source (eight bytes per lane per step: the map and
+        // record reads of a step are all issued before any is used)
+        for (uint32_t x0 = lane; x0 < osum; x0 += 64 * 8) {
+          uint32_t kk[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const uint32_t x = x0 + 64 * u;
+            kk[u] = x < osum ? map[x] : 0;
+          }
+          uint4 R[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) R[u] = rec[kk[u]];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const uint32_t x = x0 + 64 * u;
+            const uint32_t in = x - R[u].x;
+            uint32_t sv;
+            if (in < R[u].y) {
+              sv = zst::kTerm | zst::kLit | (lp + R[u].w + in);
+            } else {
+              const uint32_t t = in - R[u].y, off = R[u].z;
+              const uint32_t mo = t < off ? t : t % off;
+              const int32_t sx = int32_t(R[u].x + R[u].y + mo) - int32_t(off);
+              sv = sx < 0 ? (zst::kTerm | uint32_t(int32_t(O) + sx)) : uint32_t(sx);
+            }
+            if (x < osum) srcx[x] = sv;
+          }
+        }
+        __syncthreads();
+        PMARK(2);
+        uint32_t rounds = 0;
+        // pointer jumping until every byte names a terminal source; a step reads
+        // eight entries, then their targets, then writes (in place: any value
+        // read is an ancestor or a terminal, and sources lie before the byte)
+        for (;;) {
+          bool more = false;
+          for (uint32_t x0 = lane; x0 < osum; x0 += 64 * 8) {
+            uint32_t sv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const uint32_t x = x0 + 64 * u;
+              sv[u] = x < osum ? srcx[x] : zst::kTerm;
+            }
+            uint32_t nv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) nv[u] = (sv[u] & zst::kTerm) ? sv[u] : srcx[sv[u]];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const uint32_t x = x0 + 64 * u;
+              if (!(sv[u] & zst::kTerm)) {
+                srcx[x] = nv[u];
+                more |= !(nv[u] & zst::kTerm);
+              }
+            }
+          }
+          ++rounds;
+          if (!__any(more)) break;
+        }
+        __syncthreads();
+        PMARK(3);
+        pacc[8] += rounds;
+        // gather: lanes own aligned output dwords (four per lane per step, 16
+        // byte loads in flight, one dword store each).  A head byte before O is
+        // re-read from the previous chunk's output; tail bytes past the chunk
+        // are written as 0 and overwritten by the next chunk the same way.
+        const uint32_t g0 = O >> 2, g1 = (O + osum + 3) >> 2;
+        for (uint32_t gb = g0 + lane; gb < g1; gb += 64 * 4) {
+          const uint8_t* ptr[16];
+          uint32_t spec[16];  // 0 load, 1 RLE literal, 2 zero
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const uint32_t g = gb + 64 * (u >> 2);
+            const uint32_t a = 4 * g + (u & 3);
+            const uint32_t x = a - O;
+            const bool in = g < g1 && a >= O && x < osum;
+            const uint32_t sv = in ? srcx[x] : 0u;
+            const uint32_t idx = sv & zst::kIdx;
+            const bool lit = in && (sv & zst::kLit);
+            spec[u] = (g >= g1 || (a >= O && !in)) ? 2u : ((lit && rle) ? 1u : 0u);
+            ptr[u] = spec[u] ? out : (!in ? out + a : (lit ? lits + idx : out + idx));
+          }
+          uint32_t bv[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) bv[u] = *ptr[u];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t g = gb + 64 * q;
+            uint32_t w = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int u = 4 * q + j;
+              const uint32_t v = spec[u] == 2 ? 0u : spec[u] == 1 ? rle_byte : (bv[u] & 0xffu);
+              w |= v << (8 * j);
+            }
+            if (g < g1) reinterpret_cast<uint32_t*>(out)[g] = w;
+          }
+        }
+      } else {
+        // one sequence longer than the map: every match byte lands on this
+        // sequence's literals or on output before it; stored as aligned dwords
+        const uint4 R = rec[0];
+        const uint32_t g0 = O >> 2, g1 = (O + osum + 3) >> 2;
+        for (uint32_t gb = g0 + lane; gb < g1; gb += 64 * 4) {
+          const uint8_t* ptr[16];
+          uint32_t spec[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const uint32_t g = gb + 64 * (u >> 2);
+            const uint32_t a = 4 * g + (u & 3);
+            const uint32_t x = a - O;
+            const bool in = g < g1 && a >= O && x < osum;
+            int32_t sx;  // literal index (>= 0) of this sequence, or output offset from O
+            if (x < R.y) {
+              sx = int32_t(x);
+            } else {
+              const uint32_t t = x - R.y, off = R.z;
+              const uint32_t mo = t < off ? t : t % off;
+              sx = int32_t(R.y + mo) - int32_t(off);
+            }
+            spec[u] = (g >= g1 || (a >= O && !in)) ? 2u : ((in && sx >= 0 && rle) ? 1u : 0u);
+            ptr[u] = spec[u] ? out
+                             : (!in ? out + a
+                                    : (sx >= 0 ? lits + lp + uint32_t(sx) : out + (int32_t(O) + sx)));
+          }
+          uint32_t bv[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) bv[u] = *ptr[u];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t g = gb + 64 * q;
+            uint32_t w = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int u = 4 * q + j;
+              const uint32_t v = spec[u] == 2 ? 0u : spec[u] == 1 ? rle_byte : (bv[u] & 0xffu);
+              w |= v << (8 * j);
+            }
+            if (g < g1) reinterpret_cast<uint32_t*>(out)[g] = w;
+          }
+        }
+      }
+      PMARK(4);
+      __builtin_amdgcn_s_waitcnt(0);  // this chunk's stores visible to the next chunk's loads
+      __threadfence_block();
+      __syncthreads();
+      PMARK(5);
+      pacc[9] += 1;
+      O += osum;
+      lp += lsum;
+      i0 += cnt;
+    }
+    // literals after the last sequence
+    {
+      const uint32_t tl = lit_total - lp;
+      const uint32_t g0 = O >> 2, g1 = (O + tl + 3) >> 2;
+      for (uint32_t gb = g0 + lane; gb < g1; gb += 64 * 4) {
+        uint32_t bv[16];
+        uint32_t spec[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const uint32_t g = gb + 64 * (u >> 2);
+          const uint32_t a = 4 * g + (u & 3);
+          const bool in = g < g1 && a >= O && a - O < tl;
+          spec[u] = (g >= g1 || (a >= O && !in)) ? 2u : ((in && rle) ? 1u : 0u);
+          const uint8_t* ptr = spec[u] ? out : (!in ? out + a : lits + lp + (a - O));
+          bv[u] = *ptr;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t g = gb + 64 * q;
+          uint32_t w = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int u = 4 * q + j;
+            const uint32_t v = spec[u] == 2 ? 0u : spec[u] == 1 ? rle_byte : (bv[u] & 0xffu);
+            w |= v << (8 * j);
+          }
+          if (g < g1) reinterpret_cast<uint32_t*>(out)[g] = w;
+        }
+      }
+      O += tl;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __threadfence_block();
+    int32_t st = OKV_BLK_OK;
+    if (flags & zst::kFlagCsum) {
+      const uint64_t h = zst::xxh64_out(out, O);
+      if (uint32_t(h) != zst::rfl(zb[b].csum)) st = OKV_BLK_ZSTD_ERROR;
+    }
+    if (lane == 0) {
+      zstatus[b] = st;
+      dec_len[b] = st == OKV_BLK_OK ? O : 0;
+    }
+  }
+  if (prof && lane == 0)
+    for (int k = 0; k < 10; ++k) prof[blockIdx.x * 16 + k] = pacc[k];
 }
 
 // Exclusive scan of per-block decompressed capacities (round16(OriginalSize)).
@@ -1189,29 +1896,95 @@ __global__ void okv_zstd_desc_kernel(const Desc* __restrict__ descs, uint32_t nb
   out[b] = d;
 }
 
-void launch_zstd(hipStream_t s, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
-                 uint32_t nblk, const uint64_t* cap_off, uint8_t* dec, uint64_t* dec_len,
-                 int32_t* zstatus, uint8_t* lit, uint32_t grid) {
-  // OKV_ZSTD_PROF=1: per-phase clock64 totals printed to stderr (diagnostics only)
-  static unsigned long long* prof = nullptr;
-  const bool want = getenv("OKV_ZSTD_PROF") != nullptr;
-  if (want && !prof) (void)hipMalloc(&prof, 16 * sizeof(unsigned long long));
-  if (want) (void)hipMemsetAsync(prof, 0, 16 * sizeof(unsigned long long), s);
-  hipLaunchKernelGGL(okv_zstd_kernel, dim3(grid), dim3(64), 0, s, seg, seg_bytes, descs, nblk,
-                     cap_off, dec, dec_len, zstatus, lit, want ? prof : nullptr,
-                     getenv("OKV_ZSTD_STAGE") ? atoi(getenv("OKV_ZSTD_STAGE")) : 1);
-  if (want) {
-    unsigned long long h[16];
-    (void)hipMemcpyAsync(h, prof, sizeof(h), hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
-    fprintf(stderr,
-            "[zstd prof] blocks %llu cycles/block: total %.0f literals %.0f sequences %.0f "
-            "(phase A %.0f, phase B %.0f of which resolve %.0f) | seqs/block %.0f commits/block "
-            "%.0f hops/block %.0f\n",
-            h[7], double(h[3]) / h[7], double(h[0]) / h[7], double(h[1]) / h[7],
-            double(h[2]) / h[7], double(h[6]) / h[7], double(h[8]) / h[7], double(h[4]) / h[7],
-            double(h[5]) / h[7], double(h[9]) / h[7]);
+// Decompress every block into dec + cap_off[b] (capacities already scanned;
+// total = cap_off[nblk]).  Stages: prologue -> sequence offsets -> sequences ->
+// executor -> general kernel for the blocks the prologue handed over.
+// OKV_ZSTD_GENERAL=1 sends every block through the general kernel (A/B);
+// OKV_ZSTD_PROF=1 prints per-stage milliseconds to stderr (diagnostics only).
+int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
+             uint32_t nblk, uint64_t total) {
+  hipStream_t s = ctx->stream;
+  int rc;
+  const bool general = getenv("OKV_ZSTD_GENERAL") != nullptr;
+  const bool prof = getenv("OKV_ZSTD_PROF") != nullptr;
+  hipEvent_t ev[6] = {};
+  if (prof)
+    for (auto& e : ev) (void)hipEventCreate(&e);
+  if (prof) (void)hipEventRecord(ev[0], s);
+  zst::ZBlk* zb = nullptr;
+  static unsigned long long* eprof_buf = nullptr;
+  unsigned long long* eprof = nullptr;
+  if (prof) {
+    if (!eprof_buf) (void)hipMalloc(&eprof_buf, 16 * 8 * 4096);
+    eprof = eprof_buf;
+    (void)hipMemsetAsync(eprof, 0, 16 * 8 * 4096, s);
   }
+  if (!general) {
+    if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_zb), &ctx->z_cap_zb,
+                   size_t(nblk) * sizeof(zst::ZBlk))))
+      return rc;
+    if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_tabs), &ctx->z_cap_tabs,
+                   size_t(nblk) * zst::kTabWords * 4)))
+      return rc;
+    if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_blit), &ctx->z_cap_blit, total + 64)))
+      return rc;
+    if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_seq_off), &ctx->z_cap_seq_off,
+                   (size_t(nblk) + 1) * 8)))
+      return rc;
+    zb = reinterpret_cast<zst::ZBlk*>(ctx->z_zb);
+    hipLaunchKernelGGL(okv_zstd_pro_kernel, dim3(std::min<uint32_t>(nblk, 4096)), dim3(64), 0, s,
+                       seg, seg_bytes, descs, nblk, ctx->z_cap_off, ctx->z_dec, ctx->z_dec_len,
+                       ctx->z_status, ctx->z_blit, ctx->z_tabs, zb);
+    hipLaunchKernelGGL(okv_zstd_seqoff_kernel, dim3(1), dim3(1024), 0, s, zb, nblk,
+                       ctx->z_seq_off);
+    uint64_t nseq_total = 0;
+    OKV_HIP(hipMemcpyAsync(&nseq_total, ctx->z_seq_off + nblk, 8, hipMemcpyDeviceToHost, s));
+    OKV_HIP(hipStreamSynchronize(s));
+    if (prof) (void)hipEventRecord(ev[1], s);
+    if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_seqs), &ctx->z_cap_seqs,
+                   nseq_total * 8 + 64)))
+      return rc;
+    hipLaunchKernelGGL(okv_zstd_seq_kernel, dim3((nblk + 63) / 64), dim3(64), 0, s, zb, nblk,
+                       ctx->z_tabs, ctx->z_seq_off, ctx->z_seqs);
+    if (prof) (void)hipEventRecord(ev[2], s);
+    const uint32_t egrid = std::min<uint32_t>(
+        4096, getenv("OKV_ZSTD_EXEC_GRID") ? atoi(getenv("OKV_ZSTD_EXEC_GRID")) : 1536);
+    hipLaunchKernelGGL(okv_zstd_exec_kernel, dim3(std::min<uint32_t>(nblk, egrid)), dim3(64), 0, s,
+                       zb, nblk, ctx->z_seq_off, ctx->z_seqs, ctx->z_cap_off, ctx->z_dec,
+                       ctx->z_dec_len, ctx->z_status, eprof);
+  }
+  if (prof) (void)hipEventRecord(ev[3], s);
+  const uint32_t grid = std::min<uint32_t>(nblk, 2048);
+  if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_lit), &ctx->z_cap_lit,
+                 size_t(grid) * kZstdLitBytes)))
+    return rc;
+  hipLaunchKernelGGL(okv_zstd_kernel, dim3(grid), dim3(64), 0, s, seg, seg_bytes, descs, nblk,
+                     ctx->z_cap_off, ctx->z_dec, ctx->z_dec_len, ctx->z_status, ctx->z_lit,
+                     nullptr, zb);
+  OKV_HIP(hipGetLastError());
+  if (prof) {
+    (void)hipEventRecord(ev[4], s);
+    (void)hipStreamSynchronize(s);
+    float t[4] = {};
+    for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&t[k], ev[k], ev[k + 1]);
+    fprintf(stderr,
+            "[zstd prof] %u blocks: prologue+seqoff %.3f ms, sequences %.3f ms, executor %.3f ms, "
+            "general %.3f ms\n",
+            nblk, t[0], t[1], t[2], t[3]);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    static unsigned long long hs[16 * 4096];
+    (void)hipMemcpy(hs, eprof, sizeof(hs), hipMemcpyDeviceToHost);
+    unsigned long long h[16] = {};
+    for (int w = 0; w < 4096; ++w)
+      for (int k = 0; k < 16; ++k) h[k] += hs[w * 16 + k];
+    const double c = h[9] ? double(h[9]) : 1.0;
+    fprintf(stderr,
+            "[zstd exec] chunks %llu, cycles/chunk: load+scan %.0f map %.0f init %.0f jump %.0f "
+            "(rounds %.2f) gather %.0f commit %.0f\n",
+            h[9], h[0] / c, h[1] / c, h[2] / c, h[3] / c, h[8] / c, h[4] / c, h[5] / c);
+  }
+  return OKV_OK;
 }
 void launch_zstd_cap(hipStream_t s, const Desc* descs, uint32_t nblk, uint64_t* cap_off) {
   hipLaunchKernelGGL(okv_zstd_cap_kernel, dim3(1), dim3(1024), 0, s, descs, nblk, cap_off);

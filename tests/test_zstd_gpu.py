@@ -14,6 +14,17 @@ from tests import zstd_cases as ZC
 
 pytestmark = pytest.mark.gpu
 
+@pytest.fixture(params=["staged", "general"], autouse=True)
+def zmode(request, monkeypatch):
+    """Every case through both device paths: the staged decoder (prologue ->
+    lane-per-block sequences -> parallel executor) and the general kernel."""
+    if request.param == "general":
+        monkeypatch.setenv("OKV_ZSTD_GENERAL", "1")
+    else:
+        monkeypatch.delenv("OKV_ZSTD_GENERAL", raising=False)
+    return request.param
+
+
 SOA = ("row_start", "key_off", "key_len", "val_off", "val_len", "key_base", "val_base")
 
 
@@ -69,3 +80,55 @@ def test_zstd_segment_through_product_reader(decoder):
     got = pr.GetRange(rows[100][0], rows[900][0])
     want = orr.GetRange(rows[100][0], rows[900][0])
     assert [(r.Key, r.Value) for r in got] == [(r.Key, r.Value) for r in want]
+
+
+def test_zstd_bench_shape_blocks(decoder):
+    """64 KiB text blocks as bench.py --config cz builds them (libzstd level 3)."""
+    from tools.zstd_gen import text_zstd_segment
+    seg, descs, _ = text_zstd_segment(24, 9, 3)
+    got = _check(decoder, seg.tobytes(), [tuple(int(x) for x in d) for d in descs])
+    assert int(got.status.max()) == 0
+
+
+def test_zstd_long_runs_and_rle_literals(decoder):
+    """Matches far longer than the executor's 4 KiB byte map, offset-1 runs,
+    and blocks whose literals are RLE."""
+    rows = []
+    for i in range(120):
+        v = bytes([i % 7]) * (4500 + 37 * i) if i % 3 else (b"ab" * 2100 + bytes(range(i % 50)))
+        rows.append((b"r%06d" % i, v))
+    seg, _, _ = ZC.Z.zstd_segment(rows, 57344, 65536, level=3)
+    from oracle import pyoracle as P2
+    md = P2.bytes_to_metadata(ZC._meta_of(seg))
+    got = _check(decoder, seg, [st.desc() for st in md.entries])
+    assert int(got.status.max()) == 0
+
+
+def test_zstd_staged_equals_general_under_corruption(decoder, zmode, monkeypatch):
+    """Byte flips in the sequence sections: the staged path and the general
+    kernel apply the same checks, so statuses and bytes agree block for block;
+    blocks the oracle decodes must match it."""
+    if zmode == "general":
+        pytest.skip("compares the two paths itself")
+    import random
+    from tools.zstd_gen import text_zstd_segment
+    seg, descs, _ = text_zstd_segment(48, 13, 3)
+    b = bytearray(seg.tobytes())
+    rng = random.Random(5)
+    for i, d in enumerate(descs):
+        off, csz = int(d[0]), int(d[3])
+        for _ in range(1 + i % 3):
+            b[off + csz - 1 - rng.randrange(min(csz - 20, 3000))] ^= 1 << rng.randrange(8)
+    dl = [tuple(int(x) for x in d) for d in descs]
+    d = np.array(dl, np.uint64).reshape(-1, 4)
+    staged = decoder.decode(np.frombuffer(bytes(b), np.uint8), d, P.COMP_ZSTD)
+    monkeypatch.setenv("OKV_ZSTD_GENERAL", "1")
+    general = decoder.decode(np.frombuffer(bytes(b), np.uint8), d, P.COMP_ZSTD)
+    assert np.array_equal(staged.status, general.status)
+    for k in SOA:
+        assert np.array_equal(getattr(staged, k), getattr(general, k)), k
+    assert staged.key_arena.tobytes() == general.key_arena.tobytes()
+    assert staged.val_arena.tobytes() == general.val_arena.tobytes()
+    ref = CO.decode_soa(bytes(b), CO.descs_array(dl), P.COMP_ZSTD, False)
+    ok = ref["status"] == 0
+    assert np.array_equal(staged.status[ok], ref["status"][ok])

@@ -11,7 +11,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 seg, descs, orig = text_zstd_segment(n, 5)
 dec = okv.Decoder(0)
 for stage in ("1",):
-    os.environ["OKV_ZSTD_STAGE"] = stage
+    os.environ.pop("OKV_ZSTD_GENERAL", None)
     os.environ.pop("OKV_ZSTD_PROF", None)
     dec.profile(True)
     got = dec.decode(seg, descs, compression=okv.sst.COMP_ZSTD)
@@ -20,7 +20,7 @@ for stage in ("1",):
     print(f"stage={stage}: zstd+count {ms['count']:.2f} ms, gather {ms['copy']:.2f} ms, "
           f"{orig / ms['count'] / 1e6:.1f} GB/s decompressed", flush=True)
 for stage in ("1",):
-    os.environ["OKV_ZSTD_STAGE"] = stage
+    os.environ.pop("OKV_ZSTD_GENERAL", None)
     os.environ["OKV_ZSTD_PROF"] = "1"
     print("stage", stage, flush=True)
     dec.decode(seg, descs, compression=okv.sst.COMP_ZSTD)

@@ -257,6 +257,73 @@ int okv_synth_rows_fixed(okv_ctx *ctx, uint64_t seed, uint64_t first_row, uint64
                          uint64_t *key_off, uint16_t *key_len_out, uint8_t *val_arena,
                          uint64_t *val_off, uint32_t *val_len_out);
 
+/* ======================================================================== *
+ * Merge: snapshot_reader.Reader.GetRange's k-way merge
+ * (/root/reference/snapshot_reader/snapshot_reader.go:214-372) on the device,
+ * and the same newest-wins merge as a compaction feed.
+ * ======================================================================== */
+#define OKV_MERGE_GETRANGE 0 /* the Go loop exactly: range bound, limit, tombstones, and the
+                                stale cursor of a stream that ran out (:336-365) */
+#define OKV_MERGE_ALL 1      /* every key's owning row (compaction); L0 tombstones dropped
+                                iff drop_tombstones */
+#define OKV_DIR_ASC 0        /* sst.DirectionAscending  (segment_row_iter.go:22-25) */
+#define OKV_DIR_DESC 1       /* sst.DirectionDescending */
+#define OKV_M_EOF 1          /* okv_merge_out.status: GetRange returns an error because a
+                                RowIter.Next hit io.EOF rolling a tombstone forward (:316-331) */
+
+/* One merge input: rows [row_lo, row_hi) of a decoded segment (the okv_decode_out
+ * layout, device pointers), sorted ascending by key as the Go writer writes them.
+ * For GetRange this is the stream RowIter(direction).Seek(startRange) yields
+ * (ascending: rows >= start; descending: rows <= end, consumed from row_hi - 1).
+ * Inputs are given in the snapshot's priority order (:235-254); among equal keys
+ * the lowest index owns the key (findMaxIndexes, :404-424). */
+typedef struct okv_merge_src {
+  const uint8_t *key_arena;
+  const uint64_t *key_off;
+  const uint16_t *key_len;
+  const uint8_t *val_arena;
+  const uint64_t *val_off;
+  const uint32_t *val_len; /* 0 = Go nil: an L0 row with a nil value is a tombstone */
+  uint64_t row_lo, row_hi;
+  int32_t level; /* SegmentRecord.Level */
+  int32_t pad;
+} okv_merge_src;
+
+typedef struct okv_merge_opts {
+  int mode;            /* OKV_MERGE_* */
+  int direction;       /* OKV_DIR_* */
+  int drop_tombstones; /* OKV_MERGE_ALL only */
+  int pad;
+  uint64_t limit;      /* OKV_MERGE_GETRANGE: > 0 (Go panics on 0: the caller's check) */
+  const uint8_t *bound; /* host bytes: end (ascending) or start (descending), :340-347 */
+  uint64_t bound_len;
+} okv_merge_opts;
+
+/* Output rows in iteration order: which input and row, and optionally an
+ * index-only SoA whose offsets are relative to key_base / val_base (callers pass
+ * the lowest input arena address), so the result feeds okv_encode_rows directly.
+ * Any array pointer may be NULL. */
+typedef struct okv_merge_out {
+  uint32_t *src;
+  uint64_t *row;
+  uint64_t *key_off;
+  uint16_t *key_len;
+  uint64_t *val_off;
+  uint32_t *val_len;
+  const uint8_t *key_base;
+  const uint8_t *val_base;
+  uint64_t row_cap;
+  /* filled on return: */
+  uint64_t n_rows;   /* rows returned (set also with OKV_E_CAPACITY) */
+  uint64_t n_unique; /* distinct keys across the inputs */
+  int32_t status;    /* 0, or OKV_M_EOF (no rows are written) */
+  int32_t pad;
+} okv_merge_out;
+
+/* flags: OKV_F_DEVICE_PTRS (required), OKV_F_ASYNC. At most 64 inputs. */
+int okv_merge_rows(okv_ctx *ctx, const okv_merge_src *srcs, uint32_t nsrc,
+                   const okv_merge_opts *opts, okv_merge_out *out, uint32_t flags);
+
 /* Per-kernel timing with HIP events recorded on the context stream around
  * each launch of okv_decode_blocks (pass 1 count, pass 2 scan, pass 3
  * copy/index).  okv_profile(ctx, 1) enables and resets; okv_profile_read

@@ -21,6 +21,9 @@ F_DEVICE_PTRS, F_INDEX_ONLY, F_ASYNC, F_NO_CLOSE = 1, 2, 4, 8
 W_KEY_TOO_LARGE, W_VALUE_TOO_LARGE, W_CLOSED, W_INVALID_KEY = -101, -102, -103, -104
 W_NIL_WRITER, W_UNSUPPORTED, W_NO_ROWS = -105, -106, -107
 SYNTH_FIXED, SYNTH_ZIPF = 0, 1
+MERGE_GETRANGE, MERGE_ALL = 0, 1
+DIR_ASC, DIR_DESC = 0, 1
+M_EOF = 1
 
 # exported symbols declared by include/*.h (checked by tests/test_abi.py)
 SYMBOLS = [
@@ -29,7 +32,7 @@ SYMBOLS = [
     "okv_xxh64", "okv_hash_blocks", "okv_device_alloc", "okv_device_free", "okv_host_alloc",
     "okv_host_free", "okv_memcpy", "okv_profile", "okv_profile_read",
     "okv_encode_rows", "okv_encode_close", "okv_encode_profile_read", "okv_encode_profile_reset",
-    "okv_synth_rows_fixed",
+    "okv_synth_rows_fixed", "okv_merge_rows",
     "okv_writer_new", "okv_writer_write_row", "okv_writer_close", "okv_writer_data",
     "okv_writer_meta", "okv_writer_num_blocks", "okv_writer_block", "okv_writer_free",
     "okv_meta_fetch", "okv_meta_parse", "okv_meta_num_blocks", "okv_meta_compression",
@@ -79,6 +82,27 @@ class EncodeOut(C.Structure):
                 ("n_blocks", C.c_uint64), ("data_bytes", C.c_uint64),
                 ("meta_bytes", C.c_uint64), ("file_bytes", C.c_uint64),
                 ("meta_hash", C.c_uint64), ("bad_row", C.c_uint64)]
+
+
+class MergeSrc(C.Structure):
+    _fields_ = [("key_arena", C.c_void_p), ("key_off", C.c_void_p), ("key_len", C.c_void_p),
+                ("val_arena", C.c_void_p), ("val_off", C.c_void_p), ("val_len", C.c_void_p),
+                ("row_lo", C.c_uint64), ("row_hi", C.c_uint64), ("level", C.c_int32),
+                ("pad", C.c_int32)]
+
+
+class MergeOpts(C.Structure):
+    _fields_ = [("mode", C.c_int), ("direction", C.c_int), ("drop_tombstones", C.c_int),
+                ("pad", C.c_int), ("limit", C.c_uint64), ("bound", C.c_void_p),
+                ("bound_len", C.c_uint64)]
+
+
+class MergeOut(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("row", C.c_void_p), ("key_off", C.c_void_p),
+                ("key_len", C.c_void_p), ("val_off", C.c_void_p), ("val_len", C.c_void_p),
+                ("key_base", C.c_void_p), ("val_base", C.c_void_p), ("row_cap", C.c_uint64),
+                ("n_rows", C.c_uint64), ("n_unique", C.c_uint64), ("status", C.c_int32),
+                ("pad", C.c_int32)]
 
 
 _lib = None
@@ -136,6 +160,8 @@ def lib():
         "okv_encode_profile_read": (i32, [p, C.POINTER(C.c_double), C.POINTER(u64)]),
         "okv_encode_profile_reset": (i32, [p]),
         "okv_synth_rows_fixed": (i32, [p, u64, u64, u64, u32, u32, p, p, p, p, p, p]),
+        "okv_merge_rows": (i32, [p, C.POINTER(MergeSrc), u32, C.POINTER(MergeOpts),
+                                 C.POINTER(MergeOut), u32]),
         "okv_writer_new": (p, [u64, u64, i32, i32]),
         "okv_writer_write_row": (i32, [p, p, C.c_size_t, p, C.c_size_t]),
         "okv_writer_close": (i32, [p, i32, C.POINTER(u64), C.POINTER(u64)]),

@@ -13,6 +13,10 @@
 namespace okv {
 struct EncScratch;  // okv_encode.hip
 void enc_release(okv_ctx* ctx);
+namespace mrg {
+struct Scratch;  // okv_merge.hip
+}
+void merge_release(okv_ctx* ctx);
 // okv_decode.hip: enqueue XXH64 of each block's BlockSize bytes (device pointers).
 void launch_hash(hipStream_t stream, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
                  uint32_t nblk, uint64_t* out);
@@ -58,6 +62,7 @@ struct okv_ctx {
   double prof_ms[3] = {0, 0, 0};
   uint64_t prof_calls = 0;
   okv::EncScratch* enc = nullptr;  // encode scratch (okv_encode.hip)
+  okv::mrg::Scratch* merge = nullptr;  // merge scratch (okv_merge.hip)
   // zstd decompression scratch (okv_zstd.hip)
   uint64_t* z_cap_off = nullptr;  // [nblk + 1] decompressed-region offsets
   uint64_t* z_dec_len = nullptr;  // [nblk]

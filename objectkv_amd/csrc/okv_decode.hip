@@ -1116,6 +1116,7 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->z_seq_off);
   (void)hipFree(ctx->z_seqs);
   okv::enc_release(ctx);
+  okv::merge_release(ctx);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }

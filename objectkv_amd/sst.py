@@ -326,6 +326,38 @@ class Decoder:
         self._check(rc, "okv_decode_blocks(device)")
         return o
 
+    def merge_device(self, srcs, mode, direction, limit=0, bound=None, drop_tombstones=False,
+                     out: dict | None = None, key_base=0, val_base=0, row_cap=0):
+        """okv_merge_rows over decoded device segments.
+
+        srcs: [(soa dict of torch tensors key_arena/key_off/key_len/val_arena/
+        val_off/val_len, row_lo, row_hi, level)] in priority order.  out: torch
+        tensors src (int32), row (int64) and optionally key_off, key_len,
+        val_off, val_len (relative to key_base / val_base).  Returns the filled
+        okv_merge_out."""
+        arr = (_lib.MergeSrc * max(1, len(srcs)))()
+        for i, (t, lo, hi, level) in enumerate(srcs):
+            arr[i] = _lib.MergeSrc(_ptr(t["key_arena"]), _ptr(t["key_off"]), _ptr(t["key_len"]),
+                                   _ptr(t["val_arena"]), _ptr(t["val_off"]), _ptr(t["val_len"]),
+                                   int(lo), int(hi), int(level), 0)
+        b = None if bound is None else np.frombuffer(bytes(bound), np.uint8)
+        o = _lib.MergeOpts(mode, direction, int(drop_tombstones), 0, int(limit),
+                           _ptr(b) if b is not None and b.size else None,
+                           0 if b is None else int(b.size))
+        g = (out or {}).get
+        mo = _lib.MergeOut(_ptr(g("src")), _ptr(g("row")), _ptr(g("key_off")),
+                           _ptr(g("key_len")), _ptr(g("val_off")), _ptr(g("val_len")),
+                           key_base or None, val_base or None, int(row_cap), 0, 0, 0, 0)
+        rc = lib().okv_merge_rows(self._ctx, arr, len(srcs), C.byref(o), C.byref(mo),
+                                  F_DEVICE_PTRS)
+        if rc and rc != _lib.OKV_E_CAPACITY:
+            self._check(rc, "okv_merge_rows")
+        if rc:
+            err = OkvError(rc, "okv_merge_rows: output capacity")
+            err.out = mo
+            raise err
+        return mo
+
     def plan_device(self, seg_t, seg_bytes, descs_t, nblk, compression=COMP_NONE,
                     index_only=False):
         r, k, v = C.c_uint64(), C.c_uint64(), C.c_uint64()

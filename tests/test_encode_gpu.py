@@ -267,3 +267,30 @@ def test_general_pack_path_vs_oracle(enc):
             continue
         got = enc.encode(rows, T, D)
         assert got.seg.tobytes() == want
+
+
+def test_c1_round_trip(enc, decoder):
+    """BASELINE.json configs[0] (C1): 10 000 rows of 16 B key / 64 B value
+    written with the GPU SegmentWriter and read back in full through the
+    GPU-backed RowIter; bytes equal the oracle writer's, 239 blocks
+    (238 x 42 rows + 4), every row returned in order."""
+    from objectkv_amd import reader as R
+    rows = list(P.rows_fixed(10_000, seed=1))
+    w = okv.GpuSegmentWriter(enc)
+    for k, v in rows:
+        w.WriteRow(k, v)
+    flen, meta = w.Close()
+    rc, want, want_meta = oracle_segment(rows)
+    assert rc == 0 and w.data().tobytes() == want and meta == want_meta
+    assert flen == len(want) and w.result.n_blocks == 239
+    r = R.SegmentReader(w.data().tobytes(), flen, decoder)
+    it = r.RowIter(R.DirectionAscending)
+    got = []
+    while True:
+        try:
+            kv = it.Next()
+        except R.GoError as e:
+            assert e.kind == "EOF"
+            break
+        got.append((kv.Key, kv.Value))
+    assert got == rows

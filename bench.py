@@ -46,8 +46,13 @@ CONFIGS = {
     "c4": ("encode", 1, 100_000_000, 3584, 4096,
            "C4: encode 100 M sorted pairs (16 B key / 64 B value) into 4 KiB blocks + "
            "BlockStat index + meta block on device, key-range shards across GPUs"),
+    # compaction: K overlapping L0 segments of n rows each -> one segment
+    "cm": ("compact", 11, 16_000_000, 3584, 4096,
+           "CM: compaction of 4 overlapping L0 segments x 16 M rows (16 B key / 64 B value, "
+           "each overlapping the next by half): decode -> newest-wins merge -> encode, on device"),
 }
 ENC_METRIC = "GiB/s device-resident segment encode (data blocks written) + M rows/s"
+CMP_METRIC = "GiB/s device-resident compaction (input segment bytes) + M rows/s"
 
 
 def log(*a):
@@ -104,6 +109,8 @@ def main():
 
     if args.config == "c4":
         return run_encode(args, torch, okv, dist, world, rank, local, dev)
+    if args.config == "cm":
+        return run_compact(args, torch, okv, dist, world, rank, local, dev)
     kind, seed0, nblk, th, bs, desc = CONFIGS[args.config]
     seed = seed0 + rank
     t0 = time.time()
@@ -410,6 +417,179 @@ def run_encode(args, torch, okv, dist, world, rank, local, dev):
                      "kernel": "okv_enc_pack_lds_kernel (pack + block XXH64)",
                      "algorithmic_bytes_per_launch": int(alg)},
         "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    enc.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def _fixed_vals(seed, r0, n, vl=64):
+    """Values of rows r0 .. r0 + n - 1 of rows_fixed(seed) (splitmix64 words
+    drawn in row order; okv_synth_rows_fixed), for the guard below."""
+    w = np.arange(r0 * (vl // 8), (r0 + n) * (vl // 8), dtype=np.uint64) + np.uint64(1)
+    z = np.uint64(seed) + w * np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    z = z ^ (z >> np.uint64(31))
+    return z.astype("<u8").view(np.uint8).reshape(n, vl)
+
+
+def run_compact(args, torch, okv, dist, world, rank, local, dev):
+    """CM: one compaction step on device-resident segments -- the compactor the
+    reference leaves as a stub (sst/compactor.go:3-6) over its own merge rule
+    (GetRange: newest L0 segment owns a key, snapshot_reader.go:294-331).
+    K input segments (segment s = rows [s n/2, s n/2 + n) of seed + s, written
+    once by the device encoder) -> K batched decodes (okv_decode_blocks) ->
+    okv_merge_rows (OKV_MERGE_ALL, newest first) -> okv_encode_rows of the
+    merged rows straight from the decoded arenas (no close: the meta hash is
+    one host XXH64, as in C4).  Each rank compacts its own segment set (weak
+    scaling, no collective)."""
+    from objectkv_amd import _lib
+    from objectkv_amd.snapshot import _Addr
+    _, seed0, n, th, bs, desc = CONFIGS["cm"]
+    K, KL, VL = 4, 16, 64
+    seed0 += 100 * rank
+    stream = torch.cuda.current_stream(dev)
+    enc = okv.Encoder(local, stream=stream.cuda_stream)
+    per_block = -(-th // (6 + KL + VL))
+
+    def out_for(rows):
+        nb = -(-rows // per_block)
+        return dict(seg=torch.empty(nb * bs + (nb + 1) * (42 + KL) + 4096, dtype=torch.uint8,
+                                    device=dev),
+                    first_row=torch.empty(nb + 2, dtype=torch.int64, device=dev),
+                    desc=torch.empty((nb + 1, 4), dtype=torch.int64, device=dev),
+                    hash=torch.empty(nb + 1, dtype=torch.int64, device=dev))
+
+    t0 = time.time()
+    segs = []  # (seg tensor, file bytes, desc tensor, n_blocks)
+    for s in range(K):
+        rows = dict(key_arena=torch.empty(n * KL, dtype=torch.uint8, device=dev),
+                    key_off=torch.empty(n, dtype=torch.int64, device=dev),
+                    key_len=torch.empty(n, dtype=torch.int16, device=dev),
+                    val_arena=torch.empty(n * VL, dtype=torch.uint8, device=dev),
+                    val_off=torch.empty(n, dtype=torch.int64, device=dev),
+                    val_len=torch.empty(n, dtype=torch.int32, device=dev))
+        enc.synth_fixed_device(seed0 + s, s * n // 2, n, KL, VL, rows)
+        out = out_for(n)
+        eo = enc.encode_device(rows, n, out, threshold=th, block_size=bs, strict_go=False)
+        segs.append((out["seg"], int(eo.file_bytes), out["desc"][:eo.n_blocks].contiguous(),
+                     int(eo.n_blocks)))
+        del rows
+    in_bytes = sum(f for _s, f, _d, _nb in segs)
+    # decode outputs (SoA + arenas) per input segment
+    douts = []
+    for seg_t, fb, d_t, nb in segs:
+        r, kb, vb = enc.plan_device(seg_t, fb, d_t, nb)
+        douts.append(dict(row_start=torch.empty(nb + 1, dtype=torch.int64, device=dev),
+                          key_base=torch.empty(nb, dtype=torch.int64, device=dev),
+                          val_base=torch.empty(nb, dtype=torch.int64, device=dev),
+                          status=torch.empty(nb, dtype=torch.int32, device=dev),
+                          key_off=torch.empty(r, dtype=torch.int64, device=dev),
+                          key_len=torch.empty(r, dtype=torch.int16, device=dev),
+                          val_off=torch.empty(r, dtype=torch.int64, device=dev),
+                          val_len=torch.empty(r, dtype=torch.int32, device=dev),
+                          key_arena=torch.empty(max(kb, 16), dtype=torch.uint8, device=dev),
+                          val_arena=torch.empty(max(vb, 16), dtype=torch.uint8, device=dev),
+                          rows=r))
+    n_in = sum(d["rows"] for d in douts)
+    order = list(range(K - 1, -1, -1))  # newest (highest s) first
+    kb0 = min(douts[s]["key_arena"].data_ptr() for s in order)
+    vb0 = min(douts[s]["val_arena"].data_ptr() for s in order)
+    kspan = max(d["key_arena"].data_ptr() + d["key_arena"].numel() for d in douts) - kb0
+    vspan = max(d["val_arena"].data_ptr() + d["val_arena"].numel() for d in douts) - vb0
+    mout = dict(key_off=torch.empty(n_in, dtype=torch.int64, device=dev),
+                key_len=torch.empty(n_in, dtype=torch.int16, device=dev),
+                val_off=torch.empty(n_in, dtype=torch.int64, device=dev),
+                val_len=torch.empty(n_in, dtype=torch.int32, device=dev))
+    n_uniq = (K - 1) * n // 2 + n
+    eout = out_for(n_uniq)
+    mrows = dict(key_arena=_Addr(kb0), key_off=mout["key_off"], key_len=mout["key_len"],
+                 val_arena=_Addr(vb0), val_off=mout["val_off"], val_len=mout["val_len"])
+    log(f"[rank {rank}] built {K} segments ({in_bytes / 2**30:.2f} GiB, {n_in} rows) "
+        f"in {time.time() - t0:.1f}s")
+
+    def step(ph=None):
+        # stage times (diagnostic): host clock around each stage, the context
+        # stream drained at each boundary (the merge syncs internally anyway)
+        t = time.perf_counter()
+        for (seg_t, fb, d_t, nb), d in zip(segs, douts):
+            enc.decode_device(seg_t, fb, d_t, nb, d, sync=False)
+        if ph is not None:
+            enc.sync()
+            t, ph[0] = time.perf_counter(), ph[0] + time.perf_counter() - t
+        mo = enc.merge_device([(douts[s], 0, douts[s]["rows"], 0) for s in order],
+                              _lib.MERGE_ALL, _lib.DIR_ASC, 0, None, True, out=mout,
+                              key_base=kb0, val_base=vb0, row_cap=n_in)
+        if ph is not None:
+            enc.sync()
+            t, ph[1] = time.perf_counter(), ph[1] + time.perf_counter() - t
+        eo = enc.encode_device(mrows, int(mo.n_rows), eout, threshold=th, block_size=bs,
+                               strict_go=False, close=False, key_arena_bytes=kspan,
+                               val_arena_bytes=vspan)
+        if ph is not None:
+            enc.sync()
+            ph[2] += time.perf_counter() - t
+        return mo, eo
+
+    # correctness guard: every key once, the newest segment's value, output
+    # blocks in the overlaps byte-equal to the CPU writer over the expected rows
+    mo, eo = step()
+    torch.cuda.synchronize(dev)
+    assert int(mo.n_rows) == n_uniq == int(mo.n_unique), (mo.n_rows, n_uniq)
+    from oracle import coracle
+    for b0 in (0, (n // 2) // per_block + 3, (n + n // 4) // per_block, n_uniq // per_block - 4):
+        r0 = b0 * per_block
+        w = coracle.Writer(th, bs)
+        for r in range(r0, r0 + 3 * per_block + 1):  # +1: not Q1
+            s_new = min(K - 1, r // (n // 2))  # newest segment holding row r
+            assert w.write_row(r.to_bytes(KL, "big"),
+                               _fixed_vals(seed0 + s_new, r, 1)[0].tobytes()) == 0
+        _, want, _ = w.close()
+        got = eout["seg"][b0 * bs:(b0 + 3) * bs].cpu().numpy().tobytes()
+        assert got == want[:3 * bs], b0
+    out_bytes = int(eo.data_bytes)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    t_elapsed = time.perf_counter() - t_start
+    if dist:
+        dist.barrier()
+    t_max = t_elapsed
+    if dist:
+        tdev = dev if args.dist_backend == "nccl" else "cpu"
+        tt = torch.tensor([t_elapsed], dtype=torch.float64, device=tdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+    t_step = t_max / args.steps
+    ph = np.zeros(3)  # untimed diagnostic pass: per-stage wall time
+    for _ in range(2):
+        step(ph)
+    ph *= 1e3 / 2
+    line = {
+        "metric": CMP_METRIC, "value": round(in_bytes * world / t_step / 2**30, 3),
+        "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(t_step * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": desc, "segments_per_gpu": K, "rows_in_per_gpu": n_in,
+                   "rows_out_per_gpu": n_uniq, "input_bytes_per_gpu": in_bytes,
+                   "output_data_bytes_per_gpu": out_bytes,
+                   "parallelism": f"{world} independent compactions (no collective)"},
+        "rows_per_s": round(n_in * world / t_step),
+        "mrows_per_s": round(n_in * world / t_step / 1e6, 3),
+        "stage_ms": {"decode": round(ph[0], 4), "merge": round(ph[1], 4),
+                     "encode": round(ph[2], 4)},
+        "roofline": None, "cpu_baseline": None,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

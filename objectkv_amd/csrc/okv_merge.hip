@@ -7,7 +7,8 @@
 // okv_decode_out SoA), in the snapshot's priority order (:235-254): among equal
 // keys the lowest stream index owns the key (findMaxIndexes keeps the first
 // index, :404-424).  The merge is computed, not iterated:
-//   1. prefix: per row an 8-byte big-endian key prefix and the key's address;
+//   1. prefix: per row the first 16 key bytes (big-endian words) and the key's
+//      address;
 //   2. rank: a row's place in the merged multiset is its index in its stream
 //      plus, per other stream, a binary-searched count of smaller keys (<= for
 //      streams before it, < after it); it owns its key iff no earlier stream
@@ -58,10 +59,17 @@ enum : uint8_t {
   kEmitErr = 5,    // appended; the stale cursor's owner is an L0 tombstone: io.EOF error
 };
 
+// The first 16 key bytes as two big-endian words, zero padded: with the length
+// as the tie-break, comparing these orders keys as bytes.Compare does, so keys
+// of <= 16 bytes never touch the arenas.
+struct Key16 {
+  uint64_t a, b;
+};
+
 struct Scratch {
   uint64_t cap_rows = 0;
   uint64_t* kaddr = nullptr;  // [N] key address
-  uint64_t* pfx = nullptr;    // [N] big-endian first 8 key bytes
+  Key16* pfx = nullptr;       // [N] big-endian first 16 key bytes (zero padded)
   uint32_t* klen = nullptr;   // [N]
   uint64_t* pos = nullptr;    // [N] merged position
   uint8_t* own = nullptr;     // [N] owns its key
@@ -93,23 +101,30 @@ __device__ __forceinline__ uint32_t find_src(const uint64_t* __restrict__ base, 
   return lo;
 }
 
+// Key bytes [off, off + 8) as a big-endian word, bytes past len read as 0;
+// the eight loads are independent (one memory round trip).
+__device__ __forceinline__ uint64_t be_word(const uint8_t* k, uint32_t len, uint32_t off) {
+  uint64_t p = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) p = (p << 8) | (off + i < len ? uint64_t(k[off + i]) : 0ull);
+  return p;
+}
+
+__device__ __forceinline__ Key16 be_prefix(const uint8_t* k, uint32_t len) {
+  return Key16{be_word(k, len, 0), be_word(k, len, 8)};
+}
+
 // bytes.Compare of two keys given their prefixes, lengths and addresses.
-__device__ __forceinline__ int key_cmp(uint64_t pa, uint32_t la, const uint8_t* ka, uint64_t pb,
-                                       uint32_t lb, const uint8_t* kb) {
-  if (pa != pb) return pa < pb ? -1 : 1;
+__device__ __forceinline__ int key_cmp(const Key16& pa, uint32_t la, const uint8_t* ka,
+                                       const Key16& pb, uint32_t lb, const uint8_t* kb) {
+  if (pa.a != pb.a) return pa.a < pb.a ? -1 : 1;
+  if (pa.b != pb.b) return pa.b < pb.b ? -1 : 1;
   const uint32_t m = la < lb ? la : lb;
-  for (uint32_t i = 8; i < m; ++i) {
-    const uint32_t x = ka[i], y = kb[i];
+  for (uint32_t i = 16; i < m; i += 8) {
+    const uint64_t x = be_word(ka, la, i), y = be_word(kb, lb, i);
     if (x != y) return x < y ? -1 : 1;
   }
   return la < lb ? -1 : (la > lb ? 1 : 0);
-}
-
-__device__ __forceinline__ uint64_t be_prefix(const uint8_t* k, uint32_t len) {
-  uint64_t p = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) p = (p << 8) | (uint32_t(i) < len ? uint64_t(k[i]) : 0ull);
-  return p;
 }
 
 }  // namespace mrg
@@ -119,7 +134,7 @@ __global__ __launch_bounds__(256) void okv_merge_pfx_kernel(const mrg::Src* __re
                                                             const uint64_t* __restrict__ base,
                                                             uint32_t k, uint64_t n,
                                                             uint64_t* __restrict__ kaddr,
-                                                            uint64_t* __restrict__ pfx,
+                                                            mrg::Key16* __restrict__ pfx,
                                                             uint32_t* __restrict__ klen) {
   const uint64_t g = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (g >= n) return;
@@ -136,10 +151,10 @@ __global__ __launch_bounds__(256) void okv_merge_pfx_kernel(const mrg::Src* __re
 namespace mrg {
 // First global row in [lo, hi) whose key is > key (le) or >= key (!le): the
 // count of stream rows <= / < key, offset by the stream base.
-__device__ __forceinline__ uint64_t rank_in(const uint64_t* __restrict__ pfx,
+__device__ __forceinline__ uint64_t rank_in(const Key16* __restrict__ pfx,
                                             const uint32_t* __restrict__ klen,
                                             const uint64_t* __restrict__ kaddr, uint64_t lo,
-                                            uint64_t hi, uint64_t p0, uint32_t l0,
+                                            uint64_t hi, const Key16& p0, uint32_t l0,
                                             const uint8_t* k0, bool le) {
   while (lo < hi) {
     const uint64_t m = (lo + hi) >> 1;
@@ -159,7 +174,7 @@ __device__ __forceinline__ uint64_t rank_in(const uint64_t* __restrict__ pfx,
 // window in stream j (a few cached steps instead of a full-range search).
 __global__ __launch_bounds__(256) void okv_merge_rank_kernel(
     const uint64_t* __restrict__ base, uint32_t k, uint64_t n, const uint64_t* __restrict__ kaddr,
-    const uint64_t* __restrict__ pfx, const uint32_t* __restrict__ klen,
+    const mrg::Key16* __restrict__ pfx, const uint32_t* __restrict__ klen,
     uint64_t* __restrict__ pos, uint8_t* __restrict__ own) {
   __shared__ uint64_t s_lo[mrg::kMaxSrc], s_hi[mrg::kMaxSrc];
   const uint64_t g0 = uint64_t(blockIdx.x) * blockDim.x;
@@ -183,7 +198,7 @@ __global__ __launch_bounds__(256) void okv_merge_rank_kernel(
   const uint64_t g = g0 + threadIdx.x;
   if (g >= n) return;
   const uint32_t i = one ? i0 : mrg::find_src(base, k, g);
-  const uint64_t p0 = pfx[g];
+  const mrg::Key16 p0 = pfx[g];
   const uint32_t l0 = klen[g];
   const uint8_t* k0 = reinterpret_cast<const uint8_t*>(kaddr[g]);
   uint64_t rank = g - base[i];
@@ -310,7 +325,7 @@ __global__ void okv_merge_ends_kernel(const uint64_t* __restrict__ base, uint32_
 __global__ __launch_bounds__(256) void okv_merge_event_kernel(
     const mrg::Src* __restrict__ src, const uint64_t* __restrict__ base, uint32_t k, uint64_t nu,
     int dir, int mode, int drop_tomb, const uint64_t* __restrict__ uniq,
-    const uint64_t* __restrict__ kaddr, const uint64_t* __restrict__ pfx,
+    const uint64_t* __restrict__ kaddr, const mrg::Key16* __restrict__ pfx,
     const uint32_t* __restrict__ klen, const uint8_t* __restrict__ bound, uint32_t bound_len,
     const uint64_t* __restrict__ ends, uint8_t* __restrict__ ev, uint32_t* __restrict__ emit) {
   const uint64_t d = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -337,7 +352,7 @@ __global__ __launch_bounds__(256) void okv_merge_event_kernel(
       e = end_here ? mrg::kErr : mrg::kSkip;
     } else {
       const uint8_t* kp = reinterpret_cast<const uint8_t*>(kaddr[g]);
-      const uint64_t bp = mrg::be_prefix(bound, bound_len);
+      const mrg::Key16 bp = mrg::be_prefix(bound, bound_len);
       const int c = mrg::key_cmp(pfx[g], klen[g], kp, bp, bound_len, bound);
       const bool out = dir == OKV_DIR_DESC ? c <= 0 : c >= 0;
       if (out) {
@@ -446,7 +461,7 @@ int ensure(okv_ctx* ctx, mrg::Scratch* m, uint64_t n) {
                  reinterpret_cast<void**>(&m->own),   reinterpret_cast<void**>(&m->mg),
                  reinterpret_cast<void**>(&m->mown),  reinterpret_cast<void**>(&m->uniq),
                  reinterpret_cast<void**>(&m->ev),    reinterpret_cast<void**>(&m->escan)};
-  const size_t sz[] = {8, 8, 4, 8, 1, 8, 4, 8, 1, 4};
+  const size_t sz[] = {8, sizeof(mrg::Key16), 4, 8, 1, 8, 4, 8, 1, 4};
   const uint64_t c = std::max<uint64_t>(n + n / 8, 4096);
   for (int q = 0; q < 10; ++q) {
     (void)hipFree(*ps[q]);

@@ -56,6 +56,7 @@ struct okv_ctx {
   // per-pass event timing (okv_profile)
   int variant = 3;  // diagnostic ablation selector (OKV_COPY_VARIANT)
   uint32_t gather_grid = 0;  // 0: one workgroup per block; else persistent grid size
+  uint32_t gather_threads = 0;  // 0: by average block size; else 64 or 256 (OKV_GATHER_THREADS)
   bool prof = false;
   std::vector<hipEvent_t> ev;  // 4 per timed call
   size_t ev_used = 0;

@@ -260,7 +260,7 @@ struct GatherSmem {
 // completed in registers from the following rows; past the region end it is
 // zero (the 16-byte padding).  kU tiles per iteration keep kU windows in
 // flight per lane.
-template <bool kVal, uint32_t kU, bool kShfl>
+template <bool kVal, uint32_t kU, bool kShfl, int NT>
 __device__ __forceinline__ void gather_region(const CopyParams& P, const GatherSmem& sm,
                                               int rows, uint64_t off, uint8_t* __restrict__ arena,
                                               uint64_t dbase) {
@@ -270,7 +270,7 @@ __device__ __forceinline__ void gather_region(const CopyParams& P, const GatherS
   const uint32_t N = (total + 15) >> 4;  // chunks, including the padded tail
   const uint32_t T = (N + 63) >> 6;      // 1 KiB tiles
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t nw = kThreads / 64;
+  const uint32_t nw = NT / 64;
   const uint32_t t0 = uint32_t(uint64_t(T) * wave / nw), t1 = uint32_t(uint64_t(T) * (wave + 1) / nw);
   const uint32_t last = uint32_t(rows) - 1;
   uint32_t r = 0;
@@ -347,7 +347,7 @@ __device__ __forceinline__ void gather_region(const CopyParams& P, const GatherS
   }
 }
 
-template <int V>
+template <int V, int NT>
 __device__ __forceinline__ void gather_block(const CopyParams& P, GatherSmem& sm, uint32_t b) {
   const uint32_t tid = threadIdx.x;
   const BlockCount c = P.cnt[b];
@@ -402,19 +402,22 @@ __device__ __forceinline__ void gather_block(const CopyParams& P, GatherSmem& sm
   // diagnostic sweep: 3 = window loads x4 (product), 5 = shuffle x2, 6 = shuffle x4
   constexpr uint32_t kU = V == 5 ? 2 : 4;
   constexpr bool kShfl = V == 5 || V == 6;
-  gather_region<false, kU, kShfl>(P, sm, rows, off, P.key_arena, B.kb0);
-  gather_region<true, kU, kShfl>(P, sm, rows, off, P.val_arena, B.vb0);
+  gather_region<false, kU, kShfl, NT>(P, sm, rows, off, P.key_arena, B.kb0);
+  gather_region<true, kU, kShfl, NT>(P, sm, rows, off, P.val_arena, B.vb0);
 }
 
 // V selects a diagnostic ablation (tools/ablate.py): 0 row table only,
 // 1 + SoA index, >= 2 the full kernel (the only variant the API uses unless
 // OKV_COPY_VARIANT is set).
 // Grid: one workgroup per block, or a persistent grid striding over blocks.
-template <int V>
-__global__ __launch_bounds__(kThreads) void okv_gather_kernel(CopyParams P) {
+// NT = 256 (four waves share a block's tiles) for large blocks; NT = 64 (one
+// wave per block) for small ones, where a block has only a few 1 KiB tiles and
+// the row-table -> gather latency chain is hidden by more blocks in flight.
+template <int V, int NT>
+__global__ __launch_bounds__(NT) void okv_gather_kernel(CopyParams P) {
   __shared__ GatherSmem sm;
   for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
-    gather_block<V>(P, sm, b);
+    gather_block<V, NT>(P, sm, b);
     if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
   }
 }
@@ -936,14 +939,21 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   P.key_cap = index_only ? 0 : o->key_cap;
   P.val_cap = index_only ? 0 : o->val_cap;
   if (nblk) {
-    const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk),
-        t(kThreads);
-    switch (ctx->variant) {  // diagnostic ablations only; 3 is the product kernel
-      case 0: hipLaunchKernelGGL(okv_gather_kernel<0>, g, t, 0, ctx->stream, P); break;
-      case 1: hipLaunchKernelGGL(okv_gather_kernel<1>, g, t, 0, ctx->stream, P); break;
-      case 5: hipLaunchKernelGGL(okv_gather_kernel<5>, g, t, 0, ctx->stream, P); break;
-      case 6: hipLaunchKernelGGL(okv_gather_kernel<6>, g, t, 0, ctx->stream, P); break;
-      default: hipLaunchKernelGGL(okv_gather_kernel<3>, g, t, 0, ctx->stream, P);
+    const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
+    // one wave per block when blocks average <= 16 KiB (OKV_GATHER_THREADS=64|256 overrides)
+    const uint32_t nt = ctx->gather_threads ? ctx->gather_threads
+                                            : (w.seg_bytes / nblk <= 16384 ? 64u : 256u);
+    if (nt == 64) {
+      hipLaunchKernelGGL((okv_gather_kernel<3, 64>), g, dim3(64), 0, ctx->stream, P);
+    } else {
+      const dim3 t(kThreads);
+      switch (ctx->variant) {  // diagnostic ablations only; 3 is the product kernel
+        case 0: hipLaunchKernelGGL((okv_gather_kernel<0, kThreads>), g, t, 0, ctx->stream, P); break;
+        case 1: hipLaunchKernelGGL((okv_gather_kernel<1, kThreads>), g, t, 0, ctx->stream, P); break;
+        case 5: hipLaunchKernelGGL((okv_gather_kernel<5, kThreads>), g, t, 0, ctx->stream, P); break;
+        case 6: hipLaunchKernelGGL((okv_gather_kernel<6, kThreads>), g, t, 0, ctx->stream, P); break;
+        default: hipLaunchKernelGGL((okv_gather_kernel<3, kThreads>), g, t, 0, ctx->stream, P);
+      }
     }
     const uint32_t nbig_grid = std::min<uint32_t>(nblk, 512);
     if (index_only)
@@ -1069,6 +1079,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   ctx->device = device;
   if (const char* v = getenv("OKV_COPY_VARIANT")) ctx->variant = atoi(v);
   if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
+  if (const char* v = getenv("OKV_GATHER_THREADS")) ctx->gather_threads = uint32_t(atoi(v));
   if (stream) {
     ctx->stream = static_cast<hipStream_t>(stream);
   } else {

@@ -37,15 +37,26 @@ namespace okv {
 // ---------------------------------------------------------------------------
 // Pass 1: header walk in HBM, one lane per block.
 // ---------------------------------------------------------------------------
+// Small segments (prefetch = 1): each lane first touches one dword per 128-B
+// line of its block's record bytes -- independent loads, all in flight at
+// once -- so the dependent header chase then hits the caches instead of HBM.
+// A single-tile launch (one workgroup) also zeroes the big-block counter and
+// writes the totals itself (no memset, no scan launch): single_* non-null.
 __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     const uint8_t* __restrict__ seg, uint64_t seg_bytes, const Desc* __restrict__ descs,
     uint32_t nblk, int comp, BlockCount* __restrict__ cnt, Prefix* __restrict__ lp,
     Prefix* __restrict__ tile_tot, uint32_t* __restrict__ rec_s, uint32_t* __restrict__ big_list,
-    uint32_t* __restrict__ big_count, const int32_t* __restrict__ pre_status) {
+    uint32_t* __restrict__ big_count, const int32_t* __restrict__ pre_status, int prefetch,
+    Prefix* __restrict__ single_pre, Totals* __restrict__ single_tot,
+    uint64_t* __restrict__ single_row_start) {
   const uint32_t tid = threadIdx.x;
   const uint32_t b = blockIdx.x * kTile + tid;
   uint64_t rows = 0, kb = 0, vb = 0, p = 0;
   int32_t st = OKV_BLK_OK;
+  if (single_pre) {
+    if (tid == 0) *big_count = 0;
+    __syncthreads();
+  }
   if (b < nblk) {
     const Desc d = descs[b];
     const int32_t pre = pre_status ? pre_status[b] : int32_t(OKV_BLK_OK);
@@ -61,6 +72,23 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
       const uint64_t len = (comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
       const uint64_t orig = d.original_size;
       uint32_t* rec = rec_s + uint64_t(b) * kRCap;
+      if (prefetch && orig && len) {
+        // up to 32 lines (4 KiB), all issued before any is waited on;
+        // addresses clamped into [offset, offset + min(orig, len))
+        const uint64_t first = d.offset & ~uint64_t(3);
+        const uint64_t last = (d.offset + (orig < len ? orig : len) - 1) & ~uint64_t(3);
+        uint32_t v[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+          uint64_t a = (d.offset & ~uint64_t(127)) + 128ull * u;
+          a = a < first ? first : (a > last ? last : a);
+          v[u] = *reinterpret_cast<const uint32_t*>(seg + a);
+        }
+        uint32_t acc = 0;
+#pragma unroll
+        for (int u = 0; u < 32; ++u) acc ^= v[u];
+        asm volatile("" ::"v"(acc));  // keep the loads; their values are unused
+      }
       // The walk is a dependent chain (record i+1 starts where i ends), so
       // this kernel is bound by HBM latency x the longest block's row count.
       while (p < orig) {  // :340
@@ -123,6 +151,11 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     t.vb = inc[2] + v[2];
     t.bad = inc[3] + v[3];
     tile_tot[blockIdx.x] = t;
+    if (single_pre) {  // what okv_scan_kernel writes for one tile
+      *single_pre = Prefix{0, 0, 0, 0};
+      *single_tot = Totals{t.rows, t.kb, t.vb, t.bad};
+      if (single_row_start) single_row_start[nblk] = t.rows;
+    }
   }
 }
 
@@ -260,7 +293,9 @@ struct GatherSmem {
 // completed in registers from the following rows; past the region end it is
 // zero (the 16-byte padding).  kU tiles per iteration keep kU windows in
 // flight per lane.
-template <bool kVal, uint32_t kU, bool kShfl, int NT>
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+template <bool kVal, uint32_t kU, bool kShfl, int NT, bool kNTS = false>
 __device__ __forceinline__ void gather_region(const CopyParams& P, const GatherSmem& sm,
                                               int rows, uint64_t off, uint8_t* __restrict__ arena,
                                               uint64_t dbase) {
@@ -341,7 +376,12 @@ __device__ __forceinline__ void gather_region(const CopyParams& P, const GatherS
             out = merge_bytes(out, w, int32_t(q0 - x), int32_t((q1 < xe ? q1 : xe) - x));
           }
         }
-        *reinterpret_cast<uint4*>(arena + dbase + uint64_t(x)) = out;
+        if (kNTS) {
+          const u32x4_t o4 = {out.x, out.y, out.z, out.w};
+          __builtin_nontemporal_store(o4, reinterpret_cast<u32x4_t*>(arena + dbase + uint64_t(x)));
+        } else {
+          *reinterpret_cast<uint4*>(arena + dbase + uint64_t(x)) = out;
+        }
       }
     }
   }
@@ -399,11 +439,14 @@ __device__ __forceinline__ void gather_block(const CopyParams& P, GatherSmem& sm
     }
   }
   if (V < 2 || P.index_only) return;
-  // diagnostic sweep: 3 = window loads x4 (product), 5 = shuffle x2, 6 = shuffle x4
+  // diagnostic sweep: 3 = window loads x4 (product), 5 = shuffle x2, 6 = shuffle x4,
+  // 7 = nontemporal arena stores, 8 = values before keys
   constexpr uint32_t kU = V == 5 ? 2 : 4;
   constexpr bool kShfl = V == 5 || V == 6;
-  gather_region<false, kU, kShfl, NT>(P, sm, rows, off, P.key_arena, B.kb0);
-  gather_region<true, kU, kShfl, NT>(P, sm, rows, off, P.val_arena, B.vb0);
+  constexpr bool kNTS = V == 7;
+  if (V == 8) gather_region<true, kU, kShfl, NT, kNTS>(P, sm, rows, off, P.val_arena, B.vb0);
+  gather_region<false, kU, kShfl, NT, kNTS>(P, sm, rows, off, P.key_arena, B.kb0);
+  if (V != 8) gather_region<true, kU, kShfl, NT, kNTS>(P, sm, rows, off, P.val_arena, B.vb0);
 }
 
 // V selects a diagnostic ablation (tools/ablate.py): 0 row table only,
@@ -419,6 +462,17 @@ __global__ __launch_bounds__(NT) void okv_gather_kernel(CopyParams P) {
   for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
     gather_block<V, NT>(P, sm, b);
     if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
+  }
+}
+
+// Occupancy ablation (OKV_COPY_VARIANT 9 / 10): the product kernel with a
+// register budget for W waves per SIMD.
+template <int NT, int W>
+__global__ __launch_bounds__(NT, W) void okv_gather_occ_kernel(CopyParams P) {
+  __shared__ GatherSmem sm;
+  for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
+    gather_block<3, NT>(P, sm, b);
+    if (b + gridDim.x < P.nblk) __syncthreads();
   }
 }
 
@@ -878,14 +932,21 @@ int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_star
   int rc = ensure_blocks(ctx, nblk);
   if (rc) return rc;
   const uint32_t ntiles = (nblk + kTile - 1) / kTile;
-  OKV_HIP(hipMemsetAsync(ctx->d_big + nblk, 0, sizeof(uint32_t), ctx->stream));
+  const bool single = ntiles == 1;
+  // prefetch block lines before the chase when the segment fits in the caches
+  // and blocks are small (dense headers); 64 KiB blocks touch ~5 % of their lines
+  const int prefetch = nblk && w.seg_bytes <= (64ull << 20) && w.seg_bytes / nblk <= 16384;
+  if (!single) OKV_HIP(hipMemsetAsync(ctx->d_big + nblk, 0, sizeof(uint32_t), ctx->stream));
   if (ntiles)
     hipLaunchKernelGGL(okv_count_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, w.seg,
                        w.seg_bytes, w.descs, nblk, w.comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
-                       ctx->d_rec, ctx->d_big, ctx->d_big + nblk, w.pre);
+                       ctx->d_rec, ctx->d_big, ctx->d_big + nblk, w.pre, prefetch,
+                       single ? ctx->d_tile_pre : nullptr, single ? ctx->d_tot : nullptr,
+                       single ? d_row_start : nullptr);
   if (timed) prof_mark(ctx, 1);
-  hipLaunchKernelGGL(okv_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_tile_tot,
-                     ntiles, ctx->d_tile_pre, ctx->d_tot, d_row_start, nblk);
+  if (!single)
+    hipLaunchKernelGGL(okv_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_tile_tot,
+                       ntiles, ctx->d_tile_pre, ctx->d_tot, d_row_start, nblk);
   if (timed) prof_mark(ctx, 2);
   OKV_HIP(hipGetLastError());
   return OKV_OK;
@@ -952,6 +1013,10 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
         case 1: hipLaunchKernelGGL((okv_gather_kernel<1, kThreads>), g, t, 0, ctx->stream, P); break;
         case 5: hipLaunchKernelGGL((okv_gather_kernel<5, kThreads>), g, t, 0, ctx->stream, P); break;
         case 6: hipLaunchKernelGGL((okv_gather_kernel<6, kThreads>), g, t, 0, ctx->stream, P); break;
+        case 7: hipLaunchKernelGGL((okv_gather_kernel<7, kThreads>), g, t, 0, ctx->stream, P); break;
+        case 8: hipLaunchKernelGGL((okv_gather_kernel<8, kThreads>), g, t, 0, ctx->stream, P); break;
+        case 9: hipLaunchKernelGGL((okv_gather_occ_kernel<kThreads, 6>), g, t, 0, ctx->stream, P); break;
+        case 10: hipLaunchKernelGGL((okv_gather_occ_kernel<kThreads, 8>), g, t, 0, ctx->stream, P); break;
         default: hipLaunchKernelGGL((okv_gather_kernel<3, kThreads>), g, t, 0, ctx->stream, P);
       }
     }

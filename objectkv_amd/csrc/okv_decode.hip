@@ -47,6 +47,7 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     uint32_t nblk, int comp, BlockCount* __restrict__ cnt, Prefix* __restrict__ lp,
     Prefix* __restrict__ tile_tot, uint32_t* __restrict__ rec_s, uint32_t* __restrict__ big_list,
     uint32_t* __restrict__ big_count, const int32_t* __restrict__ pre_status, int prefetch,
+    int hdr_t,
     Prefix* __restrict__ single_pre, Totals* __restrict__ single_tot,
     uint64_t* __restrict__ single_row_start) {
   const uint32_t tid = threadIdx.x;
@@ -71,7 +72,14 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     } else {
       const uint64_t len = (comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
       const uint64_t orig = d.original_size;
+      // per record r < kRCap, for pass 3: hdr_t = 0: its position at
+      // rec_s[b * kRCap + r] (u32); hdr_t = 1: its header (klen << 32 | vlen)
+      // at rec_s64[((r / 8) * nblk + b) * 8 + r % 8] -- the lanes of a wave
+      // (consecutive blocks, same r: they step in lockstep) fill whole 64-byte
+      // segments within 8 steps, and a block's first 8 headers are 64
+      // contiguous bytes for the gather
       uint32_t* rec = rec_s + uint64_t(b) * kRCap;
+      uint64_t* hdr = reinterpret_cast<uint64_t*>(rec_s) + uint64_t(b) * 8;
       if (prefetch && orig && len) {
         // up to 32 lines (4 KiB), all issued before any is waited on;
         // addresses clamped into [offset, offset + min(orig, len))
@@ -100,7 +108,11 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
           st = OKV_BLK_PANIC;                // key/value reads (:346-349)
           break;
         }
-        if (rows < kRCap) rec[rows] = uint32_t(p);
+        if (rows < kRCap) {
+          if (hdr_t == 1) hdr[(rows >> 3) * uint64_t(nblk) * 8 + (rows & 7)] = (uint64_t(kl) << 32) | vl;
+          else if (hdr_t == 2) rec_s[((rows >> 4) * uint64_t(nblk) + b) * 16 + (rows & 15)] = uint32_t(p);
+          else rec[rows] = uint32_t(p);
+        }
         rows++;
         kb += kl;
         vb += vl;
@@ -230,7 +242,8 @@ struct CopyParams {
   const BlockCount* cnt;
   const Prefix* lp;
   const Prefix* tile_pre;
-  const uint32_t* rec_s;      // [nblk][kRCap] record positions from pass 1
+  const uint32_t* rec_s;      // pass-1 record positions (u32, block-major) or headers
+                              // (u64 klen << 32 | vlen): see okv_count_kernel
   const uint32_t* big_list;   // blocks with > kRCap rows (or >= 4 GiB walks)
   const uint32_t* big_count;
   uint64_t* row_start;
@@ -251,10 +264,8 @@ struct BlockBase {
   uint64_t row0, kb0, vb0;
   int32_t st;
 };
-__device__ __forceinline__ BlockBase block_base(const CopyParams& P, uint32_t b,
-                                                const BlockCount& c) {
-  const Prefix l = P.lp[b];
-  const Prefix t = P.tile_pre[b / kTile];
+__device__ __forceinline__ BlockBase block_base_of(const CopyParams& P, const BlockCount& c,
+                                                   const Prefix& l, const Prefix& t) {
   BlockBase r;
   r.row0 = t.rows + l.rows;
   r.kb0 = t.kb + l.kb;
@@ -266,6 +277,10 @@ __device__ __forceinline__ BlockBase block_base(const CopyParams& P, uint32_t b,
                           r.vb0 + round16(c.vbytes) > P.val_cap))))
     r.st = OKV_BLK_CAPACITY;
   return r;
+}
+__device__ __forceinline__ BlockBase block_base(const CopyParams& P, uint32_t b,
+                                                const BlockCount& c) {
+  return block_base_of(P, c, P.lp[b], P.tile_pre[b / kTile]);
 }
 
 // Lanes per row for a region whose rows average `avg` bytes.
@@ -284,44 +299,61 @@ struct GatherSmem {
   uint32_t vsb[kRCap];       // likewise for values
 };
 
+// Byte sources for the gather.  rel = position relative to the block start
+// (may be a few bytes negative for windows that begin before a row: those
+// bytes are masked off).  GlobalWin reads the segment in HBM (two aligned
+// 16-byte loads + funnel); LdsWin reads the block's LDS image (two aligned
+// ds_read_b128 + funnel), staged by LDS-DMA.
+struct GlobalWin {
+  const uint8_t* seg;
+  uint64_t seg_bytes;
+  uint64_t off;
+  __device__ __forceinline__ uint4 at(int64_t rel) const {
+    return window16(seg, seg_bytes, int64_t(off) + rel);
+  }
+  __device__ __forceinline__ void header(uint32_t pos, uint32_t& kl, uint32_t& vl) const {
+    header_global(seg, off + pos, kl, vl);
+  }
+};
+struct LdsWin {
+  const uint4* img;  // image base; block byte 0 at byte index `bias`
+  uint32_t bias;
+  __device__ __forceinline__ uint4 at(int64_t rel) const {
+    return load16_lds_b128(img, uint32_t(int64_t(bias) + rel));
+  }
+  __device__ __forceinline__ void header(uint32_t pos, uint32_t& kl, uint32_t& vl) const {
+    header_lds(reinterpret_cast<const uint32_t*>(img), bias + pos, kl, vl);
+  }
+};
+
 // Gather one arena region (keys or values) of a block.  Each wave streams
 // contiguous 1 KiB destination tiles: lane l of tile t writes chunk 64t + l
-// (16 bytes, dwordx4), gathered from the source with two aligned 16-byte
-// loads + byte funnel (window16).  The row holding the chunk's first byte is
-// found by binary search on the lane's first chunk and by linear advance
-// after (chunks only move forward).  A chunk that spills past its row is
-// completed in registers from the following rows; past the region end it is
-// zero (the 16-byte padding).  kU tiles per iteration keep kU windows in
-// flight per lane.
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-
-template <bool kVal, uint32_t kU, bool kShfl, int NT, bool kNTS = false>
-__device__ __forceinline__ void gather_region(const CopyParams& P, const GatherSmem& sm,
-                                              int rows, uint64_t off, uint8_t* __restrict__ arena,
-                                              uint64_t dbase) {
+// (16 bytes, dwordx4).  The row holding the chunk's first byte is found by
+// binary search on the lane's first chunk and by linear advance after
+// (chunks only move forward).  A chunk that spills past its row is completed
+// in registers from the following rows; past the region end it is zero (the
+// 16-byte padding).  kU tiles per iteration keep kU windows in flight per lane.
+// Tiles t0, t0 + ts, ... (< t1) of a region.
+template <bool kVal, class Src, uint32_t kU = 4>
+__device__ __forceinline__ void gather_tiles(const Src& src, const GatherSmem& sm, int rows,
+                                             uint8_t* __restrict__ arena, uint64_t dbase,
+                                             uint32_t t0, uint32_t t1, uint32_t ts) {
   const uint32_t* pre = kVal ? sm.vpre : sm.kpre;
   const uint32_t* sb = kVal ? sm.vsb : sm.ksb;
   const uint32_t total = pre[rows];
   const uint32_t N = (total + 15) >> 4;  // chunks, including the padded tail
-  const uint32_t T = (N + 63) >> 6;      // 1 KiB tiles
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t nw = NT / 64;
-  const uint32_t t0 = uint32_t(uint64_t(T) * wave / nw), t1 = uint32_t(uint64_t(T) * (wave + 1) / nw);
+  const uint32_t lane = threadIdx.x & 63;
   const uint32_t last = uint32_t(rows) - 1;
   uint32_t r = 0;
   bool searched = false;
-  for (uint32_t t = t0; t < t1; t += kU) {
-    uint4 v[kU], hi2[kU];
-    uint32_t rr[kU], shv[kU];
-    bool need2[kU];
-    // phase 1: rows and addresses; issue every load before any data is used.
-    // One aligned 16-byte load per lane; the following 16 bytes come from the
-    // neighbour lane when its line is the next one (same row), otherwise from
-    // a second load issued only on the lanes that need it.
+  for (uint32_t t = t0; t < t1; t += kU * ts) {
+    uint4 v[kU];
+    uint32_t rr[kU];
+    // phase 1: rows and addresses; issue every load before any data is used
 #pragma unroll
     for (uint32_t u = 0; u < kU; ++u) {
-      const uint32_t c = (t + u) * 64 + lane;
-      const bool ok = (t + u) < t1 && c < N;
+      const uint32_t c = (t + u * ts) * 64 + lane;
+      const bool ok = (t + u * ts) < t1 && c < N;
       const uint32_t x = (ok ? c : (t0 * 64 + lane < N ? t0 * 64 + lane : 0)) << 4;
       if (!searched) {  // binary search: r = #{k in [1, rows] : pre[k] <= x}
         uint32_t pos = 0;
@@ -336,34 +368,12 @@ __device__ __forceinline__ void gather_region(const CopyParams& P, const GatherS
         while (r < last && pre[r + 1] <= x) ++r;
       }
       rr[u] = r;
-      const uint64_t src = off + sb[r] + x;
-      if (!kShfl) {  // two aligned 16-byte loads + funnel
-        v[u] = window16(P.seg, P.seg_bytes, int64_t(src));
-        continue;
-      }
-      const uint64_t a = src & ~uint64_t(15);
-      shv[u] = uint32_t(src & 15);
-      const uint32_t na = __shfl_down(uint32_t(a), 1, 64);
-      need2[u] = shv[u] != 0 && !(lane != 63 && na == uint32_t(a) + 16u);
-      v[u] = *reinterpret_cast<const uint4*>(P.seg + a);
-      hi2[u] = make_uint4(0, 0, 0, 0);
-      if (need2[u] && a + 16 < P.seg_bytes) hi2[u] = *reinterpret_cast<const uint4*>(P.seg + a + 16);
-    }
-    // phase 2: neighbour exchange and byte funnel
-#pragma unroll
-    for (uint32_t u = 0; u < kU && kShfl; ++u) {
-      uint4 hi;
-      hi.x = __shfl_down(v[u].x, 1, 64);
-      hi.y = __shfl_down(v[u].y, 1, 64);
-      hi.z = __shfl_down(v[u].z, 1, 64);
-      hi.w = __shfl_down(v[u].w, 1, 64);
-      if (need2[u]) hi = hi2[u];
-      v[u] = funnel32(v[u], hi, shv[u]);
+      v[u] = src.at(int64_t(sb[r]) + int64_t(x));
     }
 #pragma unroll
     for (uint32_t u = 0; u < kU; ++u) {
-      const uint32_t c = (t + u) * 64 + lane;
-      if ((t + u) < t1 && c < N) {
+      const uint32_t c = (t + u * ts) * 64 + lane;
+      if ((t + u * ts) < t1 && c < N) {
         const uint32_t x = c << 4, xe = x + 16;
         uint4 out = v[u];
         const uint32_t ri = rr[u];
@@ -372,107 +382,481 @@ __device__ __forceinline__ void gather_region(const CopyParams& P, const GatherS
           for (uint32_t j = ri + 1; j <= last && pre[j] < xe; ++j) {
             const uint32_t q0 = pre[j], q1 = pre[j + 1];
             if (q1 == q0) continue;
-            const uint4 w = window16(P.seg, P.seg_bytes, int64_t(off + sb[j]) + int64_t(x));
+            const uint4 w = src.at(int64_t(sb[j]) + int64_t(x));
             out = merge_bytes(out, w, int32_t(q0 - x), int32_t((q1 < xe ? q1 : xe) - x));
           }
         }
-        if (kNTS) {
-          const u32x4_t o4 = {out.x, out.y, out.z, out.w};
-          __builtin_nontemporal_store(o4, reinterpret_cast<u32x4_t*>(arena + dbase + uint64_t(x)));
-        } else {
-          *reinterpret_cast<uint4*>(arena + dbase + uint64_t(x)) = out;
-        }
+        *reinterpret_cast<uint4*>(arena + dbase + uint64_t(x)) = out;
       }
     }
   }
 }
 
-template <int V, int NT>
-__device__ __forceinline__ void gather_block(const CopyParams& P, GatherSmem& sm, uint32_t b) {
+// Tiles of a region split over nw waves: contiguous ranges (kIL = false) or
+// interleaved (wave w: w, w + nw, ...).
+template <bool kVal, class Src, uint32_t kU = 4, bool kIL = false>
+__device__ __forceinline__ void gather_region(const Src& src, const GatherSmem& sm, int rows,
+                                              uint8_t* __restrict__ arena, uint64_t dbase,
+                                              uint32_t wave, uint32_t nw) {
+  const uint32_t T = ((kVal ? sm.vpre : sm.kpre)[rows] + 1023) >> 10;  // 1 KiB tiles
+  if (kIL)
+    gather_tiles<kVal, Src, kU>(src, sm, rows, arena, dbase, wave, T, nw);
+  else
+    gather_tiles<kVal, Src, kU>(src, sm, rows, arena, dbase, uint32_t(uint64_t(T) * wave / nw),
+                                uint32_t(uint64_t(T) * (wave + 1) / nw), 1);
+}
+
+// Pass-1 header of record r of block b (hdr_t layout of okv_count_kernel).
+__device__ __forceinline__ uint64_t rec_hv(const CopyParams& P, uint32_t r, uint32_t b) {
+  return reinterpret_cast<const uint64_t*>(P.rec_s)[((r >> 3) * uint64_t(P.nblk) + b) * 8 + (r & 7)];
+}
+
+// Per-block metadata every gather kernel starts from.
+struct BlockMeta {
+  BlockCount c;
+  BlockBase B;
+  uint64_t off;
+};
+__device__ __forceinline__ BlockMeta block_meta(const CopyParams& P, uint32_t b) {
+  BlockMeta m;
+  m.c = P.cnt[b];
+  m.B = block_base(P, b, m.c);
+  m.off = P.descs[b].offset;
+  return m;
+}
+// Block outcome (tid 0) and whether the gather kernels handle its rows
+// (else: nothing to do, or a big block for okv_copy_kernel / okv_index_kernel).
+__device__ __forceinline__ bool block_head(const CopyParams& P, uint32_t b, const BlockMeta& m) {
+  if (threadIdx.x == 0) {
+    P.row_start[b] = m.B.row0;
+    if (P.key_base) P.key_base[b] = m.B.kb0;
+    if (P.val_base) P.val_base[b] = m.B.vb0;
+    P.blk_status[b] = m.B.st;
+  }
+  return m.B.st == OKV_BLK_OK && m.c.rows != 0 && m.c.rows <= uint64_t(kRCap) &&
+         m.c.pend < (uint64_t(1) << 32);
+}
+
+// Row table (wave 0, lane r = row r): wave scans give each row's key/value
+// prefix and its source bias.
+__device__ __forceinline__ void fill_row_table(GatherSmem& sm, int rows, uint32_t rec,
+                                               uint32_t kl, uint32_t vl) {
+  const uint32_t tid = threadIdx.x & 63;
+  const uint32_t ki = wave_incl_scan32(kl, tid), vi = wave_incl_scan32(vl, tid);
+  if (int(tid) < rows) {
+    sm.rec[tid] = rec;
+    sm.kpre[tid] = ki - kl;
+    sm.vpre[tid] = vi - vl;
+    sm.ksb[tid] = rec + 6 - (ki - kl);       // >= 0: earlier keys precede rec
+    sm.vsb[tid] = rec + 6 + kl - (vi - vl);  // >= 0: earlier values precede rec
+    if (int(tid) == rows - 1) {
+      sm.rec[rows] = rec + 6 + kl + vl;
+      sm.kpre[rows] = ki;
+      sm.vpre[rows] = vi;
+    }
+  }
+}
+// ... from headers read at the pass-1 positions
+template <class Src>
+__device__ __forceinline__ void build_row_table(const Src& src, GatherSmem& sm, int rows,
+                                                uint32_t rec) {
+  uint32_t kl = 0, vl = 0;
+  if (int(threadIdx.x & 63) < rows) src.header(rec, kl, vl);
+  fill_row_table(sm, rows, rec, kl, vl);
+}
+// ... from the pass-1 headers (hv = klen << 32 | vlen): positions by a scan
+__device__ __forceinline__ void build_row_table_hv(GatherSmem& sm, int rows, uint64_t hv) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t kl = int(lane) < rows ? uint32_t(hv >> 32) : 0u;
+  const uint32_t vl = int(lane) < rows ? uint32_t(hv) : 0u;
+  const uint32_t sz = int(lane) < rows ? 6u + kl + vl : 0u;
+  fill_row_table(sm, rows, wave_incl_scan32(sz, lane) - sz, kl, vl);
+}
+
+// SoA row index of a block (lane r = row r).
+__device__ __forceinline__ void write_row_index(const CopyParams& P, const GatherSmem& sm,
+                                                const BlockMeta& m, int rows) {
   const uint32_t tid = threadIdx.x;
-  const BlockCount c = P.cnt[b];
-  const BlockBase B = block_base(P, b, c);
-  if (tid == 0) {
-    P.row_start[b] = B.row0;
-    if (P.key_base) P.key_base[b] = B.kb0;
-    if (P.val_base) P.val_base[b] = B.vb0;
-    P.blk_status[b] = B.st;
+  if (int(tid) >= rows) return;
+  const uint64_t g = m.B.row0 + tid;
+  const uint32_t kl = sm.kpre[tid + 1] - sm.kpre[tid], vl = sm.vpre[tid + 1] - sm.vpre[tid];
+  P.key_len[g] = uint16_t(kl);
+  P.val_len[g] = vl;
+  if (P.index_only) {
+    P.key_off[g] = m.off + sm.rec[tid] + 6;
+    P.val_off[g] = m.off + sm.rec[tid] + 6 + kl;
+  } else {
+    P.key_off[g] = m.B.kb0 + sm.kpre[tid];
+    P.val_off[g] = m.B.vb0 + sm.vpre[tid];
   }
-  if (B.st != OKV_BLK_OK || c.rows == 0 || c.rows > uint64_t(kRCap) ||
-      c.pend >= (uint64_t(1) << 32))
-    return;  // nothing to do, or a big block (okv_copy_kernel)
-  const int rows = int(c.rows);
-  const uint64_t off = P.descs[b].offset;
-  if (tid < 64) {  // row table: lane r holds row r
-    uint32_t rec = 0, kl = 0, vl = 0;
-    if (int(tid) < rows) {
-      rec = P.rec_s[uint64_t(b) * kRCap + tid];
-      header_global(P.seg, off + rec, kl, vl);
-    }
-    const uint32_t ki = wave_incl_scan32(kl, tid), vi = wave_incl_scan32(vl, tid);
-    if (int(tid) < rows) {
-      sm.rec[tid] = rec;
-      sm.kpre[tid] = ki - kl;
-      sm.vpre[tid] = vi - vl;
-      sm.ksb[tid] = rec + 6 - (ki - kl);       // >= 0: earlier keys precede rec
-      sm.vsb[tid] = rec + 6 + kl - (vi - vl);  // >= 0: earlier values precede rec
-      if (int(tid) == rows - 1) {
-        sm.rec[rows] = rec + 6 + kl + vl;
-        sm.kpre[rows] = ki;
-        sm.vpre[rows] = vi;
-      }
-    }
-  }
-  __syncthreads();
-  if (V < 1) return;
-  if (int(tid) < rows) {  // SoA row index
-    const uint64_t g = B.row0 + tid;
-    const uint32_t kl = sm.kpre[tid + 1] - sm.kpre[tid], vl = sm.vpre[tid + 1] - sm.vpre[tid];
-    P.key_len[g] = uint16_t(kl);
-    P.val_len[g] = vl;
-    if (P.index_only) {
-      P.key_off[g] = off + sm.rec[tid] + 6;
-      P.val_off[g] = off + sm.rec[tid] + 6 + kl;
-    } else {
-      P.key_off[g] = B.kb0 + sm.kpre[tid];
-      P.val_off[g] = B.vb0 + sm.vpre[tid];
-    }
-  }
-  if (V < 2 || P.index_only) return;
-  // diagnostic sweep: 3 = window loads x4 (product), 5 = shuffle x2, 6 = shuffle x4,
-  // 7 = nontemporal arena stores, 8 = values before keys
-  constexpr uint32_t kU = V == 5 ? 2 : 4;
-  constexpr bool kShfl = V == 5 || V == 6;
-  constexpr bool kNTS = V == 7;
-  if (V == 8) gather_region<true, kU, kShfl, NT, kNTS>(P, sm, rows, off, P.val_arena, B.vb0);
-  gather_region<false, kU, kShfl, NT, kNTS>(P, sm, rows, off, P.key_arena, B.kb0);
-  if (V != 8) gather_region<true, kU, kShfl, NT, kNTS>(P, sm, rows, off, P.val_arena, B.vb0);
 }
 
-// V selects a diagnostic ablation (tools/ablate.py): 0 row table only,
-// 1 + SoA index, >= 2 the full kernel (the only variant the API uses unless
-// OKV_COPY_VARIANT is set).
-// Grid: one workgroup per block, or a persistent grid striding over blocks.
-// NT = 256 (four waves share a block's tiles) for large blocks; NT = 64 (one
-// wave per block) for small ones, where a block has only a few 1 KiB tiles and
-// the row-table -> gather latency chain is hidden by more blocks in flight.
-template <int V, int NT>
+// Pass 3, global form: one workgroup per block reads the block straight from
+// HBM.  NT = 64 (one wave per block) for small blocks, where a block has only
+// a few 1 KiB tiles and more blocks in flight hide the row-table -> gather
+// latency chain; NT = 256 otherwise.  Record positions: rec_s[b * kRCap + r].
+template <int NT, uint32_t kU = 4, bool kIL = false, bool kHV = false, bool kTouch = false,
+          bool kSeg = false>
 __global__ __launch_bounds__(NT) void okv_gather_kernel(CopyParams P) {
   __shared__ GatherSmem sm;
   for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
-    gather_block<V, NT>(P, sm, b);
+    // kHV: pass-1 headers (hdr_t layout), loaded alongside the metadata
+    const uint64_t hv = kHV && threadIdx.x < 64 ? rec_hv(P, threadIdx.x, b) : 0;
+    const BlockMeta m = block_meta(P, b);
+    if (block_head(P, b, m)) {
+      const int rows = int(m.c.rows);
+      const GlobalWin src{P.seg, P.seg_bytes, m.off};
+      if (threadIdx.x < 64) {
+        if (kHV) {
+          build_row_table_hv(sm, rows, hv);
+        } else {
+          const uint32_t t = threadIdx.x;
+          const uint32_t rec =
+              int(t) < rows ? P.rec_s[kSeg ? ((t >> 4) * uint64_t(P.nblk) + b) * 16 + (t & 15)
+                                           : uint64_t(b) * kRCap + t]
+                            : 0u;
+          build_row_table(src, sm, rows, rec);
+        }
+      } else if (kTouch) {
+        // waves 1..: one dword per 128-B line of the block's record bytes,
+        // all in flight at once, while wave 0 builds the row table: the
+        // gather's loads then find the block on chip
+        const uint64_t end = m.off + m.c.pend;
+        uint32_t acc = 0;
+        for (uint64_t a = (m.off & ~uint64_t(127)) + 128ull * (threadIdx.x - 64); a < end;
+             a += 128ull * (NT - 64)) {
+          const uint64_t q = a < m.off ? m.off & ~uint64_t(3) : a;
+          acc ^= *reinterpret_cast<const uint32_t*>(P.seg + q);
+        }
+        asm volatile("" ::"v"(acc));
+      }
+      __syncthreads();
+      write_row_index(P, sm, m, rows);
+      if (!P.index_only) {
+        gather_region<false, GlobalWin, kU, kIL>(src, sm, rows, P.key_arena, m.B.kb0,
+                                                 threadIdx.x >> 6, NT / 64);
+        gather_region<true, GlobalWin, kU, kIL>(src, sm, rows, P.val_arena, m.B.vb0,
+                                                threadIdx.x >> 6, NT / 64);
+      }
+    }
     if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
   }
 }
 
-// Occupancy ablation (OKV_COPY_VARIANT 9 / 10): the product kernel with a
-// register budget for W waves per SIMD.
-template <int NT, int W>
-__global__ __launch_bounds__(NT, W) void okv_gather_occ_kernel(CopyParams P) {
-  __shared__ GatherSmem sm;
-  for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
-    gather_block<3, NT>(P, sm, b);
-    if (b + gridDim.x < P.nblk) __syncthreads();
+// Pass 3, staged form (large blocks): a persistent workgroup copies each
+// block's record bytes [offset, offset + pend) into an LDS image with LDS-DMA
+// (global_load_lds_dwordx4: 1 KiB per wave instruction, no VGPR round trip),
+// builds the row table from the image and assembles every arena chunk from
+// LDS, so each source line leaves HBM once (the global form re-reads the
+// header/key lines that the key and value passes share).  64 KiB + 1 KiB of
+// image per workgroup -> two workgroups per CU: while one waits on its DMA
+// the other streams stores.  Record positions: rec_s[r * nblk + b] (written
+// coalesced by pass 1).  Blocks whose walk does not fit the image use the
+// HBM window source.
+constexpr uint32_t kImgBytes = 65 * 1024;
+struct __align__(16) StagedSmem {
+  uint4 img[(kImgBytes + 32) / 16 + 1];  // [16 B guard][image][guard]
+  GatherSmem t;
+};
+#define OKV_LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+__global__ __launch_bounds__(kThreads) void okv_gather_lds_kernel(CopyParams P) {
+  __shared__ StagedSmem sm;
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  uint32_t b = blockIdx.x;
+  if (b >= P.nblk) return;
+  BlockMeta m = block_meta(P, b);
+  for (;;) {
+    const uint32_t bn = b + gridDim.x;
+    const bool live = block_head(P, b, m);  // uniform over the workgroup
+    const int rows = int(m.c.rows);
+    const uint32_t shift = uint32_t(m.off & 15);
+    const bool staged = live && shift + m.c.pend <= kImgBytes;
+    if (staged) {
+      const uint64_t base = m.off - shift;  // 16-byte aligned (seg is)
+      const uint32_t np = (shift + uint32_t(m.c.pend) + 1023) >> 10;
+      for (uint32_t p = wave; p < np; p += kThreads / 64) {
+        uint64_t a = base + (uint64_t(p) << 10) + (lane << 4);
+        if (a >= P.seg_bytes) a = base;  // never past the segment; those bytes are unused
+        __builtin_amdgcn_global_load_lds(P.seg + a, OKV_LDS_PTR(sm.img + 1 + p * 64), 16, 0, 0);
+      }
+    }
+    const uint64_t hv = live && int(tid) < rows ? rec_hv(P, tid, b) : 0u;
+    // the next block's metadata loads ride along with this block's DMA
+    BlockMeta mn;
+    if (bn < P.nblk) mn = block_meta(P, bn);
+    if (live) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const LdsWin lsrc{sm.img, 16u + shift};
+      const GlobalWin gsrc{P.seg, P.seg_bytes, m.off};
+      if (tid < 64) build_row_table_hv(sm.t, rows, hv);
+      __syncthreads();
+      write_row_index(P, sm.t, m, rows);
+      if (!P.index_only) {
+        if (staged) {
+          gather_region<false>(lsrc, sm.t, rows, P.key_arena, m.B.kb0, wave, kThreads / 64);
+          gather_region<true>(lsrc, sm.t, rows, P.val_arena, m.B.vb0, wave, kThreads / 64);
+        } else {
+          gather_region<false>(gsrc, sm.t, rows, P.key_arena, m.B.kb0, wave, kThreads / 64);
+          gather_region<true>(gsrc, sm.t, rows, P.val_arena, m.B.vb0, wave, kThreads / 64);
+        }
+      }
+      __syncthreads();  // image and row table are reused by the next block
+    }
+    if (bn >= P.nblk) break;
+    b = bn;
+    m = mn;
+  }
+}
+
+// Workgroup barrier that drains LDS traffic only (no vmcnt wait: loads and
+// stores in flight stay in flight).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Pass 3, streaming form (large blocks): persistent workgroups
+// (as many as are resident) walk blocks b, b + grid, ... straight from HBM.
+// Wave 0 software-pipelines the per-block prologue: while the workgroup
+// gathers block k it has already issued the pass-1 headers of block k+1 and
+// the metadata of block k+2 (vector loads, lane-distributed, so the raw
+// barrier's lgkmcnt wait never covers them), so the dependent
+// cnt -> headers -> gather chain is off the critical path.  Row tables are
+// double-buffered: one barrier per block.
+struct StreamTab {
+  GatherSmem t;
+  uint64_t off, kb0, vb0;
+  int32_t rows;  // 0: nothing to gather
+};
+
+// Lane-distributed metadata of block b: lane j < 14 loads u64 word j of
+// {BlockCount (5), lp[b] (4), tile_pre[b / kTile] (4), descs[b].offset}.
+__device__ __forceinline__ uint64_t meta_word(const CopyParams& P, uint32_t b, uint32_t lane) {
+  const uint64_t* src = lane < 5    ? reinterpret_cast<const uint64_t*>(P.cnt + b) + lane
+                        : lane < 9  ? reinterpret_cast<const uint64_t*>(P.lp + b) + (lane - 5)
+                        : lane < 13 ? reinterpret_cast<const uint64_t*>(P.tile_pre + b / kTile) +
+                                          (lane - 9)
+                                    : &P.descs[b].offset;
+  return *src;
+}
+__device__ __forceinline__ uint64_t lane_u64(uint64_t w, int j) {
+  return uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(w)), j))) |
+         (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(w >> 32)), j))) << 32);
+}
+__device__ __forceinline__ BlockMeta meta_of_words(const CopyParams& P, uint64_t w) {
+  BlockMeta m;
+  m.c.rows = lane_u64(w, 0);
+  m.c.kbytes = lane_u64(w, 1);
+  m.c.vbytes = lane_u64(w, 2);
+  m.c.pend = lane_u64(w, 3);
+  m.c.status = int32_t(uint32_t(lane_u64(w, 4)));
+  m.c.pad = 0;
+  const Prefix l = {lane_u64(w, 5), lane_u64(w, 6), lane_u64(w, 7), lane_u64(w, 8)};
+  const Prefix t = {lane_u64(w, 9), lane_u64(w, 10), lane_u64(w, 11), lane_u64(w, 12)};
+  m.B = block_base_of(P, m.c, l, t);
+  m.off = lane_u64(w, 13);
+  return m;
+}
+// rows of a block the gather kernels handle (0: none)
+__device__ __forceinline__ int gather_rows(const BlockMeta& m) {
+  return m.B.st == OKV_BLK_OK && m.c.rows <= uint64_t(kRCap) && m.c.pend < (uint64_t(1) << 32)
+             ? int(m.c.rows)
+             : 0;
+}
+
+__global__ __launch_bounds__(kThreads) void okv_gather_stream_kernel(CopyParams P) {
+  __shared__ StreamTab tab[2];
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint32_t G = gridDim.x;
+  uint32_t b = blockIdx.x;
+  if (b >= P.nblk) return;
+  uint64_t w_cur = 0, w_next = 0, hv = 0;  // wave 0: metadata words of b, b + G; headers of b
+  if (wave == 0) {
+    w_cur = meta_word(P, b, lane);
+    if (b + G < P.nblk) w_next = meta_word(P, b + G, lane);
+    const BlockMeta m = meta_of_words(P, w_cur);
+    if (int(lane) < gather_rows(m)) hv = rec_hv(P, lane, b);
+  }
+  for (int slot = 0;; slot ^= 1) {
+    const uint32_t bn = b + G;
+    StreamTab& T = tab[slot];
+    if (wave == 0) {
+      const BlockMeta m = meta_of_words(P, w_cur);
+      if (lane == 0) {
+        P.row_start[b] = m.B.row0;
+        if (P.key_base) P.key_base[b] = m.B.kb0;
+        if (P.val_base) P.val_base[b] = m.B.vb0;
+        P.blk_status[b] = m.B.st;
+      }
+      const int rows = gather_rows(m);
+      if (rows) {
+        build_row_table_hv(T.t, rows, hv);
+        write_row_index(P, T.t, m, rows);
+      }
+      if (lane == 0) {
+        T.off = m.off;
+        T.kb0 = m.B.kb0;
+        T.vb0 = m.B.vb0;
+        T.rows = P.index_only ? 0 : rows;
+      }
+      // prefetch: headers of block bn, metadata of block bn + G
+      hv = 0;
+      if (bn < P.nblk) {
+        const BlockMeta mn = meta_of_words(P, w_next);
+        if (int(lane) < gather_rows(mn)) hv = rec_hv(P, lane, bn);
+        w_cur = w_next;
+        if (bn + G < P.nblk) w_next = meta_word(P, bn + G, lane);
+      }
+    }
+    lds_barrier();
+    const int rows = T.rows;
+    if (rows) {
+      const GlobalWin src{P.seg, P.seg_bytes, T.off};
+      gather_region<false>(src, T.t, rows, P.key_arena, T.kb0, wave, kThreads / 64);
+      gather_region<true>(src, T.t, rows, P.val_arena, T.vb0, wave, kThreads / 64);
+    }
+    if (bn >= P.nblk) break;
+    b = bn;
+  }
+}
+
+// Pass 3, tile form (large blocks, the default): one workgroup per 4 KiB of
+// a block's arenas -- the grid is nblk x kTileSlots workgroups, wave w of
+// slot j gathers 1 KiB tiles 4j + w, 4j + w + 4 kTileSlots, ... of the block's
+// value region followed by its key region.  Each wave rebuilds the block's
+// row table from the pass-1 headers into its own LDS slice (no barrier), so a
+// workgroup's whole prologue is one round of independent loads (metadata +
+// headers), and the chip sweeps source and arenas nearly in address order, the
+// way a plain streaming copy does.  Slot -> block is XCD-aware (speed only:
+// the slots of one block share blockIdx % 8, so its metadata, headers and
+// boundary lines are fetched into one L2).
+constexpr uint32_t kTileSlots = 16;
+__global__ __launch_bounds__(kThreads) void okv_gather_tile_kernel(CopyParams P) {
+  __shared__ GatherSmem tabs[kThreads / 64];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t k = blockIdx.x >> 3;
+  const uint32_t b = (k / kTileSlots) * 8 + (blockIdx.x & 7), j = k % kTileSlots;
+  if (b >= P.nblk) return;
+  GatherSmem& sm = tabs[wave];
+  const uint64_t mw = meta_word(P, b, lane);
+  const uint64_t hv = rec_hv(P, lane, b);  // lanes >= rows: unused words (in bounds)
+  const BlockMeta m = meta_of_words(P, mw);
+  const bool lead = j == 0 && wave == 0;
+  if (lead && lane == 0) {
+    P.row_start[b] = m.B.row0;
+    if (P.key_base) P.key_base[b] = m.B.kb0;
+    if (P.val_base) P.val_base[b] = m.B.vb0;
+    P.blk_status[b] = m.B.st;
+  }
+  const int rows = gather_rows(m);
+  if (!rows || (P.index_only && !lead)) return;
+  build_row_table_hv(sm, rows, hv);
+  __builtin_amdgcn_wave_barrier();
+  if (lead) write_row_index(P, sm, m, rows);
+  if (P.index_only) return;
+  const GlobalWin src{P.seg, P.seg_bytes, m.off};
+  const uint32_t Tv = (sm.vpre[rows] + 1023) >> 10, Tk = (sm.kpre[rows] + 1023) >> 10;
+  const uint32_t t0 = j * 4 + wave, ts = kTileSlots * 4;
+  if (t0 < Tv) gather_tiles<true, GlobalWin, 1>(src, sm, rows, P.val_arena, m.B.vb0, t0, Tv, ts);
+  // key tiles continue the same numbering after the value tiles
+  const uint32_t k0 = t0 < Tv ? t0 + ((Tv - t0 + ts - 1) / ts) * ts - Tv : t0 - Tv;
+  if (k0 < Tk) gather_tiles<false, GlobalWin, 1>(src, sm, rows, P.key_arena, m.B.kb0, k0, Tk, ts);
+}
+
+// Pass 3, pipelined staged form: one 512-thread workgroup per CU with two
+// LDS images.  Wave 0 is the loader: it LDS-DMAs block k+1 into the free
+// image, waits for its own DMA only (vmcnt is per wave), builds that block's
+// row table and writes its SoA index, while waves 1-7 assemble block k's
+// arena chunks from the other image.  One raw barrier per block hands the
+// images over; the gatherers never wait on their stores (no vmcnt drain).
+struct PipeInfo {
+  uint64_t off, kb0, vb0;
+  uint32_t rows, shift;
+  int32_t mode;  // 0 skip, 1 staged (LDS image), 2 HBM windows
+};
+struct __align__(16) PipeSmem {
+  uint4 img[2][(kImgBytes + 32) / 16 + 1];
+  GatherSmem t[2];
+  PipeInfo info[2];
+};
+constexpr int kPipeThreads = 512;
+
+
+// Loader side of one block: DMA issue (staged blocks), record positions,
+// wait for this wave's loads, row table + SoA index + block outcome.
+__device__ __forceinline__ void pipe_load(const CopyParams& P, PipeSmem& sm, int slot, uint32_t b,
+                                          const BlockMeta& m) {
+  const uint32_t lane = threadIdx.x;  // wave 0 only
+  const bool live = block_head(P, b, m);
+  const int rows = int(m.c.rows);
+  const uint32_t shift = uint32_t(m.off & 15);
+  const bool staged = live && shift + m.c.pend <= kImgBytes;
+  if (staged) {
+    const uint64_t base = m.off - shift;  // 16-byte aligned (seg is)
+    const uint32_t np = (shift + uint32_t(m.c.pend) + 1023) >> 10;
+    uint4* img = sm.img[slot];
+    for (uint32_t p = 0; p < np; ++p) {
+      uint64_t a = base + (uint64_t(p) << 10) + (lane << 4);
+      if (a >= P.seg_bytes) a = base;  // never past the segment; those bytes are unused
+      __builtin_amdgcn_global_load_lds(P.seg + a, OKV_LDS_PTR(img + 1 + p * 64), 16, 0, 0);
+    }
+  }
+  const uint64_t hv = live && int(lane) < rows ? rec_hv(P, lane, b) : 0u;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (live) {
+    build_row_table_hv(sm.t[slot], rows, hv);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    write_row_index(P, sm.t[slot], m, rows);
+  }
+  if (lane == 0) {
+    PipeInfo in;
+    in.off = m.off;
+    in.kb0 = m.B.kb0;
+    in.vb0 = m.B.vb0;
+    in.rows = uint32_t(rows);
+    in.shift = shift;
+    in.mode = !live || P.index_only ? 0 : staged ? 1 : 2;
+    sm.info[slot] = in;
+  }
+}
+
+__global__ __launch_bounds__(kPipeThreads) void okv_gather_pipe_kernel(CopyParams P) {
+  __shared__ PipeSmem sm;
+  const uint32_t wave = threadIdx.x >> 6;
+  uint32_t b = blockIdx.x;
+  if (b >= P.nblk) return;
+  if (wave == 0) {
+    const BlockMeta m = block_meta(P, b);
+    pipe_load(P, sm, 0, b, m);
+  }
+  lds_barrier();
+  for (int slot = 0;; slot ^= 1) {
+    const uint32_t bn = b + gridDim.x;
+    if (wave == 0) {
+      if (bn < P.nblk) {
+        const BlockMeta m = block_meta(P, bn);
+        pipe_load(P, sm, slot ^ 1, bn, m);
+      }
+    } else {
+      const PipeInfo in = sm.info[slot];
+      if (in.mode) {
+        const int rows = int(in.rows);
+        const GatherSmem& t = sm.t[slot];
+        if (in.mode == 1) {
+          const LdsWin src{sm.img[slot], 16u + in.shift};
+          gather_region<false>(src, t, rows, P.key_arena, in.kb0, wave - 1, kPipeThreads / 64 - 1);
+          gather_region<true>(src, t, rows, P.val_arena, in.vb0, wave - 1, kPipeThreads / 64 - 1);
+        } else {
+          const GlobalWin src{P.seg, P.seg_bytes, in.off};
+          gather_region<false>(src, t, rows, P.key_arena, in.kb0, wave - 1, kPipeThreads / 64 - 1);
+          gather_region<true>(src, t, rows, P.val_arena, in.vb0, wave - 1, kPipeThreads / 64 - 1);
+        }
+      }
+    }
+    lds_barrier();
+    if (bn >= P.nblk) break;
+    b = bn;
   }
 }
 
@@ -854,7 +1238,7 @@ int ensure_blocks(okv_ctx* ctx, uint32_t nblk) {
     (void)hipFree(ctx->d_rec);
     (void)hipFree(ctx->d_big);
   }
-  OKV_HIP(hipMalloc(&ctx->d_rec, n * kRCap * sizeof(uint32_t)));
+  OKV_HIP(hipMalloc(&ctx->d_rec, n * kRCap * sizeof(uint64_t)));
   OKV_HIP(hipMalloc(&ctx->d_big, (n + 1) * sizeof(uint32_t)));
   OKV_HIP(hipMalloc(&ctx->d_cnt, n * sizeof(BlockCount)));
   OKV_HIP(hipMalloc(&ctx->d_lp, n * sizeof(Prefix)));
@@ -926,9 +1310,27 @@ int prepare(okv_ctx* ctx, const uint8_t* d_seg, uint64_t seg_bytes, const Desc* 
   return OKV_OK;
 }
 
-// Launch passes 1 and 2 on device inputs.
+// Pass-3 kernel choice.  The heuristic uses the call's average block span
+// (seg_bytes / nblk: it assumes the blocks tile the segment, which holds for
+// whole-segment decodes; a caller decoding a few blocks of a large segment
+// gets the large-block kernel, which is correct for any block size).
+enum GatherKind { kGatherGlobal64, kGatherGlobal256, kGatherLds, kGatherPipe, kGatherStream, kGatherTile };
+GatherKind choose_gather(const okv_ctx* ctx, const Work& w, uint32_t nblk, bool index_only) {
+  const bool small = nblk && w.seg_bytes / nblk <= 16384;
+  if (ctx->gather_mode == 1 || index_only || (ctx->gather_mode == 0 && small)) {
+    if (ctx->gather_threads) return ctx->gather_threads == 64 ? kGatherGlobal64 : kGatherGlobal256;
+    return small ? kGatherGlobal64 : kGatherGlobal256;
+  }
+  if (ctx->gather_mode == 2) return kGatherLds;
+  if (ctx->gather_mode == 3) return kGatherPipe;
+  if (ctx->gather_mode == 4 || uint64_t(nblk) * kTileSlots >= (1ull << 31)) return kGatherStream;
+  return kGatherTile;
+}
+
+// Launch passes 1 and 2 on device inputs.  rec_t: pass 1 stores record headers
+// (u64, hdr_t layout: the large-block kernels').
 int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_start,
-                bool timed = false) {
+                bool timed = false, int rec_t = 0) {
   int rc = ensure_blocks(ctx, nblk);
   if (rc) return rc;
   const uint32_t ntiles = (nblk + kTile - 1) / kTile;
@@ -941,6 +1343,7 @@ int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_star
     hipLaunchKernelGGL(okv_count_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, w.seg,
                        w.seg_bytes, w.descs, nblk, w.comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
                        ctx->d_rec, ctx->d_big, ctx->d_big + nblk, w.pre, prefetch,
+                       rec_t,
                        single ? ctx->d_tile_pre : nullptr, single ? ctx->d_tot : nullptr,
                        single ? d_row_start : nullptr);
   if (timed) prof_mark(ctx, 1);
@@ -971,7 +1374,9 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   Work w;
   int rc = prepare(ctx, seg, seg_bytes, descs, nblk, comp, index_only, &w);
   if (rc) return rc;
-  rc = launch_plan(ctx, w, nblk, o->row_start, true);
+  const GatherKind gk = choose_gather(ctx, w, nblk, index_only);
+  rc = launch_plan(ctx, w, nblk, o->row_start, true,
+                  gk >= kGatherLds || ctx->gather_variant == 6 ? 1 : ctx->gather_variant == 8 ? 2 : 0);
   if (rc) return rc;
   CopyParams P;
   P.seg = w.seg;
@@ -1000,24 +1405,42 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   P.key_cap = index_only ? 0 : o->key_cap;
   P.val_cap = index_only ? 0 : o->val_cap;
   if (nblk) {
-    const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
-    // one wave per block when blocks average <= 16 KiB (OKV_GATHER_THREADS=64|256 overrides)
-    const uint32_t nt = ctx->gather_threads ? ctx->gather_threads
-                                            : (w.seg_bytes / nblk <= 16384 ? 64u : 256u);
-    if (nt == 64) {
-      hipLaunchKernelGGL((okv_gather_kernel<3, 64>), g, dim3(64), 0, ctx->stream, P);
+    if (gk == kGatherTile) {
+      const uint32_t grid = ((nblk + 7) / 8) * 8 * kTileSlots;
+      hipLaunchKernelGGL(okv_gather_tile_kernel, dim3(grid), dim3(kThreads), 0, ctx->stream, P);
+    } else if (gk == kGatherStream) {
+      // persistent: every resident workgroup slot (register-bound occupancy)
+      const uint32_t grid = ctx->gather_grid ? ctx->gather_grid : ctx->stream_grid;
+      hipLaunchKernelGGL(okv_gather_stream_kernel, dim3(std::min<uint32_t>(nblk, grid)),
+                         dim3(kThreads), 0, ctx->stream, P);
+    } else if (gk == kGatherPipe) {
+      // persistent: one 512-thread workgroup per CU (two LDS images)
+      const uint32_t grid = ctx->gather_grid ? ctx->gather_grid : ctx->n_cu;
+      hipLaunchKernelGGL(okv_gather_pipe_kernel, dim3(std::min<uint32_t>(nblk, grid)),
+                         dim3(kPipeThreads), 0, ctx->stream, P);
+    } else if (gk == kGatherLds) {
+      // persistent: two workgroups per CU (LDS-bound), blocks strided over the grid
+      const uint32_t grid = ctx->gather_grid ? ctx->gather_grid : 2u * ctx->n_cu;
+      hipLaunchKernelGGL(okv_gather_lds_kernel, dim3(std::min<uint32_t>(nblk, grid)),
+                         dim3(kThreads), 0, ctx->stream, P);
     } else {
-      const dim3 t(kThreads);
-      switch (ctx->variant) {  // diagnostic ablations only; 3 is the product kernel
-        case 0: hipLaunchKernelGGL((okv_gather_kernel<0, kThreads>), g, t, 0, ctx->stream, P); break;
-        case 1: hipLaunchKernelGGL((okv_gather_kernel<1, kThreads>), g, t, 0, ctx->stream, P); break;
-        case 5: hipLaunchKernelGGL((okv_gather_kernel<5, kThreads>), g, t, 0, ctx->stream, P); break;
-        case 6: hipLaunchKernelGGL((okv_gather_kernel<6, kThreads>), g, t, 0, ctx->stream, P); break;
-        case 7: hipLaunchKernelGGL((okv_gather_kernel<7, kThreads>), g, t, 0, ctx->stream, P); break;
-        case 8: hipLaunchKernelGGL((okv_gather_kernel<8, kThreads>), g, t, 0, ctx->stream, P); break;
-        case 9: hipLaunchKernelGGL((okv_gather_occ_kernel<kThreads, 6>), g, t, 0, ctx->stream, P); break;
-        case 10: hipLaunchKernelGGL((okv_gather_occ_kernel<kThreads, 8>), g, t, 0, ctx->stream, P); break;
-        default: hipLaunchKernelGGL((okv_gather_kernel<3, kThreads>), g, t, 0, ctx->stream, P);
+      const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
+      if (gk == kGatherGlobal64 && ctx->gather_variant == 8)
+        hipLaunchKernelGGL((okv_gather_kernel<64, 4, false, false, false, true>), g, dim3(64), 0, ctx->stream, P);
+      else if (gk == kGatherGlobal64 && ctx->gather_variant == 6)
+        hipLaunchKernelGGL((okv_gather_kernel<64, 4, false, true>), g, dim3(64), 0, ctx->stream, P);
+      else if (gk == kGatherGlobal64)
+        hipLaunchKernelGGL(okv_gather_kernel<64>, g, dim3(64), 0, ctx->stream, P);
+      else switch (ctx->gather_variant) {  // A/B: tiles per iteration, interleaved tiles
+        case 1: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 4, true>), g, dim3(kThreads), 0, ctx->stream, P); break;
+        case 2: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 2, false>), g, dim3(kThreads), 0, ctx->stream, P); break;
+        case 3: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 8, false>), g, dim3(kThreads), 0, ctx->stream, P); break;
+        case 4: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 2, true>), g, dim3(kThreads), 0, ctx->stream, P); break;
+        case 5: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 8, true>), g, dim3(kThreads), 0, ctx->stream, P); break;
+        case 6: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 4, false, true>), g, dim3(kThreads), 0, ctx->stream, P); break;
+        case 7: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 4, false, false, true>), g, dim3(kThreads), 0, ctx->stream, P); break;
+        case 8: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 4, false, false, false, true>), g, dim3(kThreads), 0, ctx->stream, P); break;
+        default: hipLaunchKernelGGL((okv_gather_kernel<kThreads>), g, dim3(kThreads), 0, ctx->stream, P);
       }
     }
     const uint32_t nbig_grid = std::min<uint32_t>(nblk, 512);
@@ -1142,9 +1565,33 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   if (hipSetDevice(device) != hipSuccess) return nullptr;
   okv_ctx* ctx = new okv_ctx();
   ctx->device = device;
-  if (const char* v = getenv("OKV_COPY_VARIANT")) ctx->variant = atoi(v);
+  // A/B knobs between product kernels (all bit-exact): OKV_GATHER=global|tile|stream|lds|pipe,
+  // OKV_GATHER_THREADS=64|256 (global form), OKV_GATHER_GRID=<workgroups>
+  if (const char* v = getenv("OKV_GATHER")) {
+    if (!strcmp(v, "global")) ctx->gather_mode = 1;
+    else if (!strcmp(v, "lds")) ctx->gather_mode = 2;
+    else if (!strcmp(v, "pipe")) ctx->gather_mode = 3;
+    else if (!strcmp(v, "stream")) ctx->gather_mode = 4;
+    else if (!strcmp(v, "tile")) ctx->gather_mode = 5;
+    else if (strcmp(v, "auto")) { delete ctx; return nullptr; }
+  }
+  if (const char* v = getenv("OKV_GATHER_THREADS")) {
+    ctx->gather_threads = uint32_t(atoi(v));
+    if (ctx->gather_threads != 64 && ctx->gather_threads != 256) { delete ctx; return nullptr; }
+  }
   if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
-  if (const char* v = getenv("OKV_GATHER_THREADS")) ctx->gather_threads = uint32_t(atoi(v));
+  if (const char* v = getenv("OKV_GATHER_VARIANT")) ctx->gather_variant = atoi(v);
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        ncu > 0)
+      ctx->n_cu = uint32_t(ncu);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, okv_gather_stream_kernel, kThreads,
+                                                     0) != hipSuccess || per_cu < 1)
+      per_cu = 4;
+    ctx->stream_grid = uint32_t(per_cu) * ctx->n_cu;
+  }
   if (stream) {
     ctx->stream = static_cast<hipStream_t>(stream);
   } else {

@@ -1,6 +1,12 @@
-"""Diagnostic: interleaved A/B of okv_gather_kernel variants in ONE process
-(cdna_hip_programming.md §5.4 rule 24).  Usage: python tools/ablate.py 3 5 6
-Variant = OKV_COPY_VARIANT value, optional ":grid" suffix for a persistent grid."""
+"""Diagnostic A/B of the pass-3 gather forms, interleaved in ONE process
+(cdna_hip_programming.md §5.4 rule 24), with a bit-equality check of every
+output array between the arms.
+
+usage: python tools/ablate.py [arm ...]     arm = <mode>[:<grid>[:<threads>[:<variant>]]]
+  mode = lds | global (OKV_GATHER), grid = OKV_GATHER_GRID, threads = 64 | 256
+env:   ABL_NBLK (65536), ABL_ROUNDS (5), ABL_KIND (1 = Zipf C3, 0 = fixed C2),
+       ABL_BS (65536), ABL_TH (57344)
+"""
 import os
 import sys
 
@@ -11,46 +17,72 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import objectkv_amd as okv  # noqa: E402
 
-variants = sys.argv[1:] or ["3"]
+arms = sys.argv[1:] or ["global", "lds"]
 nblk = int(os.environ.get("ABL_NBLK", "65536"))
 rounds = int(os.environ.get("ABL_ROUNDS", "5"))
-w = okv.synth_segment(1, 3, nblocks=nblk, threshold=57344, block_size=65536)
+kind = int(os.environ.get("ABL_KIND", "1"))
+bs = int(os.environ.get("ABL_BS", "65536"))
+th = int(os.environ.get("ABL_TH", "57344"))
+w = okv.synth_segment(kind, 3, nblocks=nblk, threshold=th, block_size=bs)
 seg = w.data_view()
 d = w.descs()[:nblk]
 dev = torch.device("cuda", 0)
 stream = torch.cuda.current_stream(dev).cuda_stream
 decs = {}
-for v in variants:
-    var, _, grid = v.partition(":")
-    os.environ["OKV_COPY_VARIANT"] = var
+for a in arms:
+    mode, _, rest = a.partition(":")
+    grid, _, rest = rest.partition(":")
+    thr, _, var = rest.partition(":")
+    os.environ["OKV_GATHER_VARIANT"] = var or "0"
+    os.environ["OKV_GATHER"] = mode
     os.environ["OKV_GATHER_GRID"] = grid or "0"
-    decs[v] = okv.Decoder(0, stream=stream)
+    if thr:
+        os.environ["OKV_GATHER_THREADS"] = thr
+    else:
+        os.environ.pop("OKV_GATHER_THREADS", None)
+    decs[a] = okv.Decoder(0, stream=stream)
 seg_t = torch.empty(seg.nbytes + 64, dtype=torch.uint8, device=dev)
 seg_t[:seg.nbytes].copy_(torch.from_numpy(seg))
 d_t = torch.from_numpy(d.view(np.int64).copy()).to(dev)
-first = decs[variants[0]]
+first = decs[arms[0]]
 rows, kb, vb = first.plan_device(seg_t, seg.nbytes, d_t, nblk)
-out = {k: torch.empty(n, dtype=t, device=dev) for k, n, t in [
-    ("row_start", nblk + 1, torch.int64), ("key_base", nblk, torch.int64),
-    ("val_base", nblk, torch.int64), ("status", nblk, torch.int32),
-    ("key_off", rows, torch.int64), ("key_len", rows, torch.int16),
-    ("val_off", rows, torch.int64), ("val_len", rows, torch.int32),
-    ("key_arena", kb, torch.uint8), ("val_arena", vb, torch.uint8)]}
-res = {v: [] for v in variants}
-for v, dec in decs.items():  # warm up
+
+
+def new_out():
+    return {k: torch.full((n,), 0x5A, dtype=t, device=dev) for k, n, t in [
+        ("row_start", nblk + 1, torch.int64), ("key_base", nblk, torch.int64),
+        ("val_base", nblk, torch.int64), ("status", nblk, torch.int32),
+        ("key_off", rows, torch.int64), ("key_len", rows, torch.int16),
+        ("val_off", rows, torch.int64), ("val_len", rows, torch.int32),
+        ("key_arena", kb, torch.uint8), ("val_arena", vb, torch.uint8)]}
+
+
+outs = {a: new_out() for a in arms}
+for a, dec in decs.items():  # warm up + equality between arms
     for _ in range(2):
-        dec.decode_device(seg_t, seg.nbytes, d_t, nblk, out, sync=False)
+        dec.decode_device(seg_t, seg.nbytes, d_t, nblk, outs[a], sync=False)
 torch.cuda.synchronize()
+ref = outs[arms[0]]
+for a in arms[1:]:
+    bad = [k for k in ref if not torch.equal(ref[k], outs[a][k])]
+    print(f"arm {a} vs {arms[0]}: {'EQUAL' if not bad else 'DIFFER ' + ','.join(bad)}",
+          flush=True)
+del outs
+out = new_out()
+res = {a: [] for a in arms}
 for r in range(rounds):
-    for v, dec in decs.items():
+    for a, dec in decs.items():
         dec.profile(True)
         for _ in range(5):
             dec.decode_device(seg_t, seg.nbytes, d_t, nblk, out, sync=False)
         ms, n = dec.profile_read()
         dec.profile(False)
-        res[v].append((ms["copy"] / n, ms["count"] / n))
-for v in variants:
-    cp = sorted(x[0] for x in res[v])
-    ct = sorted(x[1] for x in res[v])
-    print(f"variant={v} copy_ms median={cp[len(cp) // 2]:.4f} min={cp[0]:.4f} "
-          f"count_ms median={ct[len(ct) // 2]:.4f}", flush=True)
+        res[a].append((ms["copy"] / n, ms["count"] / n))
+alg = int(d[:, 2].sum()) + kb + vb + rows * 22 + nblk * 28
+for a in arms:
+    cp = sorted(x[0] for x in res[a])
+    ct = sorted(x[1] for x in res[a])
+    med = cp[len(cp) // 2]
+    print(f"arm={a:16s} gather_ms median={med:.4f} min={cp[0]:.4f} "
+          f"count_ms median={ct[len(ct) // 2]:.4f}  alg {alg / med / 1e6:.0f} GB/s "
+          f"frac {alg / med / 1e6 / 8000:.3f}", flush=True)

@@ -48,9 +48,13 @@ extern "C" {
 
 /* ---- SegmentWriter ------------------------------------------------------- */
 typedef struct okv_writer okv_writer;
-/* SegmentWriterOptions (segment_writer_option.go:5-16).  BloomFilter is not
- * supported (bloom bytes are parity-unpinned). */
+/* SegmentWriterOptions (segment_writer_option.go:5-16). */
 okv_writer *okv_writer_new(uint64_t threshold_bytes, uint64_t block_size, int zstd_level, int lz4);
+/* options.BloomFilter != nil (segment_writer_option.go:20): the meta block
+ * carries [1][u64 LE len][bytes] (segment_writer.go:295-300).  bytes =
+ * BloomFilter.WriteTo, computed by the caller (BloomFilter.Add per row,
+ * :133-136); an opaque pass-through here.  Call any time before Close. */
+void okv_writer_set_bloom(okv_writer *w, const uint8_t *bytes, uint64_t len);
 int okv_writer_write_row(okv_writer *w, const uint8_t *key, size_t klen, const uint8_t *val,
                          size_t vlen);
 /* Close (segment_writer.go:211-282).  strict_go != 0 reproduces the Go panic

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OKV_ABI_VERSION 1
+#define OKV_ABI_VERSION 2 /* 2: okv_encode_opts.bloom / bloom_len */
 
 /* ---- return codes (int) -------------------------------------------------- */
 #define OKV_OK 0
@@ -188,8 +188,10 @@ typedef struct okv_rows {
   uint64_t key_arena_bytes, val_arena_bytes;
 } okv_rows;
 
-/* SegmentWriterOptions (segment_writer_option.go:5-16).  BloomFilter is not
- * supported (writes bloom byte 0, as BloomFilter == nil). */
+/* SegmentWriterOptions (segment_writer_option.go:5-16).  The bloom filter is
+ * an opaque pass-through: the caller runs BloomFilter.Add per row
+ * (segment_writer.go:133-136) and hands over BloomFilter.WriteTo's bytes; the
+ * meta block then carries [1][u64 LE length][bytes] (:295-300), else [0]. */
 typedef struct okv_encode_opts {
   uint64_t threshold_bytes; /* DataBlockThresholdBytes (default 3584) */
   uint64_t block_size;      /* DataBlockSize (default 4096) */
@@ -198,6 +200,8 @@ typedef struct okv_encode_opts {
                                OKV_COMP_ZSTD -> OKV_W_UNSUPPORTED */
   int strict_go;            /* 1: a Close with no open block panics in Go (Q1) ->
                                OKV_W_NIL_WRITER; 0: write the footer normally */
+  const uint8_t *bloom;     /* host bytes of BloomFilter.WriteTo, or NULL (BloomFilter nil) */
+  uint64_t bloom_len;
 } okv_encode_opts;
 
 /* Output: the segment file, written as the Go writer writes it:
@@ -325,10 +329,11 @@ int okv_merge_rows(okv_ctx *ctx, const okv_merge_src *srcs, uint32_t nsrc,
                    const okv_merge_opts *opts, okv_merge_out *out, uint32_t flags);
 
 /* Per-kernel timing with HIP events recorded on the context stream around
- * each launch of okv_decode_blocks (pass 1 count, pass 2 scan, pass 3
- * copy/index).  okv_profile(ctx, 1) enables and resets; okv_profile_read
- * synchronises the stream and returns the summed milliseconds per pass
- * (ms[3]) and the number of decode calls timed. */
+ * each stage of okv_decode_blocks.  okv_profile(ctx, 1) enables and resets;
+ * okv_profile_read synchronises the stream and returns the summed
+ * milliseconds per stage, ms[4] = {pass 1 count, pass 2 scan, pass 3 gather
+ * (+ big-block copy / index), zstd decompression (0 for uncompressed)}, and
+ * the number of decode calls timed. */
 int okv_profile(okv_ctx *ctx, int enable);
 int okv_profile_read(okv_ctx *ctx, double *ms, uint64_t *calls);
 

@@ -35,6 +35,7 @@ SYMBOLS = [
     "okv_synth_rows_fixed", "okv_merge_rows",
     "okv_writer_new", "okv_writer_write_row", "okv_writer_close", "okv_writer_data",
     "okv_writer_meta", "okv_writer_num_blocks", "okv_writer_block", "okv_writer_free",
+    "okv_writer_set_bloom",
     "okv_meta_fetch", "okv_meta_parse", "okv_meta_num_blocks", "okv_meta_compression",
     "okv_meta_descs", "okv_meta_first_key", "okv_meta_last_key", "okv_meta_block",
     "okv_meta_free", "okv_synth_segment",
@@ -73,7 +74,8 @@ class Rows(C.Structure):
 
 class EncodeOpts(C.Structure):
     _fields_ = [("threshold_bytes", C.c_uint64), ("block_size", C.c_uint64),
-                ("compression", C.c_int), ("strict_go", C.c_int)]
+                ("compression", C.c_int), ("strict_go", C.c_int), ("bloom", C.c_void_p),
+                ("bloom_len", C.c_uint64)]
 
 
 class EncodeOut(C.Structure):
@@ -171,6 +173,7 @@ def lib():
         "okv_writer_block": (i32, [p, u64, C.POINTER(BlockDesc), C.POINTER(u64),
                                    C.POINTER(p), C.POINTER(u64)]),
         "okv_writer_free": (None, [p]),
+        "okv_writer_set_bloom": (None, [p, p, u64]),
         "okv_meta_fetch": (i32, [p, u64, C.c_int64, C.POINTER(p)]),
         "okv_meta_parse": (i32, [p, u64, C.POINTER(p)]),
         "okv_meta_num_blocks": (u64, [p]),

@@ -39,7 +39,7 @@ struct okv_ctx {
   okv::Prefix* d_lp = nullptr;
   okv::Prefix* d_tile_tot = nullptr;
   okv::Prefix* d_tile_pre = nullptr;
-  uint32_t* d_rec = nullptr;       // nblk x kRCap record positions (pass 1)
+  uint32_t* d_rec = nullptr;       // nblk x kRCap record positions (pass 1, rec_index)
   uint32_t* d_big = nullptr;       // big-block list + its counter (d_big[nblk])
   size_t cap_blocks = 0;
   okv::Totals* d_tot = nullptr;
@@ -54,16 +54,12 @@ struct okv_ctx {
   uint64_t* d_hash = nullptr;
   size_t cap_hash = 0;
   // per-pass event timing (okv_profile)
-  int gather_mode = 0;  // 0 auto, 1 global, 2 LDS-staged, 3 pipelined LDS, 4 stream (OKV_GATHER)
   uint32_t gather_grid = 0;  // 0: default grid; else workgroups (OKV_GATHER_GRID)
   uint32_t gather_threads = 0;  // 0: by average block size; else 64 or 256 (OKV_GATHER_THREADS)
-  int gather_variant = 0;    // A/B (OKV_GATHER_VARIANT)
-  uint32_t n_cu = 256;       // compute units (persistent grids)
-  uint32_t stream_grid = 1024;  // resident workgroups of okv_gather_stream_kernel
   bool prof = false;
-  std::vector<hipEvent_t> ev;  // 4 per timed call
+  std::vector<hipEvent_t> ev;  // 5 per timed call
   size_t ev_used = 0;
-  double prof_ms[3] = {0, 0, 0};
+  double prof_ms[4] = {0, 0, 0, 0};  // count, scan, gather, zstd stage
   uint64_t prof_calls = 0;
   okv::EncScratch* enc = nullptr;  // encode scratch (okv_encode.hip)
   okv::mrg::Scratch* merge = nullptr;  // merge scratch (okv_merge.hip)

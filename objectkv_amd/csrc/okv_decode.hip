@@ -34,6 +34,12 @@
 
 namespace okv {
 
+// Record positions from pass 1: record r < kRCap of block b at
+// [r / 16][block][r % 16] -- 64-byte segments of 16 records per block.
+__device__ __forceinline__ uint64_t rec_index(uint32_t nblk, uint32_t b, uint32_t r) {
+  return ((r >> 4) * uint64_t(nblk) + b) * 16 + (r & 15);
+}
+
 // ---------------------------------------------------------------------------
 // Pass 1: header walk in HBM, one lane per block.
 // ---------------------------------------------------------------------------
@@ -47,7 +53,7 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     uint32_t nblk, int comp, BlockCount* __restrict__ cnt, Prefix* __restrict__ lp,
     Prefix* __restrict__ tile_tot, uint32_t* __restrict__ rec_s, uint32_t* __restrict__ big_list,
     uint32_t* __restrict__ big_count, const int32_t* __restrict__ pre_status, int prefetch,
-    int hdr_t,
+
     Prefix* __restrict__ single_pre, Totals* __restrict__ single_tot,
     uint64_t* __restrict__ single_row_start) {
   const uint32_t tid = threadIdx.x;
@@ -72,14 +78,9 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     } else {
       const uint64_t len = (comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
       const uint64_t orig = d.original_size;
-      // per record r < kRCap, for pass 3: hdr_t = 0: its position at
-      // rec_s[b * kRCap + r] (u32); hdr_t = 1: its header (klen << 32 | vlen)
-      // at rec_s64[((r / 8) * nblk + b) * 8 + r % 8] -- the lanes of a wave
-      // (consecutive blocks, same r: they step in lockstep) fill whole 64-byte
-      // segments within 8 steps, and a block's first 8 headers are 64
-      // contiguous bytes for the gather
-      uint32_t* rec = rec_s + uint64_t(b) * kRCap;
-      uint64_t* hdr = reinterpret_cast<uint64_t*>(rec_s) + uint64_t(b) * 8;
+      // position of record r < kRCap for pass 3 at rec_s[rec_index(nblk, b, r)]:
+      // the lanes of a wave (consecutive blocks, same r: they step in
+      // lockstep) fill whole 64-byte segments within 16 steps
       if (prefetch && orig && len) {
         // up to 32 lines (4 KiB), all issued before any is waited on;
         // addresses clamped into [offset, offset + min(orig, len))
@@ -109,9 +110,7 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
           break;
         }
         if (rows < kRCap) {
-          if (hdr_t == 1) hdr[(rows >> 3) * uint64_t(nblk) * 8 + (rows & 7)] = (uint64_t(kl) << 32) | vl;
-          else if (hdr_t == 2) rec_s[((rows >> 4) * uint64_t(nblk) + b) * 16 + (rows & 15)] = uint32_t(p);
-          else rec[rows] = uint32_t(p);
+          rec_s[rec_index(nblk, b, uint32_t(rows))] = uint32_t(p);
         }
         rows++;
         kb += kl;
@@ -299,11 +298,9 @@ struct GatherSmem {
   uint32_t vsb[kRCap];       // likewise for values
 };
 
-// Byte sources for the gather.  rel = position relative to the block start
-// (may be a few bytes negative for windows that begin before a row: those
-// bytes are masked off).  GlobalWin reads the segment in HBM (two aligned
-// 16-byte loads + funnel); LdsWin reads the block's LDS image (two aligned
-// ds_read_b128 + funnel), staged by LDS-DMA.
+// Byte source for the gather: the segment in HBM (two aligned 16-byte loads +
+// funnel).  rel = position relative to the block start (may be a few bytes
+// negative for windows that begin before a row: those bytes are masked off).
 struct GlobalWin {
   const uint8_t* seg;
   uint64_t seg_bytes;
@@ -315,17 +312,6 @@ struct GlobalWin {
     header_global(seg, off + pos, kl, vl);
   }
 };
-struct LdsWin {
-  const uint4* img;  // image base; block byte 0 at byte index `bias`
-  uint32_t bias;
-  __device__ __forceinline__ uint4 at(int64_t rel) const {
-    return load16_lds_b128(img, uint32_t(int64_t(bias) + rel));
-  }
-  __device__ __forceinline__ void header(uint32_t pos, uint32_t& kl, uint32_t& vl) const {
-    header_lds(reinterpret_cast<const uint32_t*>(img), bias + pos, kl, vl);
-  }
-};
-
 // Gather one arena region (keys or values) of a block.  Each wave streams
 // contiguous 1 KiB destination tiles: lane l of tile t writes chunk 64t + l
 // (16 bytes, dwordx4).  The row holding the chunk's first byte is found by
@@ -392,23 +378,15 @@ __device__ __forceinline__ void gather_tiles(const Src& src, const GatherSmem& s
   }
 }
 
-// Tiles of a region split over nw waves: contiguous ranges (kIL = false) or
-// interleaved (wave w: w, w + nw, ...).
-template <bool kVal, class Src, uint32_t kU = 4, bool kIL = false>
+// Tiles of a region split over nw waves in contiguous ranges (measured:
+// interleaving the tiles over the waves, 2 or 8 tiles per iteration are slower).
+template <bool kVal, class Src>
 __device__ __forceinline__ void gather_region(const Src& src, const GatherSmem& sm, int rows,
                                               uint8_t* __restrict__ arena, uint64_t dbase,
                                               uint32_t wave, uint32_t nw) {
   const uint32_t T = ((kVal ? sm.vpre : sm.kpre)[rows] + 1023) >> 10;  // 1 KiB tiles
-  if (kIL)
-    gather_tiles<kVal, Src, kU>(src, sm, rows, arena, dbase, wave, T, nw);
-  else
-    gather_tiles<kVal, Src, kU>(src, sm, rows, arena, dbase, uint32_t(uint64_t(T) * wave / nw),
-                                uint32_t(uint64_t(T) * (wave + 1) / nw), 1);
-}
-
-// Pass-1 header of record r of block b (hdr_t layout of okv_count_kernel).
-__device__ __forceinline__ uint64_t rec_hv(const CopyParams& P, uint32_t r, uint32_t b) {
-  return reinterpret_cast<const uint64_t*>(P.rec_s)[((r >> 3) * uint64_t(P.nblk) + b) * 8 + (r & 7)];
+  gather_tiles<kVal, Src>(src, sm, rows, arena, dbase, uint32_t(uint64_t(T) * wave / nw),
+                          uint32_t(uint64_t(T) * (wave + 1) / nw), 1);
 }
 
 // Per-block metadata every gather kernel starts from.
@@ -464,15 +442,6 @@ __device__ __forceinline__ void build_row_table(const Src& src, GatherSmem& sm, 
   if (int(threadIdx.x & 63) < rows) src.header(rec, kl, vl);
   fill_row_table(sm, rows, rec, kl, vl);
 }
-// ... from the pass-1 headers (hv = klen << 32 | vlen): positions by a scan
-__device__ __forceinline__ void build_row_table_hv(GatherSmem& sm, int rows, uint64_t hv) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t kl = int(lane) < rows ? uint32_t(hv >> 32) : 0u;
-  const uint32_t vl = int(lane) < rows ? uint32_t(hv) : 0u;
-  const uint32_t sz = int(lane) < rows ? 6u + kl + vl : 0u;
-  fill_row_table(sm, rows, wave_incl_scan32(sz, lane) - sz, kl, vl);
-}
-
 // SoA row index of a block (lane r = row r).
 __device__ __forceinline__ void write_row_index(const CopyParams& P, const GatherSmem& sm,
                                                 const BlockMeta& m, int rows) {
@@ -491,372 +460,32 @@ __device__ __forceinline__ void write_row_index(const CopyParams& P, const Gathe
   }
 }
 
-// Pass 3, global form: one workgroup per block reads the block straight from
-// HBM.  NT = 64 (one wave per block) for small blocks, where a block has only
-// a few 1 KiB tiles and more blocks in flight hide the row-table -> gather
-// latency chain; NT = 256 otherwise.  Record positions: rec_s[b * kRCap + r].
-template <int NT, uint32_t kU = 4, bool kIL = false, bool kHV = false, bool kTouch = false,
-          bool kSeg = false>
+// Pass 3: one workgroup per block reads the block straight from HBM.  NT = 64
+// (one wave per block) for small blocks, where a block has only a few 1 KiB
+// tiles and more blocks in flight hide the row-table -> gather latency chain;
+// NT = 256 otherwise.  The row table's header reads also pull the record
+// boundary lines on chip just before the key and value passes need them.
+template <int NT>
 __global__ __launch_bounds__(NT) void okv_gather_kernel(CopyParams P) {
   __shared__ GatherSmem sm;
   for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
-    // kHV: pass-1 headers (hdr_t layout), loaded alongside the metadata
-    const uint64_t hv = kHV && threadIdx.x < 64 ? rec_hv(P, threadIdx.x, b) : 0;
     const BlockMeta m = block_meta(P, b);
     if (block_head(P, b, m)) {
       const int rows = int(m.c.rows);
       const GlobalWin src{P.seg, P.seg_bytes, m.off};
       if (threadIdx.x < 64) {
-        if (kHV) {
-          build_row_table_hv(sm, rows, hv);
-        } else {
-          const uint32_t t = threadIdx.x;
-          const uint32_t rec =
-              int(t) < rows ? P.rec_s[kSeg ? ((t >> 4) * uint64_t(P.nblk) + b) * 16 + (t & 15)
-                                           : uint64_t(b) * kRCap + t]
-                            : 0u;
-          build_row_table(src, sm, rows, rec);
-        }
-      } else if (kTouch) {
-        // waves 1..: one dword per 128-B line of the block's record bytes,
-        // all in flight at once, while wave 0 builds the row table: the
-        // gather's loads then find the block on chip
-        const uint64_t end = m.off + m.c.pend;
-        uint32_t acc = 0;
-        for (uint64_t a = (m.off & ~uint64_t(127)) + 128ull * (threadIdx.x - 64); a < end;
-             a += 128ull * (NT - 64)) {
-          const uint64_t q = a < m.off ? m.off & ~uint64_t(3) : a;
-          acc ^= *reinterpret_cast<const uint32_t*>(P.seg + q);
-        }
-        asm volatile("" ::"v"(acc));
+        const uint32_t t = threadIdx.x;
+        const uint32_t rec = int(t) < rows ? P.rec_s[rec_index(P.nblk, b, t)] : 0u;
+        build_row_table(src, sm, rows, rec);
       }
       __syncthreads();
       write_row_index(P, sm, m, rows);
       if (!P.index_only) {
-        gather_region<false, GlobalWin, kU, kIL>(src, sm, rows, P.key_arena, m.B.kb0,
-                                                 threadIdx.x >> 6, NT / 64);
-        gather_region<true, GlobalWin, kU, kIL>(src, sm, rows, P.val_arena, m.B.vb0,
-                                                threadIdx.x >> 6, NT / 64);
+        gather_region<false>(src, sm, rows, P.key_arena, m.B.kb0, threadIdx.x >> 6, NT / 64);
+        gather_region<true>(src, sm, rows, P.val_arena, m.B.vb0, threadIdx.x >> 6, NT / 64);
       }
     }
     if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
-  }
-}
-
-// Pass 3, staged form (large blocks): a persistent workgroup copies each
-// block's record bytes [offset, offset + pend) into an LDS image with LDS-DMA
-// (global_load_lds_dwordx4: 1 KiB per wave instruction, no VGPR round trip),
-// builds the row table from the image and assembles every arena chunk from
-// LDS, so each source line leaves HBM once (the global form re-reads the
-// header/key lines that the key and value passes share).  64 KiB + 1 KiB of
-// image per workgroup -> two workgroups per CU: while one waits on its DMA
-// the other streams stores.  Record positions: rec_s[r * nblk + b] (written
-// coalesced by pass 1).  Blocks whose walk does not fit the image use the
-// HBM window source.
-constexpr uint32_t kImgBytes = 65 * 1024;
-struct __align__(16) StagedSmem {
-  uint4 img[(kImgBytes + 32) / 16 + 1];  // [16 B guard][image][guard]
-  GatherSmem t;
-};
-#define OKV_LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
-
-__global__ __launch_bounds__(kThreads) void okv_gather_lds_kernel(CopyParams P) {
-  __shared__ StagedSmem sm;
-  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  uint32_t b = blockIdx.x;
-  if (b >= P.nblk) return;
-  BlockMeta m = block_meta(P, b);
-  for (;;) {
-    const uint32_t bn = b + gridDim.x;
-    const bool live = block_head(P, b, m);  // uniform over the workgroup
-    const int rows = int(m.c.rows);
-    const uint32_t shift = uint32_t(m.off & 15);
-    const bool staged = live && shift + m.c.pend <= kImgBytes;
-    if (staged) {
-      const uint64_t base = m.off - shift;  // 16-byte aligned (seg is)
-      const uint32_t np = (shift + uint32_t(m.c.pend) + 1023) >> 10;
-      for (uint32_t p = wave; p < np; p += kThreads / 64) {
-        uint64_t a = base + (uint64_t(p) << 10) + (lane << 4);
-        if (a >= P.seg_bytes) a = base;  // never past the segment; those bytes are unused
-        __builtin_amdgcn_global_load_lds(P.seg + a, OKV_LDS_PTR(sm.img + 1 + p * 64), 16, 0, 0);
-      }
-    }
-    const uint64_t hv = live && int(tid) < rows ? rec_hv(P, tid, b) : 0u;
-    // the next block's metadata loads ride along with this block's DMA
-    BlockMeta mn;
-    if (bn < P.nblk) mn = block_meta(P, bn);
-    if (live) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      const LdsWin lsrc{sm.img, 16u + shift};
-      const GlobalWin gsrc{P.seg, P.seg_bytes, m.off};
-      if (tid < 64) build_row_table_hv(sm.t, rows, hv);
-      __syncthreads();
-      write_row_index(P, sm.t, m, rows);
-      if (!P.index_only) {
-        if (staged) {
-          gather_region<false>(lsrc, sm.t, rows, P.key_arena, m.B.kb0, wave, kThreads / 64);
-          gather_region<true>(lsrc, sm.t, rows, P.val_arena, m.B.vb0, wave, kThreads / 64);
-        } else {
-          gather_region<false>(gsrc, sm.t, rows, P.key_arena, m.B.kb0, wave, kThreads / 64);
-          gather_region<true>(gsrc, sm.t, rows, P.val_arena, m.B.vb0, wave, kThreads / 64);
-        }
-      }
-      __syncthreads();  // image and row table are reused by the next block
-    }
-    if (bn >= P.nblk) break;
-    b = bn;
-    m = mn;
-  }
-}
-
-// Workgroup barrier that drains LDS traffic only (no vmcnt wait: loads and
-// stores in flight stay in flight).
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-// Pass 3, streaming form (large blocks): persistent workgroups
-// (as many as are resident) walk blocks b, b + grid, ... straight from HBM.
-// Wave 0 software-pipelines the per-block prologue: while the workgroup
-// gathers block k it has already issued the pass-1 headers of block k+1 and
-// the metadata of block k+2 (vector loads, lane-distributed, so the raw
-// barrier's lgkmcnt wait never covers them), so the dependent
-// cnt -> headers -> gather chain is off the critical path.  Row tables are
-// double-buffered: one barrier per block.
-struct StreamTab {
-  GatherSmem t;
-  uint64_t off, kb0, vb0;
-  int32_t rows;  // 0: nothing to gather
-};
-
-// Lane-distributed metadata of block b: lane j < 14 loads u64 word j of
-// {BlockCount (5), lp[b] (4), tile_pre[b / kTile] (4), descs[b].offset}.
-__device__ __forceinline__ uint64_t meta_word(const CopyParams& P, uint32_t b, uint32_t lane) {
-  const uint64_t* src = lane < 5    ? reinterpret_cast<const uint64_t*>(P.cnt + b) + lane
-                        : lane < 9  ? reinterpret_cast<const uint64_t*>(P.lp + b) + (lane - 5)
-                        : lane < 13 ? reinterpret_cast<const uint64_t*>(P.tile_pre + b / kTile) +
-                                          (lane - 9)
-                                    : &P.descs[b].offset;
-  return *src;
-}
-__device__ __forceinline__ uint64_t lane_u64(uint64_t w, int j) {
-  return uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(w)), j))) |
-         (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(w >> 32)), j))) << 32);
-}
-__device__ __forceinline__ BlockMeta meta_of_words(const CopyParams& P, uint64_t w) {
-  BlockMeta m;
-  m.c.rows = lane_u64(w, 0);
-  m.c.kbytes = lane_u64(w, 1);
-  m.c.vbytes = lane_u64(w, 2);
-  m.c.pend = lane_u64(w, 3);
-  m.c.status = int32_t(uint32_t(lane_u64(w, 4)));
-  m.c.pad = 0;
-  const Prefix l = {lane_u64(w, 5), lane_u64(w, 6), lane_u64(w, 7), lane_u64(w, 8)};
-  const Prefix t = {lane_u64(w, 9), lane_u64(w, 10), lane_u64(w, 11), lane_u64(w, 12)};
-  m.B = block_base_of(P, m.c, l, t);
-  m.off = lane_u64(w, 13);
-  return m;
-}
-// rows of a block the gather kernels handle (0: none)
-__device__ __forceinline__ int gather_rows(const BlockMeta& m) {
-  return m.B.st == OKV_BLK_OK && m.c.rows <= uint64_t(kRCap) && m.c.pend < (uint64_t(1) << 32)
-             ? int(m.c.rows)
-             : 0;
-}
-
-__global__ __launch_bounds__(kThreads) void okv_gather_stream_kernel(CopyParams P) {
-  __shared__ StreamTab tab[2];
-  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const uint32_t G = gridDim.x;
-  uint32_t b = blockIdx.x;
-  if (b >= P.nblk) return;
-  uint64_t w_cur = 0, w_next = 0, hv = 0;  // wave 0: metadata words of b, b + G; headers of b
-  if (wave == 0) {
-    w_cur = meta_word(P, b, lane);
-    if (b + G < P.nblk) w_next = meta_word(P, b + G, lane);
-    const BlockMeta m = meta_of_words(P, w_cur);
-    if (int(lane) < gather_rows(m)) hv = rec_hv(P, lane, b);
-  }
-  for (int slot = 0;; slot ^= 1) {
-    const uint32_t bn = b + G;
-    StreamTab& T = tab[slot];
-    if (wave == 0) {
-      const BlockMeta m = meta_of_words(P, w_cur);
-      if (lane == 0) {
-        P.row_start[b] = m.B.row0;
-        if (P.key_base) P.key_base[b] = m.B.kb0;
-        if (P.val_base) P.val_base[b] = m.B.vb0;
-        P.blk_status[b] = m.B.st;
-      }
-      const int rows = gather_rows(m);
-      if (rows) {
-        build_row_table_hv(T.t, rows, hv);
-        write_row_index(P, T.t, m, rows);
-      }
-      if (lane == 0) {
-        T.off = m.off;
-        T.kb0 = m.B.kb0;
-        T.vb0 = m.B.vb0;
-        T.rows = P.index_only ? 0 : rows;
-      }
-      // prefetch: headers of block bn, metadata of block bn + G
-      hv = 0;
-      if (bn < P.nblk) {
-        const BlockMeta mn = meta_of_words(P, w_next);
-        if (int(lane) < gather_rows(mn)) hv = rec_hv(P, lane, bn);
-        w_cur = w_next;
-        if (bn + G < P.nblk) w_next = meta_word(P, bn + G, lane);
-      }
-    }
-    lds_barrier();
-    const int rows = T.rows;
-    if (rows) {
-      const GlobalWin src{P.seg, P.seg_bytes, T.off};
-      gather_region<false>(src, T.t, rows, P.key_arena, T.kb0, wave, kThreads / 64);
-      gather_region<true>(src, T.t, rows, P.val_arena, T.vb0, wave, kThreads / 64);
-    }
-    if (bn >= P.nblk) break;
-    b = bn;
-  }
-}
-
-// Pass 3, tile form (large blocks, the default): one workgroup per 4 KiB of
-// a block's arenas -- the grid is nblk x kTileSlots workgroups, wave w of
-// slot j gathers 1 KiB tiles 4j + w, 4j + w + 4 kTileSlots, ... of the block's
-// value region followed by its key region.  Each wave rebuilds the block's
-// row table from the pass-1 headers into its own LDS slice (no barrier), so a
-// workgroup's whole prologue is one round of independent loads (metadata +
-// headers), and the chip sweeps source and arenas nearly in address order, the
-// way a plain streaming copy does.  Slot -> block is XCD-aware (speed only:
-// the slots of one block share blockIdx % 8, so its metadata, headers and
-// boundary lines are fetched into one L2).
-constexpr uint32_t kTileSlots = 16;
-__global__ __launch_bounds__(kThreads) void okv_gather_tile_kernel(CopyParams P) {
-  __shared__ GatherSmem tabs[kThreads / 64];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t k = blockIdx.x >> 3;
-  const uint32_t b = (k / kTileSlots) * 8 + (blockIdx.x & 7), j = k % kTileSlots;
-  if (b >= P.nblk) return;
-  GatherSmem& sm = tabs[wave];
-  const uint64_t mw = meta_word(P, b, lane);
-  const uint64_t hv = rec_hv(P, lane, b);  // lanes >= rows: unused words (in bounds)
-  const BlockMeta m = meta_of_words(P, mw);
-  const bool lead = j == 0 && wave == 0;
-  if (lead && lane == 0) {
-    P.row_start[b] = m.B.row0;
-    if (P.key_base) P.key_base[b] = m.B.kb0;
-    if (P.val_base) P.val_base[b] = m.B.vb0;
-    P.blk_status[b] = m.B.st;
-  }
-  const int rows = gather_rows(m);
-  if (!rows || (P.index_only && !lead)) return;
-  build_row_table_hv(sm, rows, hv);
-  __builtin_amdgcn_wave_barrier();
-  if (lead) write_row_index(P, sm, m, rows);
-  if (P.index_only) return;
-  const GlobalWin src{P.seg, P.seg_bytes, m.off};
-  const uint32_t Tv = (sm.vpre[rows] + 1023) >> 10, Tk = (sm.kpre[rows] + 1023) >> 10;
-  const uint32_t t0 = j * 4 + wave, ts = kTileSlots * 4;
-  if (t0 < Tv) gather_tiles<true, GlobalWin, 1>(src, sm, rows, P.val_arena, m.B.vb0, t0, Tv, ts);
-  // key tiles continue the same numbering after the value tiles
-  const uint32_t k0 = t0 < Tv ? t0 + ((Tv - t0 + ts - 1) / ts) * ts - Tv : t0 - Tv;
-  if (k0 < Tk) gather_tiles<false, GlobalWin, 1>(src, sm, rows, P.key_arena, m.B.kb0, k0, Tk, ts);
-}
-
-// Pass 3, pipelined staged form: one 512-thread workgroup per CU with two
-// LDS images.  Wave 0 is the loader: it LDS-DMAs block k+1 into the free
-// image, waits for its own DMA only (vmcnt is per wave), builds that block's
-// row table and writes its SoA index, while waves 1-7 assemble block k's
-// arena chunks from the other image.  One raw barrier per block hands the
-// images over; the gatherers never wait on their stores (no vmcnt drain).
-struct PipeInfo {
-  uint64_t off, kb0, vb0;
-  uint32_t rows, shift;
-  int32_t mode;  // 0 skip, 1 staged (LDS image), 2 HBM windows
-};
-struct __align__(16) PipeSmem {
-  uint4 img[2][(kImgBytes + 32) / 16 + 1];
-  GatherSmem t[2];
-  PipeInfo info[2];
-};
-constexpr int kPipeThreads = 512;
-
-
-// Loader side of one block: DMA issue (staged blocks), record positions,
-// wait for this wave's loads, row table + SoA index + block outcome.
-__device__ __forceinline__ void pipe_load(const CopyParams& P, PipeSmem& sm, int slot, uint32_t b,
-                                          const BlockMeta& m) {
-  const uint32_t lane = threadIdx.x;  // wave 0 only
-  const bool live = block_head(P, b, m);
-  const int rows = int(m.c.rows);
-  const uint32_t shift = uint32_t(m.off & 15);
-  const bool staged = live && shift + m.c.pend <= kImgBytes;
-  if (staged) {
-    const uint64_t base = m.off - shift;  // 16-byte aligned (seg is)
-    const uint32_t np = (shift + uint32_t(m.c.pend) + 1023) >> 10;
-    uint4* img = sm.img[slot];
-    for (uint32_t p = 0; p < np; ++p) {
-      uint64_t a = base + (uint64_t(p) << 10) + (lane << 4);
-      if (a >= P.seg_bytes) a = base;  // never past the segment; those bytes are unused
-      __builtin_amdgcn_global_load_lds(P.seg + a, OKV_LDS_PTR(img + 1 + p * 64), 16, 0, 0);
-    }
-  }
-  const uint64_t hv = live && int(lane) < rows ? rec_hv(P, lane, b) : 0u;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (live) {
-    build_row_table_hv(sm.t[slot], rows, hv);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    write_row_index(P, sm.t[slot], m, rows);
-  }
-  if (lane == 0) {
-    PipeInfo in;
-    in.off = m.off;
-    in.kb0 = m.B.kb0;
-    in.vb0 = m.B.vb0;
-    in.rows = uint32_t(rows);
-    in.shift = shift;
-    in.mode = !live || P.index_only ? 0 : staged ? 1 : 2;
-    sm.info[slot] = in;
-  }
-}
-
-__global__ __launch_bounds__(kPipeThreads) void okv_gather_pipe_kernel(CopyParams P) {
-  __shared__ PipeSmem sm;
-  const uint32_t wave = threadIdx.x >> 6;
-  uint32_t b = blockIdx.x;
-  if (b >= P.nblk) return;
-  if (wave == 0) {
-    const BlockMeta m = block_meta(P, b);
-    pipe_load(P, sm, 0, b, m);
-  }
-  lds_barrier();
-  for (int slot = 0;; slot ^= 1) {
-    const uint32_t bn = b + gridDim.x;
-    if (wave == 0) {
-      if (bn < P.nblk) {
-        const BlockMeta m = block_meta(P, bn);
-        pipe_load(P, sm, slot ^ 1, bn, m);
-      }
-    } else {
-      const PipeInfo in = sm.info[slot];
-      if (in.mode) {
-        const int rows = int(in.rows);
-        const GatherSmem& t = sm.t[slot];
-        if (in.mode == 1) {
-          const LdsWin src{sm.img[slot], 16u + in.shift};
-          gather_region<false>(src, t, rows, P.key_arena, in.kb0, wave - 1, kPipeThreads / 64 - 1);
-          gather_region<true>(src, t, rows, P.val_arena, in.vb0, wave - 1, kPipeThreads / 64 - 1);
-        } else {
-          const GlobalWin src{P.seg, P.seg_bytes, in.off};
-          gather_region<false>(src, t, rows, P.key_arena, in.kb0, wave - 1, kPipeThreads / 64 - 1);
-          gather_region<true>(src, t, rows, P.val_arena, in.vb0, wave - 1, kPipeThreads / 64 - 1);
-        }
-      }
-    }
-    lds_barrier();
-    if (bn >= P.nblk) break;
-    b = bn;
   }
 }
 
@@ -1238,7 +867,7 @@ int ensure_blocks(okv_ctx* ctx, uint32_t nblk) {
     (void)hipFree(ctx->d_rec);
     (void)hipFree(ctx->d_big);
   }
-  OKV_HIP(hipMalloc(&ctx->d_rec, n * kRCap * sizeof(uint64_t)));
+  OKV_HIP(hipMalloc(&ctx->d_rec, n * kRCap * sizeof(uint32_t)));
   OKV_HIP(hipMalloc(&ctx->d_big, (n + 1) * sizeof(uint32_t)));
   OKV_HIP(hipMalloc(&ctx->d_cnt, n * sizeof(BlockCount)));
   OKV_HIP(hipMalloc(&ctx->d_lp, n * sizeof(Prefix)));
@@ -1250,10 +879,12 @@ int ensure_blocks(okv_ctx* ctx, uint32_t nblk) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-// Event slot k (0..3) of the current timed call, or nullptr when not profiling.
+// Event slot k (0..kProfEv-1) of the current timed call, or nullptr when not
+// profiling: 0 start, 1 zstd stage done, 2 pass 1 done, 3 pass 2 done, 4 end.
+constexpr int kProfEv = 5;
 hipEvent_t prof_event(okv_ctx* ctx, int k) {
   if (!ctx->prof) return nullptr;
-  const size_t need = ctx->ev_used + 4;
+  const size_t need = ctx->ev_used + kProfEv;
   while (ctx->ev.size() < need) {
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) return nullptr;
@@ -1265,7 +896,7 @@ hipEvent_t prof_event(okv_ctx* ctx, int k) {
 void prof_mark(okv_ctx* ctx, int k) {
   hipEvent_t e = prof_event(ctx, k);
   if (e) (void)hipEventRecord(e, ctx->stream);
-  if (e && k == 3) ctx->ev_used += 4;
+  if (e && k == kProfEv - 1) ctx->ev_used += kProfEv;
 }
 
 // Working inputs of passes 1-3: the segment itself, or for zstd blocks the
@@ -1310,27 +941,18 @@ int prepare(okv_ctx* ctx, const uint8_t* d_seg, uint64_t seg_bytes, const Desc* 
   return OKV_OK;
 }
 
-// Pass-3 kernel choice.  The heuristic uses the call's average block span
-// (seg_bytes / nblk: it assumes the blocks tile the segment, which holds for
-// whole-segment decodes; a caller decoding a few blocks of a large segment
-// gets the large-block kernel, which is correct for any block size).
-enum GatherKind { kGatherGlobal64, kGatherGlobal256, kGatherLds, kGatherPipe, kGatherStream, kGatherTile };
-GatherKind choose_gather(const okv_ctx* ctx, const Work& w, uint32_t nblk, bool index_only) {
-  const bool small = nblk && w.seg_bytes / nblk <= 16384;
-  if (ctx->gather_mode == 1 || index_only || (ctx->gather_mode == 0 && small)) {
-    if (ctx->gather_threads) return ctx->gather_threads == 64 ? kGatherGlobal64 : kGatherGlobal256;
-    return small ? kGatherGlobal64 : kGatherGlobal256;
-  }
-  if (ctx->gather_mode == 2) return kGatherLds;
-  if (ctx->gather_mode == 3) return kGatherPipe;
-  if (ctx->gather_mode == 4 || uint64_t(nblk) * kTileSlots >= (1ull << 31)) return kGatherStream;
-  return kGatherTile;
+// Pass-3 workgroup width from the call's average block span (seg_bytes /
+// nblk: it assumes the blocks tile the segment, which holds for whole-segment
+// decodes; a caller decoding a few blocks of a large segment gets the
+// 256-thread form, which is correct for any block size).
+uint32_t gather_threads(const okv_ctx* ctx, const Work& w, uint32_t nblk) {
+  if (ctx->gather_threads) return ctx->gather_threads;
+  return nblk && w.seg_bytes / nblk <= 16384 ? 64u : 256u;
 }
 
-// Launch passes 1 and 2 on device inputs.  rec_t: pass 1 stores record headers
-// (u64, hdr_t layout: the large-block kernels').
+// Launch passes 1 and 2 on device inputs.
 int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_start,
-                bool timed = false, int rec_t = 0) {
+                bool timed = false) {
   int rc = ensure_blocks(ctx, nblk);
   if (rc) return rc;
   const uint32_t ntiles = (nblk + kTile - 1) / kTile;
@@ -1343,14 +965,13 @@ int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_star
     hipLaunchKernelGGL(okv_count_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, w.seg,
                        w.seg_bytes, w.descs, nblk, w.comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
                        ctx->d_rec, ctx->d_big, ctx->d_big + nblk, w.pre, prefetch,
-                       rec_t,
                        single ? ctx->d_tile_pre : nullptr, single ? ctx->d_tot : nullptr,
                        single ? d_row_start : nullptr);
-  if (timed) prof_mark(ctx, 1);
+  if (timed) prof_mark(ctx, 2);
   if (!single)
     hipLaunchKernelGGL(okv_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_tile_tot,
                        ntiles, ctx->d_tile_pre, ctx->d_tot, d_row_start, nblk);
-  if (timed) prof_mark(ctx, 2);
+  if (timed) prof_mark(ctx, 3);
   OKV_HIP(hipGetLastError());
   return OKV_OK;
 }
@@ -1374,9 +995,8 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   Work w;
   int rc = prepare(ctx, seg, seg_bytes, descs, nblk, comp, index_only, &w);
   if (rc) return rc;
-  const GatherKind gk = choose_gather(ctx, w, nblk, index_only);
-  rc = launch_plan(ctx, w, nblk, o->row_start, true,
-                  gk >= kGatherLds || ctx->gather_variant == 6 ? 1 : ctx->gather_variant == 8 ? 2 : 0);
+  prof_mark(ctx, 1);
+  rc = launch_plan(ctx, w, nblk, o->row_start, true);
   if (rc) return rc;
   CopyParams P;
   P.seg = w.seg;
@@ -1405,44 +1025,11 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   P.key_cap = index_only ? 0 : o->key_cap;
   P.val_cap = index_only ? 0 : o->val_cap;
   if (nblk) {
-    if (gk == kGatherTile) {
-      const uint32_t grid = ((nblk + 7) / 8) * 8 * kTileSlots;
-      hipLaunchKernelGGL(okv_gather_tile_kernel, dim3(grid), dim3(kThreads), 0, ctx->stream, P);
-    } else if (gk == kGatherStream) {
-      // persistent: every resident workgroup slot (register-bound occupancy)
-      const uint32_t grid = ctx->gather_grid ? ctx->gather_grid : ctx->stream_grid;
-      hipLaunchKernelGGL(okv_gather_stream_kernel, dim3(std::min<uint32_t>(nblk, grid)),
-                         dim3(kThreads), 0, ctx->stream, P);
-    } else if (gk == kGatherPipe) {
-      // persistent: one 512-thread workgroup per CU (two LDS images)
-      const uint32_t grid = ctx->gather_grid ? ctx->gather_grid : ctx->n_cu;
-      hipLaunchKernelGGL(okv_gather_pipe_kernel, dim3(std::min<uint32_t>(nblk, grid)),
-                         dim3(kPipeThreads), 0, ctx->stream, P);
-    } else if (gk == kGatherLds) {
-      // persistent: two workgroups per CU (LDS-bound), blocks strided over the grid
-      const uint32_t grid = ctx->gather_grid ? ctx->gather_grid : 2u * ctx->n_cu;
-      hipLaunchKernelGGL(okv_gather_lds_kernel, dim3(std::min<uint32_t>(nblk, grid)),
-                         dim3(kThreads), 0, ctx->stream, P);
-    } else {
-      const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
-      if (gk == kGatherGlobal64 && ctx->gather_variant == 8)
-        hipLaunchKernelGGL((okv_gather_kernel<64, 4, false, false, false, true>), g, dim3(64), 0, ctx->stream, P);
-      else if (gk == kGatherGlobal64 && ctx->gather_variant == 6)
-        hipLaunchKernelGGL((okv_gather_kernel<64, 4, false, true>), g, dim3(64), 0, ctx->stream, P);
-      else if (gk == kGatherGlobal64)
-        hipLaunchKernelGGL(okv_gather_kernel<64>, g, dim3(64), 0, ctx->stream, P);
-      else switch (ctx->gather_variant) {  // A/B: tiles per iteration, interleaved tiles
-        case 1: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 4, true>), g, dim3(kThreads), 0, ctx->stream, P); break;
-        case 2: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 2, false>), g, dim3(kThreads), 0, ctx->stream, P); break;
-        case 3: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 8, false>), g, dim3(kThreads), 0, ctx->stream, P); break;
-        case 4: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 2, true>), g, dim3(kThreads), 0, ctx->stream, P); break;
-        case 5: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 8, true>), g, dim3(kThreads), 0, ctx->stream, P); break;
-        case 6: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 4, false, true>), g, dim3(kThreads), 0, ctx->stream, P); break;
-        case 7: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 4, false, false, true>), g, dim3(kThreads), 0, ctx->stream, P); break;
-        case 8: hipLaunchKernelGGL((okv_gather_kernel<kThreads, 4, false, false, false, true>), g, dim3(kThreads), 0, ctx->stream, P); break;
-        default: hipLaunchKernelGGL((okv_gather_kernel<kThreads>), g, dim3(kThreads), 0, ctx->stream, P);
-      }
-    }
+    const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
+    if (gather_threads(ctx, w, nblk) == 64)
+      hipLaunchKernelGGL(okv_gather_kernel<64>, g, dim3(64), 0, ctx->stream, P);
+    else
+      hipLaunchKernelGGL(okv_gather_kernel<kThreads>, g, dim3(kThreads), 0, ctx->stream, P);
     const uint32_t nbig_grid = std::min<uint32_t>(nblk, 512);
     if (index_only)
       hipLaunchKernelGGL(okv_index_kernel, dim3((nbig_grid + kThreads - 1) / kThreads),
@@ -1451,7 +1038,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       hipLaunchKernelGGL(okv_copy_kernel, dim3(nbig_grid), dim3(kThreads), 0, ctx->stream, P);
     OKV_HIP(hipGetLastError());
   }
-  prof_mark(ctx, 3);
+  prof_mark(ctx, 4);
   if (flags & OKV_F_ASYNC) return OKV_OK;
   Totals T;
   rc = read_totals(ctx, &T);
@@ -1565,33 +1152,16 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   if (hipSetDevice(device) != hipSuccess) return nullptr;
   okv_ctx* ctx = new okv_ctx();
   ctx->device = device;
-  // A/B knobs between product kernels (all bit-exact): OKV_GATHER=global|tile|stream|lds|pipe,
-  // OKV_GATHER_THREADS=64|256 (global form), OKV_GATHER_GRID=<workgroups>
-  if (const char* v = getenv("OKV_GATHER")) {
-    if (!strcmp(v, "global")) ctx->gather_mode = 1;
-    else if (!strcmp(v, "lds")) ctx->gather_mode = 2;
-    else if (!strcmp(v, "pipe")) ctx->gather_mode = 3;
-    else if (!strcmp(v, "stream")) ctx->gather_mode = 4;
-    else if (!strcmp(v, "tile")) ctx->gather_mode = 5;
-    else if (strcmp(v, "auto")) { delete ctx; return nullptr; }
-  }
+  // A/B knobs of the pass-3 launch (both bit-exact): OKV_GATHER_THREADS=64|256
+  // (workgroup width), OKV_GATHER_GRID=<workgroups> (persistent grid)
   if (const char* v = getenv("OKV_GATHER_THREADS")) {
     ctx->gather_threads = uint32_t(atoi(v));
-    if (ctx->gather_threads != 64 && ctx->gather_threads != 256) { delete ctx; return nullptr; }
+    if (ctx->gather_threads != 64 && ctx->gather_threads != 256) {
+      delete ctx;
+      return nullptr;
+    }
   }
   if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
-  if (const char* v = getenv("OKV_GATHER_VARIANT")) ctx->gather_variant = atoi(v);
-  {
-    int ncu = 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
-        ncu > 0)
-      ctx->n_cu = uint32_t(ncu);
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, okv_gather_stream_kernel, kThreads,
-                                                     0) != hipSuccess || per_cu < 1)
-      per_cu = 4;
-    ctx->stream_grid = uint32_t(per_cu) * ctx->n_cu;
-  }
   if (stream) {
     ctx->stream = static_cast<hipStream_t>(stream);
   } else {
@@ -1761,7 +1331,7 @@ int okv_profile(okv_ctx* ctx, int enable) {
   OKV_HIP(hipStreamSynchronize(ctx->stream));
   ctx->prof = enable != 0;
   ctx->ev_used = 0;
-  ctx->prof_ms[0] = ctx->prof_ms[1] = ctx->prof_ms[2] = 0;
+  for (double& m : ctx->prof_ms) m = 0;
   ctx->prof_calls = 0;
   return OKV_OK;
 }
@@ -1769,17 +1339,19 @@ int okv_profile(okv_ctx* ctx, int enable) {
 int okv_profile_read(okv_ctx* ctx, double* ms, uint64_t* calls) {
   if (!ctx) return OKV_E_ARG;
   OKV_HIP(hipStreamSynchronize(ctx->stream));
-  for (size_t i = 0; i + 4 <= ctx->ev_used; i += 4) {
-    for (int k = 0; k < 3; ++k) {
+  // intervals: [0,1] zstd stage, [1,2] pass 1, [2,3] pass 2, [3,4] pass 3
+  static const int slot[4] = {3, 0, 1, 2};  // -> ms {count, scan, gather, zstd}
+  for (size_t i = 0; i + kProfEv <= ctx->ev_used; i += kProfEv) {
+    for (int k = 0; k < 4; ++k) {
       float t = 0.f;
       OKV_HIP(hipEventElapsedTime(&t, ctx->ev[i + k], ctx->ev[i + k + 1]));
-      ctx->prof_ms[k] += t;
+      ctx->prof_ms[slot[k]] += t;
     }
     ctx->prof_calls++;
   }
   ctx->ev_used = 0;
   if (ms)
-    for (int k = 0; k < 3; ++k) ms[k] = ctx->prof_ms[k];
+    for (int k = 0; k < 4; ++k) ms[k] = ctx->prof_ms[k];
   if (calls) *calls = ctx->prof_calls;
   return OKV_OK;
 }

@@ -590,11 +590,12 @@ __global__ __launch_bounds__(kThreads) void okv_enc_offset_kernel(
     Desc* __restrict__ desc, const uint64_t* __restrict__ bsl, const uint64_t* __restrict__ esl,
     const uint64_t* __restrict__ btile_pre, const uint64_t* __restrict__ etile_pre, uint64_t nb,
     const uint16_t* __restrict__ key_len, uint64_t n, const uint64_t* __restrict__ first,
-    uint64_t* __restrict__ moff, EncTotals* __restrict__ tot) {
+    uint64_t* __restrict__ moff, EncTotals* __restrict__ tot, uint64_t bloom_extra) {
   const uint64_t k = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-  // meta head: u16+FirstKey, u16+lastKey, bloom byte, compression byte,
-  // index-type byte, u64 entry count (:288-325)
-  const uint64_t head = 2u + key_len[0] + 2u + key_len[n - 1] + 3u + 8u;
+  // meta head: u16+FirstKey, u16+lastKey, bloom byte [+ u64 length + filter
+  // bytes: bloom_extra], compression byte, index-type byte, u64 entry count
+  // (:288-325)
+  const uint64_t head = 2u + key_len[0] + 2u + key_len[n - 1] + 3u + 8u + bloom_extra;
   if (k == 0) tot->head = head;
   if (k >= nb) return;
   const uint64_t t = k / kETile;
@@ -1102,6 +1103,7 @@ struct MetaParams {
   uint64_t count;   // block index entries (the head's u64 count, :320)
   int comp_byte;
   uint8_t* meta;
+  uint64_t bloom_len;  // ~0: no bloom filter; else its WriteTo length
 };
 
 __global__ __launch_bounds__(kThreads) void okv_enc_meta_kernel(MetaParams P) {
@@ -1115,10 +1117,17 @@ __global__ __launch_bounds__(kThreads) void okv_enc_meta_kernel(MetaParams P) {
     put_le(p, kz, 2);
     put_bytes(p + 2, P.key_arena + P.key_off[P.n - 1], kz);
     p += 2 + kz;
-    p[0] = 0;  // no bloom filter
-    p[1] = uint8_t(P.comp_byte);
-    p[2] = 0;  // not a partitioned block index
-    put_le(p + 3, P.count, 8);
+    if (P.bloom_len != ~uint64_t(0)) {  // :295-300 (the filter bytes: a host copy)
+      p[0] = 1;
+      put_le(p + 1, P.bloom_len, 8);
+      p += 9 + P.bloom_len;
+    } else {
+      p[0] = 0;  // :301-303
+      p += 1;
+    }
+    p[0] = uint8_t(P.comp_byte);
+    p[1] = 0;  // not a partitioned block index
+    put_le(p + 2, P.count, 8);
   }
   if (k >= P.nb) return;
   uint8_t* p = P.meta + P.moff[k];
@@ -1352,6 +1361,7 @@ uint32_t ceil_div(uint64_t a, uint64_t b) { return uint32_t((a + b - 1) / b); }
 
 struct Plan {
   uint64_t nb, data_bytes, meta_bytes, file_bytes, last_raw;
+  uint64_t head;  // meta head bytes (keys, bloom, compression, count)
   uint64_t w;     // most rows any block start can take (max next(a) - a)
   uint64_t bmax;  // largest BlockSize
   uint64_t avg_rec;  // mean record size
@@ -1436,12 +1446,13 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
                      uint64_t(nbt), epre, &e->d_tot->meta_ent);
   hipLaunchKernelGGL(okv_enc_offset_kernel, dim3(ceil_div(nb, kThreads)), dim3(kThreads), 0,
                      ctx->stream, e->desc, e->bsl, e->esl, bpre, epre, nb, R.kl, n, e->first,
-                     e->moff, e->d_tot);
+                     e->moff, e->d_tot, o.bloom ? 8 + o.bloom_len : 0);
   OKV_HIP(hipGetLastError());
   if ((rc = read_enc_totals(ctx, e))) return rc;
   if (e->h_tot->fault) return set_err(ctx, OKV_E_HIP, "encode: block chain inconsistent");
   pl->nb = nb;
   pl->data_bytes = e->h_tot->data_bytes;
+  pl->head = e->h_tot->head;
   pl->meta_bytes = e->h_tot->head + e->h_tot->meta_ent;
   pl->file_bytes = pl->data_bytes + pl->meta_bytes + 25;
   pl->last_raw = e->h_tot->last_raw;
@@ -1524,6 +1535,10 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   mp.count = pl.nb;
   mp.comp_byte = o.compression == OKV_COMP_LZ4 ? 2 : 0;
   mp.meta = seg + pl.data_bytes;
+  mp.bloom_len = o.bloom ? o.bloom_len : ~uint64_t(0);
+  if (o.bloom && o.bloom_len)  // BloomFilter.WriteTo bytes at head - 10 - len (after flag + u64)
+    OKV_HIP(hipMemcpyAsync(mp.meta + pl.head - 10 - o.bloom_len, o.bloom, o.bloom_len,
+                           hipMemcpyHostToDevice, ctx->stream));
   if ((reinterpret_cast<uintptr_t>(mp.meta) & 15) == 0) {
     // head bytes by the first lane of a one-block launch (nb = 0), entries via LDS
     MetaParams head = mp;

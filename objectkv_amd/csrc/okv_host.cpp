@@ -106,6 +106,8 @@ struct okv_writer {
   std::vector<Stat> index;    // blockIndex
   std::vector<uint8_t> meta;
   bool closed = false;
+  bool has_bloom = false;      // options.BloomFilter != nil
+  std::vector<uint8_t> bloom;  // its WriteTo bytes (opaque pass-through)
 
   void flush() {  // flushCurrentDataBlock :148-204
     const bool use_zstd = zstd_level > 0, use_lz4 = !use_zstd && lz4;
@@ -178,7 +180,13 @@ int okv_writer_close(okv_writer* w, int strict_go, uint64_t* file_len, uint64_t*
   putb(m, w->index[0].first_key.data(), w->index[0].first_key.size());
   put16(m, uint16_t(w->last_key.size()));
   putb(m, w->last_key.data(), w->last_key.size());
-  m.push_back(0);  // no bloom filter
+  if (w->has_bloom) {  // :295-300
+    m.push_back(1);
+    put64(m, w->bloom.size());
+    putb(m, w->bloom.data(), w->bloom.size());
+  } else {
+    m.push_back(0);  // :301-303
+  }
   const bool use_zstd = w->zstd_level > 0, use_lz4 = !use_zstd && w->lz4;
   m.push_back(use_zstd ? 1 : (use_lz4 ? 2 : 0));
   m.push_back(0);  // simple block index
@@ -223,6 +231,10 @@ int okv_writer_block(const okv_writer* w, uint64_t i, okv_block_desc* desc, uint
   if (first_key) *first_key = s.first_key.data();
   if (first_key_len) *first_key_len = s.first_key.size();
   return OKV_OK;
+}
+void okv_writer_set_bloom(okv_writer* w, const uint8_t* bytes, uint64_t len) {
+  w->has_bloom = true;
+  w->bloom.assign(bytes, bytes + len);
 }
 void okv_writer_free(okv_writer* w) { delete w; }
 

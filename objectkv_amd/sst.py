@@ -53,20 +53,31 @@ def xxh64(data, seed: int = 0) -> int:
 
 class SegmentWriter:
     """Host C++ SegmentWriter (okv_writer_*); raises OkvError with the Go
-    sentinel codes of include/okv_host.h."""
+    sentinel codes of include/okv_host.h.  bloom: the caller's filter object
+    (SegmentWriterOptions.BloomFilter) with add(key) and to_bytes() -- add runs
+    per row as in WriteRow (segment_writer.go:133-136), Close serialises
+    to_bytes() into the meta block (:295-300); the library treats the bytes
+    as opaque."""
 
-    def __init__(self, threshold=3584, block_size=4096, zstd_level=0, lz4=False, _handle=None):
+    def __init__(self, threshold=3584, block_size=4096, zstd_level=0, lz4=False, _handle=None,
+                 bloom=None):
         L = lib()
         self._h = _handle or L.okv_writer_new(threshold, block_size, zstd_level, int(lz4))
         if not self._h:
             raise OkvError(-1, "okv_writer_new")
+        self.bloom = bloom
 
     def WriteRow(self, key: bytes, val: bytes):
         rc = lib().okv_writer_write_row(self._h, key, len(key), val, len(val))
         if rc:
             raise OkvError(rc, "WriteRow")
+        if self.bloom is not None:
+            self.bloom.add(bytes(key))
 
     def Close(self, strict_go=True):
+        if self.bloom is not None:
+            b = np.frombuffer(self.bloom.to_bytes(), np.uint8)
+            lib().okv_writer_set_bloom(self._h, _ptr(b), b.size)
         fl, ml = C.c_uint64(), C.c_uint64()
         rc = lib().okv_writer_close(self._h, int(strict_go), C.byref(fl), C.byref(ml))
         if rc:
@@ -256,11 +267,12 @@ class Decoder:
         self._check(lib().okv_profile(self._ctx, int(enable)), "okv_profile")
 
     def profile_read(self):
-        """-> ({'count': ms, 'scan': ms, 'copy': ms} summed, number of calls)"""
-        ms = (C.c_double * 3)()
+        """-> ({'count', 'scan', 'copy' (pass 3 gather), 'zstd'}: ms summed over
+        the timed calls, number of calls)"""
+        ms = (C.c_double * 4)()
         n = C.c_uint64()
         self._check(lib().okv_profile_read(self._ctx, ms, C.byref(n)), "okv_profile_read")
-        return {"count": ms[0], "scan": ms[1], "copy": ms[2]}, n.value
+        return {"count": ms[0], "scan": ms[1], "copy": ms[2], "zstd": ms[3]}, n.value
 
     # -- host-pointer API ------------------------------------------------------
     def plan(self, seg, descs: np.ndarray, compression=COMP_NONE, index_only=False):
@@ -424,19 +436,25 @@ class Encoder(Decoder):
         self._check(lib().okv_encode_profile_reset(self._ctx), "okv_encode_profile_reset")
 
     @staticmethod
-    def _opts(threshold, block_size, compression, strict_go):
-        return _lib.EncodeOpts(threshold, block_size, compression, int(strict_go))
+    def _opts(threshold, block_size, compression, strict_go, bloom=None):
+        """bloom: BloomFilter.WriteTo bytes (kept alive on the returned struct)."""
+        o = _lib.EncodeOpts(threshold, block_size, compression, int(strict_go), None, 0)
+        if bloom is not None:
+            o._bloom = np.frombuffer(bytes(bloom), np.uint8) if len(bloom) else \
+                np.zeros(1, np.uint8)
+            o.bloom, o.bloom_len = o._bloom.ctypes.data, len(bloom)
+        return o
 
     def encode(self, rows, threshold=3584, block_size=4096, compression=COMP_NONE,
-               strict_go=True) -> Encoded:
+               strict_go=True, bloom=None) -> Encoded:
         """Host-buffer encode: rows is a list of (key, value) pairs or the dict
-        of SoA arrays from pack_rows()."""
+        of SoA arrays from pack_rows().  bloom: the filter's WriteTo bytes."""
         r = rows if isinstance(rows, dict) else pack_rows(rows)
         n = int(r["key_len"].size)
         R = _lib.Rows(_ptr(r["key_arena"]), _ptr(r["key_off"]), _ptr(r["key_len"]),
                       _ptr(r["val_arena"]), _ptr(r["val_off"]), _ptr(r["val_len"]), n,
                       int(r["key_arena"].size), int(r["val_arena"].size))
-        o = self._opts(threshold, block_size, compression, strict_go)
+        o = self._opts(threshold, block_size, compression, strict_go, bloom)
         out = _lib.EncodeOut()
         rc = lib().okv_encode_rows(self._ctx, C.byref(R), C.byref(o), C.byref(out), 0)
         if rc != OKV_E_CAPACITY:
@@ -454,7 +472,7 @@ class Encoder(Decoder):
 
     def encode_device(self, rows: dict, n_rows: int, out: dict, threshold=3584,
                       block_size=4096, compression=COMP_NONE, strict_go=True, close=True,
-                      key_arena_bytes=0, val_arena_bytes=0):
+                      key_arena_bytes=0, val_arena_bytes=0, bloom=None):
         """Device-resident encode.  rows: torch tensors key_arena, key_off,
         key_len, val_arena, val_off, val_len; out: torch tensors seg (uint8),
         optional first_row, desc (int64 [cap, 4]), hash.  Returns the filled
@@ -463,7 +481,7 @@ class Encoder(Decoder):
         R = _lib.Rows(_ptr(rows["key_arena"]), _ptr(rows["key_off"]), _ptr(rows["key_len"]),
                       _ptr(rows["val_arena"]), _ptr(rows["val_off"]), _ptr(rows["val_len"]),
                       n_rows, key_arena_bytes, val_arena_bytes)
-        o = self._opts(threshold, block_size, compression, strict_go)
+        o = self._opts(threshold, block_size, compression, strict_go, bloom)
         g = out.get
         caps = [t.shape[0] for t in (g("first_row"), g("desc"), g("hash")) if t is not None]
         blk_cap = min([caps[0] - 1 if g("first_row") is not None else caps[0]] + caps[1:]) \
@@ -498,11 +516,13 @@ class GpuSegmentWriter:
     GPU.  WriteRow validates each row exactly as Go does (:80-91) and buffers
     it; Close runs okv_encode_rows over the buffered rows and returns
     (file length, meta block bytes).  ``data()`` is what the Go writer's sink
-    holds afterwards."""
+    holds afterwards.  bloom: as SegmentWriter's (add per row, WriteTo bytes
+    into the meta block)."""
 
     def __init__(self, encoder: Encoder, threshold=3584, block_size=4096, zstd_level=0,
-                 lz4=False, strict_go=True):
+                 lz4=False, strict_go=True, bloom=None):
         self._enc = encoder
+        self.bloom = bloom
         self._opts = dict(threshold=threshold, block_size=block_size,
                           compression=COMP_ZSTD if zstd_level > 0 else
                           (COMP_LZ4 if lz4 else COMP_NONE), strict_go=strict_go)
@@ -522,11 +542,14 @@ class GpuSegmentWriter:
         if not key:
             raise OkvError(_lib.W_INVALID_KEY, "key cannot be empty: ErrInvalidKey")
         self._rows.append((key, val))
+        if self.bloom is not None:
+            self.bloom.add(key)
 
     def Close(self):
         if self._closed:  # Go: blockWriter is nil after the first Close -> panic (Q1)
             raise OkvError(_lib.W_NIL_WRITER, "Close on a closed writer")
-        self.result = self._enc.encode(self._rows, **self._opts)
+        bloom = self.bloom.to_bytes() if self.bloom is not None else None
+        self.result = self._enc.encode(self._rows, bloom=bloom, **self._opts)
         self._closed = True
         return self.result.file_bytes, self.result.meta()
 

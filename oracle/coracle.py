@@ -60,6 +60,7 @@ def lib():
         L.oref_writer_num_blocks.restype = u64
         L.oref_writer_num_blocks.argtypes = [p]
         L.oref_writer_free.argtypes = [p]
+        L.oref_writer_set_bloom.argtypes = [p, p, u64]
         L.oref_parse_meta.argtypes = [p, u64, C.POINTER(Meta)]
         L.oref_fetch_meta.argtypes = [p, u64, C.c_int64, C.POINTER(Meta), C.POINTER(u64),
                                       C.POINTER(u64)]
@@ -67,6 +68,8 @@ def lib():
         L.oref_encode_go.restype = C.c_int
         L.oref_encode_go.argtypes = [p, p, p, p, p, p, u64, u64, u64, C.c_int, C.c_int,
                                      C.POINTER(u64)]
+        L.oref_encode_soa.restype = p
+        L.oref_encode_soa.argtypes = [p, p, p, p, p, p, u64, u64, u64, C.POINTER(C.c_int)]
         L.oref_decode_range_go.restype = u64
         L.oref_decode_range_go.argtypes = [p, u64, p, u64, C.c_int, C.c_int, C.POINTER(u64)]
         L.oref_block_counts.argtypes = [p, u64, p, u64, C.c_int, p, p, p, p]
@@ -87,6 +90,11 @@ def xxh64(data: bytes, seed: int = 0) -> int:
 class Writer:
     def __init__(self, threshold=3584, block_size=4096, zstd_level=0, lz4=False):
         self.h = lib().oref_writer_new(threshold, block_size, zstd_level, int(lz4))
+
+    def set_bloom(self, data: bytes):
+        """BloomFilter != nil: the meta block carries these WriteTo bytes."""
+        buf = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+        lib().oref_writer_set_bloom(self.h, _ptr(buf), len(data))
 
     def write_row(self, key: bytes, val: bytes) -> int:
         return lib().oref_writer_write_row(self.h, key, len(key), val, len(val))
@@ -203,6 +211,42 @@ def decode_go(seg, descs: np.ndarray, compression=0, threads=1):
     rows = lib().oref_decode_range_go(_ptr(s), len(seg), _ptr(descs), len(descs), compression,
                                       threads, C.byref(pay))
     return rows, pay.value
+
+
+def _view(ptr, n):
+    """numpy uint8 view of n bytes at ptr (no copy; owner keeps it alive)."""
+    if not n:
+        return np.zeros(0, np.uint8)
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(n,))
+
+
+class SoaSegment:
+    """oref_encode_soa result: .file / .meta are views into the writer."""
+
+    def __init__(self, rows: dict, n, threshold, block_size):
+        rc = C.c_int()
+        self.h = lib().oref_encode_soa(_ptr(rows["key_arena"]), _ptr(rows["key_off"]),
+                                       _ptr(rows["key_len"]), _ptr(rows["val_arena"]),
+                                       _ptr(rows["val_off"]), _ptr(rows["val_len"]), n,
+                                       threshold, block_size, C.byref(rc))
+        self.rc = rc.value
+        self.file = self.meta = None
+        if self.rc == 0:
+            f, fl, m, ml = C.c_void_p(), C.c_uint64(), C.c_void_p(), C.c_uint64()
+            self.rc = lib().oref_writer_close(self.h, C.byref(f), C.byref(fl), C.byref(m),
+                                              C.byref(ml))
+            if self.rc == 0:
+                self.file, self.meta = _view(f.value, fl.value), _view(m.value, ml.value)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oref_writer_free(self.h)
+            self.h = None
+
+
+def encode_soa(rows: dict, n, threshold=3584, block_size=4096) -> SoaSegment:
+    """One segment from SoA numpy rows, single-threaded (the oracle writer)."""
+    return SoaSegment(rows, n, threshold, block_size)
 
 
 def encode_go(rows: dict, n, threshold=3584, block_size=4096, lz4=False, threads=1):

@@ -150,6 +150,8 @@ struct oref_writer {
   uint64_t nidx, capidx;
   int closed;
   obuf meta;
+  int has_bloom; /* options.BloomFilter != nil (segment_writer_option.go:20) */
+  obuf bloom;    /* its WriteTo bytes, supplied by the caller (opaque here) */
 };
 
 oref_writer *oref_writer_new(uint64_t threshold_bytes, uint64_t block_size, int zstd_level,
@@ -238,7 +240,13 @@ int oref_writer_close(oref_writer *w, const uint8_t **file, uint64_t *file_len,
   ob_put(m, f->first_key.p, f->first_key.n);
   ob_u16(m, (uint16_t)w->last_key.n);
   ob_put(m, w->last_key.p, w->last_key.n);
-  ob_u8(m, 0); /* bloom: only BloomFilter == nil is restated (:301-303) */
+  if (w->has_bloom) { /* :295-300: flag 1, u64 length, BloomFilter.WriteTo bytes */
+    ob_u8(m, 1);
+    ob_u64(m, w->bloom.n);
+    ob_put(m, w->bloom.p, w->bloom.n);
+  } else {
+    ob_u8(m, 0); /* :301-303 */
+  }
   int use_zstd = w->zstd_level > 0, use_lz4 = !use_zstd && w->lz4;
   ob_u8(m, use_zstd ? 1 : (use_lz4 ? 2 : 0)); /* :306-314 */
   ob_u8(m, 0);                                /* :317 simple index */
@@ -265,8 +273,18 @@ const uint8_t *oref_writer_bytes(const oref_writer *w, uint64_t *len) {
 }
 uint64_t oref_writer_num_blocks(const oref_writer *w) { return w->nidx; }
 
+/* BloomFilter != nil: the writer serialises these bytes into the meta block
+ * (the caller runs BloomFilter.Add per row, segment_writer.go:133-136, and
+ * hands over WriteTo's bytes before Close; the filter is opaque here). */
+void oref_writer_set_bloom(oref_writer *w, const uint8_t *bytes, uint64_t len) {
+  w->has_bloom = 1;
+  w->bloom.n = 0;
+  ob_put(&w->bloom, bytes, len);
+}
+
 void oref_writer_free(oref_writer *w) {
   if (!w) return;
+  free(w->bloom.p);
   for (uint64_t i = 0; i < w->nidx; i++) free(w->idx[i].first_key.p);
   free(w->idx);
   free(w->block.p);
@@ -635,6 +653,22 @@ int oref_encode_go(const uint8_t *key_arena, const uint64_t *key_off, const uint
   free(th);
   if (file_bytes) *file_bytes = bytes;
   return rc;
+}
+
+/* One segment from SoA rows, single-threaded: WriteRow for every row
+ * (segment_writer.go:80-146); the caller then calls oref_writer_close once
+ * (:211-328).  The oracle side of the full-size encode parity test; *rc = 0
+ * or the first writer error. */
+oref_writer *oref_encode_soa(const uint8_t *key_arena, const uint64_t *key_off,
+                             const uint16_t *key_len, const uint8_t *val_arena,
+                             const uint64_t *val_off, const uint32_t *val_len, uint64_t n,
+                             uint64_t threshold, uint64_t block_size, int *rc) {
+  oref_writer *w = oref_writer_new(threshold, block_size, 0, 0);
+  *rc = 0;
+  for (uint64_t i = 0; i < n && !*rc; i++)
+    *rc = oref_writer_write_row(w, key_arena + key_off[i], key_len[i], val_arena + val_off[i],
+                                val_len[i]);
+  return w;
 }
 
 /* ======================================================================= */

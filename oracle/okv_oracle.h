@@ -71,6 +71,9 @@ int oref_writer_close(oref_writer *w, const uint8_t **file, uint64_t *file_len,
 /* bytes written to the external writer so far (blocks + footer) */
 const uint8_t *oref_writer_bytes(const oref_writer *w, uint64_t *len);
 uint64_t oref_writer_num_blocks(const oref_writer *w);
+/* options.BloomFilter != nil: the meta block carries [1][u64 len][bytes]
+ * (segment_writer.go:295-300); bytes = BloomFilter.WriteTo, opaque here. */
+void oref_writer_set_bloom(oref_writer *w, const uint8_t *bytes, uint64_t len);
 void oref_writer_free(oref_writer *w);
 
 /* ---- block index entry ------------------------------------------------- */
@@ -132,6 +135,14 @@ int oref_encode_go(const uint8_t *key_arena, const uint64_t *key_off, const uint
                    const uint8_t *val_arena, const uint64_t *val_off, const uint32_t *val_len,
                    uint64_t n, uint64_t threshold, uint64_t block_size, int lz4, int threads,
                    uint64_t *file_bytes);
+
+/* One segment from SoA rows on one thread (full-size encode parity): every
+ * row written, the writer returned for ONE oref_writer_close, then
+ * oref_writer_free; *rc = 0 or the first writer error. */
+oref_writer *oref_encode_soa(const uint8_t *key_arena, const uint64_t *key_off,
+                             const uint16_t *key_len, const uint8_t *val_arena,
+                             const uint64_t *val_off, const uint32_t *val_len, uint64_t n,
+                             uint64_t threshold, uint64_t block_size, int *rc);
 
 /* ---- SoA restatement of the product's output layout -------------------- */
 /* Pass 1: per-block (status, rows, key bytes, value bytes). */

@@ -169,17 +169,17 @@ def _b(x):  # Go treats a nil slice as empty in bytes.Equal / bytes.Compare
 
 
 class SegmentWriterOptions:
-    """segment_writer_option.go:5-16; defaults :18-27 (bloom not restated)."""
+    """segment_writer_option.go:5-16; defaults :18-27.  BloomFilter: an object
+    with add(key) and to_bytes() (oracle/bloom_ref.py restates bits-and-blooms
+    v2.0.3; its bytes are parity-unpinned), or None."""
 
     def __init__(self, DataBlockThresholdBytes=3584, DataBlockSize=4096,
                  ZSTDCompressionLevel=0, LZ4Compression=False, BloomFilter=None):
-        if BloomFilter is not None:
-            raise NotImplementedError("bloom (bits-and-blooms v2.0.3) bytes are parity-unpinned")
         self.DataBlockThresholdBytes = DataBlockThresholdBytes
         self.DataBlockSize = DataBlockSize
         self.ZSTDCompressionLevel = ZSTDCompressionLevel
         self.LZ4Compression = LZ4Compression
-        self.BloomFilter = None
+        self.BloomFilter = BloomFilter
 
 
 class SegmentWriter:
@@ -216,6 +216,8 @@ class SegmentWriter:
         self.last_key = bytes(key)  # :118
         self.block += struct.pack("<HI", len(key), len(val)) + key + val  # :121-127
         self.raw += 6 + len(key) + len(val)  # :131
+        if self.options.BloomFilter is not None:  # :133-136
+            self.options.BloomFilter.add(bytes(key))
         if len(self.block) >= self.options.DataBlockThresholdBytes:  # :138
             self._flush()
 
@@ -255,7 +257,11 @@ class SegmentWriter:
         m = bytearray()
         m += struct.pack("<H", len(fk)) + fk
         m += struct.pack("<H", len(self.last_key)) + self.last_key
-        m += b"\x00"  # no bloom :301-303
+        if o.BloomFilter is not None:  # :295-300
+            bb = o.BloomFilter.to_bytes()
+            m += b"\x01" + struct.pack("<Q", len(bb)) + bb
+        else:
+            m += b"\x00"  # :301-303
         use_zstd = o.ZSTDCompressionLevel > 0
         use_lz4 = (not use_zstd) and o.LZ4Compression
         m += bytes([1 if use_zstd else (2 if use_lz4 else 0)])  # :306-314
@@ -361,7 +367,7 @@ def bytes_to_metadata(meta: bytes) -> SegmentMetadata:
     md.LastKey = r.must(n)
     if r.must(1)[0] == 1:  # :184
         blen = struct.unpack("<Q", r.must(8))[0]
-        md.BloomFilter = r.must(blen)  # opaque (bloom.ReadFrom not restated)
+        md.BloomFilter = r.must(blen)  # WriteTo bytes; GetRow probes them (bloom_ref)
     c = r.must(1)[0]
     md.ZSTDCompression = c == 1
     md.LZ4Compression = c == 2
@@ -483,6 +489,10 @@ class SegmentReader:
 
     def GetRow(self, key):  # :362-404
         md = self._md()
+        if md.BloomFilter is not None:  # :371-378 (probeBloomFilter :245-258)
+            from oracle.bloom_ref import BloomFilter
+            if not BloomFilter.from_bytes(md.BloomFilter).test(_b(key)):
+                raise GoError(ErrNoRows, "did not find row in bloom filter")
         cand = md.BlockIndex.descend_le(key)
         if not cand:
             raise GoError(ErrNoRows, "did not find potential block")

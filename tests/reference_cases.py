@@ -174,16 +174,35 @@ def case_row_iter_seek(impl):
 
 
 def case_rollover(impl):
-    """TestRollover, segment_row_iter_test.go:380-450 (written with
-    BloomFilter=nil: the bloom only feeds GetRow, never RowIter)."""
+    """TestRollover, segment_row_iter_test.go:380-450, with the options the Go
+    test uses: DefaultSegmentWriterOptions, whose BloomFilter is
+    NewWithEstimates(100000, 1e-6) (segment_writer_option.go:20) -- the meta
+    block carries the filter (segment_writer.go:295-300) and the reader must
+    parse past it (segment_reader.go:183-201)."""
     rows = [(b"key%03d" % i, b"value%03d-I-SHOULD-NOT-SHOW" % i) for i in range(1, 200, 2)]
-    seg, flen, meta = impl.write(rows + [(b"key900", b"value900")])
+    seg, flen, meta = impl.write(rows + [(b"key900", b"value900")], BloomFilter="default")
+    assert meta[2 + 6 + 2 + 6] == 1  # bloom flag after the first/last keys
     r = impl.reader(seg, flen)
     it = r.RowIter(impl.DirectionDescending)
     it.Seek(b"key006")  # :420-423
     got = [it.Next().Key for _ in range(3)]  # :425-443
     assert got == [b"key005", b"key003", b"key001"]
     assert _kind(impl, it.Next) == impl.EOF  # :445-449
+    # GetRow behind the bloom probe (segment_reader.go:371-378), hit and miss
+    assert r.GetRow(b"key005").Value == b"value005-I-SHOULD-NOT-SHOW"
+    assert _kind(impl, r.GetRow, b"key004") == "ErrNoRows"
+
+
+def case_rollover_no_bloom(impl):
+    """TestRollover's rows written with BloomFilter = nil."""
+    rows = [(b"key%03d" % i, b"value%03d-I-SHOULD-NOT-SHOW" % i) for i in range(1, 200, 2)]
+    seg, flen, meta = impl.write(rows + [(b"key900", b"value900")])
+    assert meta[2 + 6 + 2 + 6] == 0
+    r = impl.reader(seg, flen)
+    it = r.RowIter(impl.DirectionDescending)
+    it.Seek(b"key006")
+    assert [it.Next().Key for _ in range(3)] == [b"key005", b"key003", b"key001"]
+    assert _kind(impl, it.Next) == impl.EOF
 
 
 def case_larger_than_block(impl):
@@ -208,4 +227,4 @@ def case_larger_than_block(impl):
 
 CASES = [case_read_uncompressed, case_read_blank_value, case_read_single_row,
          case_corrupt_file_end, case_corrupt_file_middle, case_row_iter_next,
-         case_row_iter_seek, case_rollover, case_larger_than_block]
+         case_row_iter_seek, case_rollover, case_rollover_no_bloom, case_larger_than_block]

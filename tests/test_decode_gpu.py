@@ -221,3 +221,76 @@ def test_random_fuzz_against_c_oracle(decoder):
 def test_empty_batch(decoder):
     got = decoder.decode(b"\x00" * 32, np.zeros((0, 4), np.uint64))
     assert got.row_start.tolist() == [0]
+
+
+def _mixed_segment(kinds, seed):
+    """Raw record blocks of mixed shapes, back to back at 16-byte offsets:
+    's' 4 KiB with 42 rows of 16/64, 'L' 64 KiB with <= 40 rows of 1-3 KiB
+    values, 'M' more than kRCap (64) rows (staged path, okv_copy_kernel)."""
+    rng = np.random.default_rng(seed)
+    seg, descs = bytearray(), []
+    for kind in kinds:
+        body = bytearray()
+        if kind == "s":
+            shape = [(16, 64)] * 42
+        elif kind == "L":
+            shape = [(int(rng.integers(8, 257)), int(rng.integers(1000, 3000)))
+                     for _ in range(int(rng.integers(5, 28)))]
+        else:
+            shape = [(int(rng.integers(1, 20)), int(rng.integers(0, 40)))
+                     for _ in range(int(rng.integers(65, 300)))]
+        for kl, vl in shape:
+            body += kl.to_bytes(2, "little") + vl.to_bytes(4, "little")
+            body += rng.integers(0, 256, kl + vl, dtype=np.uint8).tobytes()
+        bsize = (len(body) // 4096 + 1) * 4096
+        off = len(seg)
+        seg += body + bytes(bsize - len(body))
+        descs.append((off, bsize, len(body), 0))
+    return bytes(seg), np.array(descs, np.uint64).reshape(-1, 4)
+
+
+@pytest.fixture(scope="module")
+def decoders_by_width():
+    """One decoder per pass-3 workgroup width (OKV_GATHER_THREADS), so both
+    gather forms run on the same inputs whatever the average block size."""
+    import os
+    decs = {}
+    try:
+        for w in ("64", "256"):
+            os.environ["OKV_GATHER_THREADS"] = w
+            decs[w] = okv.Decoder(0)
+    finally:
+        os.environ.pop("OKV_GATHER_THREADS", None)
+    yield decs
+    for d in decs.values():
+        d.close()
+
+
+@pytest.mark.parametrize("width", ["64", "256"])
+def test_mixed_blocks_both_gather_widths(decoders_by_width, width):
+    """A segment mixing 4 KiB blocks, 64 KiB blocks with few rows and blocks
+    over kRCap rows, through the 64- and the 256-thread gather."""
+    rng = np.random.default_rng(11)
+    kinds = list(rng.choice(["s", "s", "L", "M"], size=300))
+    seg, d = _mixed_segment(kinds, 5)
+    for index_only in (False, True):
+        got = decoders_by_width[width].decode(seg, d, index_only=index_only)
+        _assert_same_as_oracle(got, seg, d, 0, index_only)
+
+
+@pytest.mark.parametrize("nblk", [255, 256, 257, 513])
+def test_single_tile_and_scan_paths(decoder, decoders_by_width, nblk):
+    """<= 256 blocks: pass 1 writes the totals itself (one tile, no scan
+    launch, in-kernel big-block counter reset); more: okv_scan_kernel.  Both
+    with a block over kRCap rows, against the oracle and each other."""
+    kinds = ["s"] * nblk
+    kinds[nblk // 2] = "M"
+    kinds[-1] = "M"
+    seg, d = _mixed_segment(kinds, nblk)
+    outs = [dec.decode(seg, d) for dec in (decoder, *decoders_by_width.values())]
+    for got in outs:
+        _assert_same_as_oracle(got, seg, d, 0, False)
+    # the same decoder again after a larger call (scratch reuse, counter reset)
+    again = decoder.decode(seg, d)
+    assert again.val_arena.tobytes() == outs[0].val_arena.tobytes()
+    assert np.array_equal(again.row_start, outs[0].row_start)

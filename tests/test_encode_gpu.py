@@ -55,7 +55,11 @@ class GpuWriterImpl(ProductImpl):
 
     @classmethod
     def write(cls, rows, **kw):
-        w = okv.GpuSegmentWriter(cls.encoder)
+        bloom = None
+        if kw.get("BloomFilter") == "default":
+            from oracle.bloom_ref import default_filter
+            bloom = default_filter()
+        w = okv.GpuSegmentWriter(cls.encoder, bloom=bloom)
         for k, v in rows:
             w.WriteRow(k, v)
         flen, meta = w.Close()
@@ -294,3 +298,50 @@ def test_c1_round_trip(enc, decoder):
             break
         got.append((kv.Key, kv.Value))
     assert got == rows
+
+
+def test_bloom_pass_through(enc, decoder):
+    """DefaultSegmentWriterOptions' bloom filter (segment_writer_option.go:20):
+    the caller's WriteTo bytes land in the meta block as [1][u64 len][bytes]
+    (segment_writer.go:295-300) through every product writer -- the host C++
+    writer, the GPU encoder on host buffers and on device tensors -- byte for
+    byte as the oracle writer writes them; the segment decodes and its
+    metadata parses past the filter."""
+    from oracle.bloom_ref import default_filter
+    rng = random.Random(3)
+    rows = sorted(_random_rows(rng, 3000, 40, 300))
+    f = default_filter()
+    for k, _v in rows:
+        f.add(k)
+    bb = f.to_bytes()
+    w = CO.Writer()
+    for k, v in rows:
+        assert w.write_row(k, v) == 0
+    w.set_bloom(bb)
+    rc, want, want_meta = w.close()
+    assert rc == 0
+    # host C++ writer (the filter object is the caller's: add per row)
+    hw = okv.SegmentWriter(bloom=default_filter())
+    for k, v in rows:
+        hw.WriteRow(k, v)
+    flen, meta = hw.Close()
+    assert hw.data().tobytes() == want and meta == want_meta
+    # GPU encoder, host buffers
+    got = enc.encode(rows, bloom=bb)
+    assert got.seg.tobytes() == want and got.meta() == want_meta
+    # GPU encoder, device tensors (the bench path) + Close's meta hash / trailer
+    r = okv.sst.pack_rows(rows)
+    t = {k: torch.from_numpy((v.view(np.int64) if v.dtype == np.uint64 else
+                              v.view(np.int16) if v.dtype == np.uint16 else
+                              v.view(np.int32) if v.dtype == np.uint32 else v).copy()).to("cuda")
+         for k, v in r.items()}
+    seg_t = torch.zeros(len(want) + 4096, dtype=torch.uint8, device="cuda")
+    eo = enc.encode_device(t, len(rows), {"seg": seg_t}, bloom=bb,
+                           key_arena_bytes=r["key_arena"].size,
+                           val_arena_bytes=r["val_arena"].size)
+    assert eo.file_bytes == len(want)
+    assert seg_t[:eo.file_bytes].cpu().numpy().tobytes() == want
+    md = okv.fetch_metadata(want, len(want))
+    dec = decoder.decode(want, md.descs)
+    assert [(k, v or b"") for b in range(md.descs.shape[0]) for k, v in dec.block_rows(b)] == \
+        [(k, v) for k, v in rows]

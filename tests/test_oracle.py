@@ -13,6 +13,7 @@ from __future__ import annotations
 import json
 import os
 import random
+import struct
 
 import numpy as np
 import pytest
@@ -26,6 +27,9 @@ R200 = [(b"key%03d" % i, b"value%03d" % i) for i in range(200)]
 
 
 def write(rows, **kw):
+    if kw.get("BloomFilter") == "default":
+        from oracle.bloom_ref import default_filter
+        kw["BloomFilter"] = default_filter()
     w = P.SegmentWriter(P.SegmentWriterOptions(**kw))
     for k, v in rows:
         w.WriteRow(k, v)
@@ -304,3 +308,47 @@ def test_zstd_blocks_c_and_python_oracles_agree():
         py = P.decode_soa(seg, descs, P.COMP_ZSTD)
         c = CO.decode_soa(seg, CO.descs_array(descs), P.COMP_ZSTD)
         assert py["status"] == [want[name]] and list(c["status"]) == py["status"], name
+
+
+# ---- bloom filter pass-through (segment_writer.go:133-136, :295-300) -----------
+
+
+def test_murmur3_and_default_filter():
+    """MurmurHash3_x64_128 canonical vectors (spaolacci/murmur3 v1.1.0 Sum128)
+    and DefaultSegmentWriterOptions' filter shape.  Filter bytes stay
+    parity-unpinned: no reference test asserts them (oracle/bloom_ref.py)."""
+    from oracle import bloom_ref as B
+    assert B.murmur3_128(b"") == (0, 0)
+    assert B.murmur3_128(b"hello") == (0xCBD8A7B341BD9B02, 0x5B1E906A48AE1D19)
+    h1, h2 = B.murmur3_128(b"foo")
+    assert struct.pack("<QQ", h1, h2) == b"aE\xf5\x01W\x86q\xe2\x87}\xba+\xe4\x87\xaf~"
+    f = B.default_filter()
+    assert (f.m, f.k) == (2875518, 20) and len(f.to_bytes()) == 24 + 8 * ((f.m + 63) // 64)
+    keys = [b"key%03d" % i for i in range(0, 200, 2)]
+    for k in keys:
+        f.add(k)
+    g = B.BloomFilter.from_bytes(f.to_bytes())
+    assert all(g.test(k) for k in keys)  # no false negatives
+    assert sum(g.test(b"key%03d" % i) for i in range(1, 200, 2)) <= 1
+
+
+def test_bloom_segment_c_and_python_oracles_agree():
+    """Both restated writers serialise the same caller-supplied filter bytes
+    into the meta block: [1][u64 LE len][WriteTo bytes]; BytesToMetadata parses
+    past them."""
+    from oracle import bloom_ref as B
+    rows = [(b"key%03d" % i, b"value%03d-I-SHOULD-NOT-SHOW" % i) for i in range(1, 200, 2)]
+    f = B.default_filter()
+    seg_py, flen, meta = write(rows, BloomFilter=f)
+    w = CO.Writer()
+    for k, v in rows:
+        assert w.write_row(k, v) == 0
+    w.set_bloom(f.to_bytes())
+    rc, seg_c, meta_c = w.close()
+    assert rc == 0 and seg_c == seg_py and meta_c == meta
+    bb = f.to_bytes()
+    at = 2 + 6 + 2 + 6
+    assert meta[at] == 1 and struct.unpack_from("<Q", meta, at + 1)[0] == len(bb)
+    assert meta[at + 9:at + 9 + len(bb)] == bb
+    rc, md = CO.parse_meta(meta)
+    assert rc == 0 and md["has_bloom"] and len(md["entries"]) == 2

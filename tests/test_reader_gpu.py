@@ -20,8 +20,12 @@ class ProductImpl:
 
     @staticmethod
     def write(rows, **kw):
+        bloom = None
+        if kw.get("BloomFilter") == "default":  # the caller's filter; bytes pass through
+            from oracle.bloom_ref import default_filter
+            bloom = default_filter()
         w = okv.SegmentWriter(kw.get("DataBlockThresholdBytes", 3584),
-                              kw.get("DataBlockSize", 4096))
+                              kw.get("DataBlockSize", 4096), bloom=bloom)
         for k, v in rows:
             w.WriteRow(k, v)
         flen, meta = w.Close()

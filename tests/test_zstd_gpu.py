@@ -105,9 +105,11 @@ def test_zstd_long_runs_and_rle_literals(decoder):
 
 
 def test_zstd_staged_equals_general_under_corruption(decoder, zmode, monkeypatch):
-    """Byte flips in the sequence sections: the staged path and the general
-    kernel apply the same checks, so statuses and bytes agree block for block;
-    blocks the oracle decodes must match it."""
+    """Byte flips in the sequence sections of 48 blocks.  Two-sided against the
+    oracle (libzstd as the decoder checker): every block's status must equal
+    the oracle's -- a corrupt frame the checker rejects must fail on the
+    device too, and vice versa -- and the decoded rows of the blocks that
+    succeed must equal its bytes.  Both device paths, and they agree."""
     if zmode == "general":
         pytest.skip("compares the two paths itself")
     import random
@@ -120,15 +122,10 @@ def test_zstd_staged_equals_general_under_corruption(decoder, zmode, monkeypatch
         for _ in range(1 + i % 3):
             b[off + csz - 1 - rng.randrange(min(csz - 20, 3000))] ^= 1 << rng.randrange(8)
     dl = [tuple(int(x) for x in d) for d in descs]
-    d = np.array(dl, np.uint64).reshape(-1, 4)
-    staged = decoder.decode(np.frombuffer(bytes(b), np.uint8), d, P.COMP_ZSTD)
+    staged = _check(decoder, bytes(b), dl)
     monkeypatch.setenv("OKV_ZSTD_GENERAL", "1")
-    general = decoder.decode(np.frombuffer(bytes(b), np.uint8), d, P.COMP_ZSTD)
+    general = _check(decoder, bytes(b), dl)
     assert np.array_equal(staged.status, general.status)
-    for k in SOA:
-        assert np.array_equal(getattr(staged, k), getattr(general, k)), k
-    assert staged.key_arena.tobytes() == general.key_arena.tobytes()
     assert staged.val_arena.tobytes() == general.val_arena.tobytes()
-    ref = CO.decode_soa(bytes(b), CO.descs_array(dl), P.COMP_ZSTD, False)
-    ok = ref["status"] == 0
-    assert np.array_equal(staged.status[ok], ref["status"][ok])
+    # the flips must actually exercise both outcomes
+    assert 0 < int((staged.status != 0).sum()) < len(dl)

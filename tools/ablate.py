@@ -1,9 +1,9 @@
-"""Diagnostic A/B of the pass-3 gather forms, interleaved in ONE process
+"""Diagnostic A/B of pass-3 launch forms, interleaved in ONE process
 (cdna_hip_programming.md §5.4 rule 24), with a bit-equality check of every
 output array between the arms.
 
-usage: python tools/ablate.py [arm ...]     arm = <mode>[:<grid>[:<threads>[:<variant>]]]
-  mode = lds | global (OKV_GATHER), grid = OKV_GATHER_GRID, threads = 64 | 256
+usage: python tools/ablate.py [arm ...]     arm = <threads>[:<grid>]
+  threads = 64 | 256 | auto (OKV_GATHER_THREADS), grid = OKV_GATHER_GRID (0: one per block)
 env:   ABL_NBLK (65536), ABL_ROUNDS (5), ABL_KIND (1 = Zipf C3, 0 = fixed C2),
        ABL_BS (65536), ABL_TH (57344)
 """
@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import objectkv_amd as okv  # noqa: E402
 
-arms = sys.argv[1:] or ["global", "lds"]
+arms = sys.argv[1:] or ["auto", "64"]
 nblk = int(os.environ.get("ABL_NBLK", "65536"))
 rounds = int(os.environ.get("ABL_ROUNDS", "5"))
 kind = int(os.environ.get("ABL_KIND", "1"))
@@ -30,13 +30,9 @@ dev = torch.device("cuda", 0)
 stream = torch.cuda.current_stream(dev).cuda_stream
 decs = {}
 for a in arms:
-    mode, _, rest = a.partition(":")
-    grid, _, rest = rest.partition(":")
-    thr, _, var = rest.partition(":")
-    os.environ["OKV_GATHER_VARIANT"] = var or "0"
-    os.environ["OKV_GATHER"] = mode
+    thr, _, grid = a.partition(":")
     os.environ["OKV_GATHER_GRID"] = grid or "0"
-    if thr:
+    if thr in ("64", "256"):
         os.environ["OKV_GATHER_THREADS"] = thr
     else:
         os.environ.pop("OKV_GATHER_THREADS", None)

@@ -2,25 +2,31 @@
 """bench.py -- device-resident SST block decode throughput (BASELINE.json).
 
 One "step" = one batched ReadBlockWithStat over the whole per-GPU workload
-(okv_decode_blocks: count + scan + copy kernels), inputs already resident in
-HBM.  Default workload = BASELINE.json configs[2] (C3): 65 536 x 64 KiB
+(okv_decode_blocks: count + scan + gather kernels), inputs already resident
+in HBM.  Default workload = BASELINE.json configs[2] (C3): 65 536 x 64 KiB
 blocks, Zipf key 8-256 B / value 0-4096 B, full decode (keys and values
 materialised into packed arenas + SoA row index: Go's fresh-copy semantics).
 
-Multi-GPU (launched by torch.distributed.run): one process per GPU, each
-decodes its own segment (seed 3 + rank) -- blocks/segments are independent,
-so there is no data-path collective (weak scaling).  Timing: barrier +
-synchronize on both sides of K steps, max over ranks.
+Multi-GPU: one process per GPU, each decoding its own segment (seed 3 +
+rank) -- blocks/segments are independent, so there is no data-path
+collective (weak scaling).  `--gpus N` without a launcher spawns the N rank
+processes itself (before anything touches HIP); under torch.distributed.run
+WORLD_SIZE must equal N.  Timing: barrier + synchronize on both sides of K
+steps, max over ranks.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2]
-                    [--mode full|index] [--no-cpu] [--e2e]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+                    [--config c3|c2|c5|cz|c4|cm|c1] [--mode full|index]
+                    [--no-cpu] [--no-verify] [--e2e]
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -45,14 +51,22 @@ CONFIGS = {
     # encode: total rows (split across ranks by key range), key/value bytes
     "c4": ("encode", 1, 100_000_000, 3584, 4096,
            "C4: encode 100 M sorted pairs (16 B key / 64 B value) into 4 KiB blocks + "
-           "BlockStat index + meta block on device, key-range shards across GPUs"),
+           "BlockStat index + meta block + trailer (Close) on device, key-range shards across "
+           "GPUs"),
     # compaction: K overlapping L0 segments of n rows each -> one segment
     "cm": ("compact", 11, 16_000_000, 3584, 4096,
            "CM: compaction of 4 overlapping L0 segments x 16 M rows (16 B key / 64 B value, "
            "each overlapping the next by half): decode -> newest-wins merge -> encode, on device"),
+    # C1: one segment round trip of 10 000 rows (write + full ascending read)
+    "c1": ("roundtrip", 1, 10_000, 3584, 4096,
+           "C1: single segment round trip, 10 000 x 16 B key / 64 B value: write (WriteRow x n "
+           "+ Close) + full ascending read"),
 }
-ENC_METRIC = "GiB/s device-resident segment encode (data blocks written) + M rows/s"
+ENC_METRIC = "GiB/s device-resident segment encode (data blocks written, Close included) + M rows/s"
 CMP_METRIC = "GiB/s device-resident compaction (input segment bytes) + M rows/s"
+RT_METRIC = "MB/s segment round trip (write + full ascending read, segment bytes) + rows/s"
+DECODE_SOURCES = ("objectkv_amd/csrc/okv_decode.hip", "objectkv_amd/csrc/okv_kernels.hpp",
+                  "objectkv_amd/csrc/okv_ctx.hpp")
 
 
 def log(*a):
@@ -70,6 +84,165 @@ def cpu_model():
     return platform.processor()
 
 
+def host_cores():
+    """Cores this process may run on (the CPU baseline's thread count)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def thread_counts():
+    """CPU baseline thread counts: 1, 16, 64 and every core this process may
+    use.  Memory-allocation-heavy Go-semantics code can scale past its best
+    count into allocator contention, so the reported value is the best of
+    the sweep (with its thread count) and the all-cores figure is kept."""
+    c = host_cores()
+    return sorted({1, min(16, c), min(64, c), c})
+
+
+def sweep(run_once, budget_s):
+    """{threads: (units per second, passes, seconds)} for run_once(threads) ->
+    units done, each count run in whole passes until budget_s is spent."""
+    res = {}
+    for nth in thread_counts():
+        n_pass, t_cpu, units = 0, 0.0, 0.0
+        while t_cpu < budget_s:
+            t1 = time.perf_counter()
+            units += run_once(nth)
+            t_cpu += time.perf_counter() - t1
+            n_pass += 1
+        res[nth] = (units / t_cpu, n_pass, t_cpu)
+    return res
+
+
+def sweep_summary(res, scale, unit, kind, sample):
+    """cpu_baseline entry: the best thread count's rate as value."""
+    best = max(res, key=lambda k: res[k][0])
+    allc = max(res)
+    return {"value": round(res[best][0] * scale, 4), "unit": unit, "cores": best, "kind": kind,
+            "single_thread_value": round(res[1][0] * scale, 4),
+            "all_cores": {"cores": allc, "value": round(res[allc][0] * scale, 4)},
+            "by_threads": {str(k): round(v[0] * scale, 4) for k, v in sorted(res.items())},
+            "sample": sample + f"; host CPU: {cpu_model()}, nproc={os.cpu_count()}, "
+                               f"affinity={host_cores()}"}
+
+
+def source_sha(paths=DECODE_SOURCES):
+    h = hashlib.sha256()
+    for p in paths:
+        with open(os.path.join(ROOT, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(config, mode, kernel):
+    """HBM bytes per launch of `kernel` from profiles/r2/pmc_<config>_<mode>.json
+    -- used only if it was collected from the decode sources being timed
+    (same source_sha); else None."""
+    path = os.path.join(ROOT, "profiles", "r2", f"pmc_{config}_{mode}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    if d.get("source_sha") != source_sha():
+        return None, "stale (decode sources changed since the PMC run)"
+    for name, k in d.get("kernels", {}).items():
+        if kernel in name:
+            return k["hbm_bytes"], os.path.relpath(path, ROOT)
+    return None, None
+
+
+# ---- process launch ---------------------------------------------------------------
+
+
+def spawn_ranks(args, cmd=None):
+    """`--gpus N` without a launcher: start N rank processes (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_*) running this script with the same arguments, and
+    wait.  Runs before this process imports torch or touches HIP; only rank 0
+    prints the result line.  Returns the worst exit status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
+class Dist:
+    """Rank layout + the control-plane collectives (barrier, max and gather of
+    elapsed times).  No data-path collective exists: each rank owns its
+    segment(s)."""
+
+    def __init__(self, args, torch):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != args.gpus:
+            raise SystemExit(f"WORLD_SIZE={self.world} but --gpus {args.gpus}")
+        if args.device_mod:
+            self.local %= args.device_mod
+        self.torch = torch
+        self.backend = args.dist_backend
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device("cuda", self.local)
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist.init_process_group(self.backend)
+            assert dist.get_world_size() == self.world, (dist.get_world_size(), self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def gather(self, x: float):
+        """x from every rank (rank order)."""
+        if not self.dist:
+            return [x]
+        torch = self.torch
+        tdev = self.dev if self.backend == "nccl" else "cpu"
+        t = torch.tensor([x], dtype=torch.float64, device=tdev)
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [float(o.item()) for o in out]
+
+    def timed(self, step, steps):
+        """Barrier + synchronize, K steps, synchronize + barrier; returns
+        (max over ranks of the elapsed seconds, per-rank seconds)."""
+        torch = self.torch
+        self.barrier()
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize(self.dev)
+        el = time.perf_counter() - t0
+        self.barrier()
+        per = self.gather(el)
+        return max(per), per
+
+    def info(self):
+        return {"world_size": self.dist.get_world_size() if self.dist else 1,
+                "dist_backend": self.backend if self.dist else None}
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,40 +251,90 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="full", choices=["full", "index"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the oracle comparison of the bench outputs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--e2e", action="store_true", help="also time the host-buffer path")
+    ap.add_argument("--e2e", action="store_true",
+                    help="also time the pinned, pipelined host-buffer path (PCIe both ways)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="control-plane backend (barrier, max time); gloo for rehearsals")
     ap.add_argument("--device-mod", type=int, default=0,
                     help="rehearsal only: map LOCAL_RANK -> LOCAL_RANK %% N (ranks share a GPU)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args)
 
     import torch
 
     import objectkv_amd as okv
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.device_mod:
-        local %= args.device_mod
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(args.dist_backend)
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local)
+    D = Dist(args, torch)
+    kind = CONFIGS[args.config][0]
+    try:
+        if kind == "encode":
+            return run_encode(args, torch, okv, D)
+        if kind == "compact":
+            return run_compact(args, torch, okv, D)
+        if kind == "roundtrip":
+            return run_roundtrip(args, torch, okv, D)
+        return run_decode(args, torch, okv, D)
+    finally:
+        D.close()
 
-    if args.config == "c4":
-        return run_encode(args, torch, okv, dist, world, rank, local, dev)
-    if args.config == "cm":
-        return run_compact(args, torch, okv, dist, world, rank, local, dev)
+
+def emit(D, line):
+    if D.rank == 0:
+        print(json.dumps(line), flush=True)
+
+
+# ---- decode (C2 / C3 / C5 / CZ) ---------------------------------------------------
+
+
+def verify_decode(dec_out, seg, descs, comp, index_only, full, torch):
+    """The bench path's own outputs against the C oracle (oracle/coracle.py):
+    full = every output array; else the totals + 64 blocks spread over the
+    segment (their rows, lengths and arena bytes)."""
+    from oracle import coracle as CO
+    d = np.ascontiguousarray(descs, np.uint64)
+    host = {k: v.cpu().numpy() for k, v in dec_out.items()}
+    for k, dt in (("row_start", np.uint64), ("key_base", np.uint64), ("val_base", np.uint64),
+                  ("key_off", np.uint64), ("val_off", np.uint64), ("key_len", np.uint16),
+                  ("val_len", np.uint32)):
+        host[k] = host[k].view(dt)
+    nblk = d.shape[0]
+    if full:
+        ref = CO.decode_soa(seg, d.view(CO.DESC_DTYPE).reshape(-1), comp, index_only)
+        rows = int(ref["row_start"][-1])
+        keys = ["status", "row_start", "key_off", "key_len", "val_off", "val_len"]
+        if not index_only:
+            keys += ["key_base", "val_base"]
+        for k in keys:
+            got = host[k][:rows] if k in ("key_off", "key_len", "val_off", "val_len") else host[k]
+            assert np.array_equal(got, ref[k]), f"bench output {k} differs from the oracle"
+        if not index_only:
+            for k in ("key_arena", "val_arena"):
+                n = ref[k].size
+                assert np.array_equal(host[k][:n], ref[k]), f"bench output {k} differs"
+        return {"verified": "all output arrays == oracle (oref_decode_soa)", "rows": rows}
+    pick = np.unique(np.linspace(0, nblk - 1, min(64, nblk)).astype(np.int64))
+    for b in pick:
+        ref = CO.decode_soa(seg, d[b:b + 1].view(CO.DESC_DTYPE).reshape(-1), comp, index_only)
+        r0, r1 = int(host["row_start"][b]), int(host["row_start"][b + 1])
+        assert r1 - r0 == int(ref["row_start"][-1]) and host["status"][b] == ref["status"][0]
+        assert np.array_equal(host["key_len"][r0:r1], ref["key_len"])
+        assert np.array_equal(host["val_len"][r0:r1], ref["val_len"])
+        if not index_only:
+            kb, vb = int(host["key_base"][b]), int(host["val_base"][b])
+            assert np.array_equal(host["key_arena"][kb:kb + ref["key_arena"].size],
+                                  ref["key_arena"])
+            assert np.array_equal(host["val_arena"][vb:vb + ref["val_arena"].size],
+                                  ref["val_arena"])
+    return {"verified": f"{len(pick)} sampled blocks == oracle", "rows": None}
+
+
+def run_decode(args, torch, okv, D):
     kind, seed0, nblk, th, bs, desc = CONFIGS[args.config]
+    rank, world, dev = D.rank, D.world, D.dev
     seed = seed0 + rank
     t0 = time.time()
     comp = 0
@@ -129,10 +352,11 @@ def main():
         f"({nblk} blocks) in {time.time() - t0:.1f}s")
     in_bytes = int(descs[:, 1].sum())  # sum BlockSize (headline GiB/s numerator)
     orig_bytes = int(descs[:, 2].sum())
+    comp_bytes = int(descs[:, 3].sum())
 
     # ---- device-resident inputs ---------------------------------------------
     stream = torch.cuda.current_stream(dev)
-    dec = okv.Decoder(local, stream=stream.cuda_stream)
+    dec = okv.Decoder(D.local, stream=stream.cuda_stream)
     seg_t = torch.empty(seg.nbytes + 64, dtype=torch.uint8, device=dev)
     seg_t[:seg.nbytes].copy_(torch.from_numpy(seg))
     d_t = torch.from_numpy(descs.view(np.int64).copy()).to(dev)
@@ -155,95 +379,56 @@ def main():
         return dec.decode_device(seg_t, seg.nbytes, d_t, nblk, out, compression=comp,
                                  index_only=index_only, sync=sync)
 
-    # correctness guard on the bench path itself (totals + statuses)
+    # correctness guard on the bench path itself: totals, statuses, and the
+    # outputs against the oracle (every array on rank 0, sampled blocks elsewhere)
     o = step(sync=True)
     assert o.n_rows == rows and o.n_bad_blocks == 0, (o.n_rows, rows, o.n_bad_blocks)
+    ver = None
+    if not args.no_verify:
+        t1 = time.time()
+        ver = verify_decode(out, seg, descs, comp, index_only, rank == 0, torch)
+        ver["seconds"] = round(time.time() - t1, 1)
+        log(f"[rank {rank}] {ver['verified']} ({ver['seconds']} s)")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
 
     # ---- timed region ----------------------------------------------------------
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
     dec.profile(True)
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    t_elapsed = time.perf_counter() - t_start
-    if dist:
-        dist.barrier()
+    t_max, per = D.timed(step, args.steps)
     kern_ms, calls = dec.profile_read()
     dec.profile(False)
-    t_max = t_elapsed
-    if dist:
-        tdev = dev if args.dist_backend == "nccl" else "cpu"
-        tt = torch.tensor([t_elapsed], dtype=torch.float64, device=tdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
     ms_per_step = 1e3 * t_max / args.steps
 
-    # ---- roofline for the dominant kernel (pass 3) ------------------------------
-    copy_ms = kern_ms["copy"] / max(calls, 1)
-    count_ms = kern_ms["count"] / max(calls, 1)
-    scan_ms = kern_ms["scan"] / max(calls, 1)
+    # ---- roofline for the dominant kernel ------------------------------------------
+    ms = {k: v / max(calls, 1) for k, v in kern_ms.items()}
     if index_only:
         # index mode reads only the record headers: 6 B per row (+ the descs)
         alg = rows * 6 + rows * 22 + nblk * 12
+        roof_kernel, roof_ms = "okv_gather_kernel (index)", ms["copy"]
+    elif comp:
+        # the zstd stage dominates: compressed frames in, decompressed blocks out
+        alg = comp_bytes + orig_bytes
+        roof_kernel, roof_ms = "zstd stage (okv_zstd_* kernels)", ms["zstd"]
     else:
         # read OriginalSize per block; write payload (padded arenas) + 22 B/row
         # SoA (u64 key_off, u16 key_len, u64 val_off, u32 val_len) + 28 B/block
         alg = orig_bytes + payload + rows * 22 + nblk * 28
-    achieved = alg / (copy_ms * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.config}_{args.mode}.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            traffic = json.load(f).get("copy_kernel_hbm_bytes_per_launch")
+        roof_kernel, roof_ms = "okv_gather_kernel", ms["copy"]
+    achieved = alg / (roof_ms * 1e-3) / 1e9
+    traffic, traffic_src = (None, None) if comp else pmc_traffic(args.config, args.mode,
+                                                                 "okv_gather_kernel")
 
     # ---- CPU baseline (rank 0, N = 1 only) ---------------------------------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        from oracle import coracle
-        threads = min(16, os.cpu_count() or 1)
-        cd = coracle.descs_array([tuple(int(x) for x in d) for d in descs])
-        res = {}
-        for nth in (1, threads):
-            # bounded sample: whole passes over the first blocks until the budget is spent
-            sample = nblk if args.config not in ("c3", "cz") else 4096 * nth
-            sample = min(sample, nblk)
-            n_pass, t_cpu, nrows_cpu = 0, 0.0, 0
-            budget = args.cpu_seconds / 2
-            while t_cpu < budget:
-                t1 = time.perf_counter()
-                r_, _pay = coracle.decode_go(seg, cd[:sample], comp, nth)
-                t_cpu += time.perf_counter() - t1
-                n_pass += 1
-                nrows_cpu += r_
-            sbytes = int(descs[:sample, 1].sum()) * n_pass
-            res[nth] = (sbytes / t_cpu / 2**30, nrows_cpu / t_cpu, sample, n_pass, t_cpu)
-        v1, vN = res[1], res[threads]
-        cpu = {"value": round(vN[0], 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-               "rows_per_s": round(vN[1]), "single_thread_value": round(v1[0], 4),
-               "single_thread_rows_per_s": round(v1[1]),
-               "sample": (f"{vN[2]} of {nblk} blocks x {vN[3]} passes ({vN[4]:.1f}s) on "
-                          f"{threads} threads; 1 thread: {v1[2]} blocks x {v1[3]} passes "
-                          f"({v1[4]:.1f}s); C restatement of Go ReadBlockWithStat with Go "
-                          f"allocation semantics (Go toolchain unavailable); host CPU: "
-                          f"{cpu_model()}, nproc={os.cpu_count()}")}
+        cpu = cpu_decode_baseline(args, seg, descs, nblk, comp)
 
-    # ---- optional end-to-end (host buffers, PCIe both ways) -----------------------
     e2e = None
-    if args.e2e and rank == 0:
-        t1 = time.perf_counter()
-        n_e2e = 3
-        for _ in range(n_e2e):
-            got = dec.decode(seg, descs, compression=comp, index_only=index_only)
-        t_e2e = (time.perf_counter() - t1) / n_e2e
-        e2e = {"GiB_s": round(in_bytes / t_e2e / 2**30, 3), "ms": round(t_e2e * 1e3, 2),
-               "note": "pageable host buffers, H2D + plan + decode + D2H, synchronous"}
-        del got
+    if args.e2e and rank == 0 and world == 1:
+        from tools.e2e import run_e2e
+        dec.close()
+        e2e = run_e2e(args.config, torch=torch)
 
     total_in = in_bytes * world
     total_rows = rows * world
@@ -262,35 +447,65 @@ def main():
         "rows_per_s": round(total_rows / (t_max / args.steps)),
         "mrows_per_s": round(total_rows / (t_max / args.steps) / 1e6, 3),
         "original_GiB_s": round(orig_bytes * world / (t_max / args.steps) / 2**30, 3),
-        "kernel_ms": {"count": round(count_ms, 4), "scan": round(scan_ms, 4),
-                      "copy": round(copy_ms, 4)},
+        "per_rank_ms_per_step": [round(1e3 * p / args.steps, 4) for p in per],
+        "kernel_ms": {k: round(v, 4) for k, v in ms.items()},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": "okv_gather_kernel" if not index_only
-                     else "okv_gather_kernel (index)", "algorithmic_bytes_per_launch": int(alg)},
+                     "traffic": traffic, "kernel": roof_kernel,
+                     "algorithmic_bytes_per_launch": int(alg),
+                     "timing": "HIP events around the kernel on its stream, averaged over the "
+                               "timed steps",
+                     "traffic_source": traffic_src, "decode_source_sha": source_sha()},
         "cpu_baseline": cpu,
+        "verify": ver,
+        "dist": D.info(),
     }
     if e2e:
         line["e2e"] = e2e
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    dec.close()
-    if dist:
-        dist.destroy_process_group()
+    emit(D, line)
+    if not e2e:
+        dec.close()
 
 
-def run_encode(args, torch, okv, dist, world, rank, local, dev):
+def cpu_decode_baseline(args, seg, descs, nblk, comp):
+    """The C restatement of ReadBlockWithStat with Go's allocation semantics
+    (per-block buffer copy, per-row key/value heap copies), swept over thread
+    counts (thread t decodes a contiguous block range of the sample)."""
+    from oracle import coracle
+    cd = np.ascontiguousarray(descs, np.uint64).view(coracle.DESC_DTYPE).reshape(-1)
+    big = args.config in ("c3", "cz", "c5")
+    samples = {}
+
+    def once(nth):
+        sample = min(nblk, 4096 * nth if big else nblk)
+        samples[nth] = sample
+        coracle.decode_go(seg, cd[:sample], comp, nth)
+        return int(descs[:sample, 1].sum())
+    res = sweep(once, args.cpu_seconds / len(thread_counts()))
+    return sweep_summary(res, 1 / 2**30, "GiB/s", "port",
+                         f"first min({nblk}, 4096 x threads) blocks per pass (all {nblk} at "
+                         f"{max(res)} threads), whole passes for "
+                         f"{args.cpu_seconds / len(thread_counts()):.1f} s per thread count; C "
+                         f"restatement of Go ReadBlockWithStat with Go allocation semantics (Go "
+                         f"toolchain unavailable)")
+
+
+# ---- encode (C4) ------------------------------------------------------------------
+
+
+def run_encode(args, torch, okv, D):
     """C4: okv_encode_rows over rows resident in HBM.  One step = the whole
-    device encode of this rank's key-range shard (cut + pack + block hash +
-    meta block, OKV_F_NO_CLOSE); the meta XXH64 + trailer (one sequential hash,
-    host) is timed separately as `close_ms`.  Total rows fixed across N:
-    strong scaling."""
+    encode of this rank's key-range shard, Close included: cut + pack + block
+    hash + meta block on device, then the meta block's XXH64 and the 25-byte
+    trailer (one sequential hash over the meta block, on the host).  Total
+    rows fixed across N: strong scaling."""
     _, seed, total_rows, th, bs, desc = CONFIGS["c4"]
+    rank, world, dev = D.rank, D.world, D.dev
     KL, VL = 16, 64
     lo, hi = total_rows * rank // world, total_rows * (rank + 1) // world
     n = hi - lo
     stream = torch.cuda.current_stream(dev)
-    enc = okv.Encoder(local, stream=stream.cuda_stream)
+    enc = okv.Encoder(D.local, stream=stream.cuda_stream)
     t0 = time.time()
     rows = dict(key_arena=torch.empty(n * KL, dtype=torch.uint8, device=dev),
                 key_off=torch.empty(n, dtype=torch.int64, device=dev),
@@ -311,93 +526,59 @@ def run_encode(args, torch, okv, dist, world, rank, local, dev):
     log(f"[rank {rank}] generated {n} rows ({n * (KL + VL) / 2**30:.2f} GiB payload) "
         f"in {time.time() - t0:.1f}s")
 
-    # correctness guard: full encode with close; block count/sizes; the first
-    # blocks against the CPU writer; every block hash re-verified on device
-    eo = enc.encode_device(rows, n, out, threshold=th, block_size=bs, strict_go=False)
+    def step():
+        return enc.encode_device(rows, n, out, threshold=th, block_size=bs, strict_go=False)
+
+    # correctness guard: the whole segment file against the oracle writer on
+    # rank 0 (tests/test_full_size_gpu.py does the same at 100 M rows); block
+    # count/sizes and device-rehashed blocks on every rank
+    eo = step()
     assert eo.n_blocks == nb and eo.data_bytes == nb * bs, (eo.n_blocks, nb)
-    from oracle import coracle
-    w = coracle.Writer(th, bs)
-    nchk = min(n, 3 * per_block + 1)
-    ka = rows["key_arena"][:nchk * KL].cpu().numpy().tobytes()
-    va = rows["val_arena"][:nchk * VL].cpu().numpy().tobytes()
-    for i in range(nchk):
-        assert w.write_row(ka[i * KL:(i + 1) * KL], va[i * VL:(i + 1) * VL]) == 0
-    _, want, _ = w.close()
-    nfull = min(3, nb - 1)
-    assert out["seg"][:nfull * bs].cpu().numpy().tobytes() == want[:nfull * bs]
     hv = torch.empty(nb, dtype=torch.int64, device=dev)
     enc._check(okv._lib.lib().okv_hash_blocks(enc._ctx, out["seg"].data_ptr(), eo.data_bytes,
                                                out["desc"].data_ptr(), nb, hv.data_ptr(),
                                                okv._lib.F_DEVICE_PTRS), "hash")
     assert torch.equal(hv, out["hash"][:nb])
-    data_bytes, meta_bytes = eo.data_bytes, eo.meta_bytes
-
-    def step():
-        return enc.encode_device(rows, n, out, threshold=th, block_size=bs, strict_go=False,
-                                 close=False)
+    ver = None
+    if rank == 0 and not args.no_verify:
+        from oracle import coracle
+        t1 = time.time()
+        host = {k: v.cpu().numpy() for k, v in rows.items()}
+        for k, dt in (("key_off", np.uint64), ("val_off", np.uint64), ("key_len", np.uint16),
+                      ("val_len", np.uint32)):
+            host[k] = host[k].view(dt)
+        want = coracle.encode_soa(host, n, th, bs)
+        assert want.rc == 0 and want.file.size == eo.file_bytes
+        step_b = 1 << 28
+        for i in range(0, want.file.size, step_b):
+            j = min(want.file.size, i + step_b)
+            assert np.array_equal(out["seg"][i:j].cpu().numpy(), want.file[i:j]), (i, j)
+        del host, want
+        ver = {"verified": "whole segment file == oracle writer (oref_encode_soa)",
+               "seconds": round(time.time() - t1, 1)}
+        log(f"[rank {rank}] {ver['verified']} ({ver['seconds']} s)")
+    data_bytes, meta_bytes, file_bytes = eo.data_bytes, eo.meta_bytes, eo.file_bytes
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
     enc.profile(True)
     enc.profile_reset_encode()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        eo = step()
-    torch.cuda.synchronize(dev)
-    t_elapsed = time.perf_counter() - t_start
-    if dist:
-        dist.barrier()
+    t_max, per = D.timed(step, args.steps)
     ph, calls = enc.profile_read_encode()
     enc.profile(False)
-    t1 = time.perf_counter()
-    enc.close_device(eo)
-    close_ms = (time.perf_counter() - t1) * 1e3
-    t_max = t_elapsed
-    if dist:
-        tdev = dev if args.dist_backend == "nccl" else "cpu"
-        tt = torch.tensor([t_elapsed], dtype=torch.float64, device=tdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
     t_step = t_max / args.steps
     ph = {k: v / max(calls, 1) for k, v in ph.items()}
+    # device-only step (no Close), for reference
+    t_dev, _ = D.timed(lambda: enc.encode_device(rows, n, out, threshold=th, block_size=bs,
+                                                 strict_go=False, close=False), args.steps)
     # pack kernel: read payload (16+64 B/row) + SoA (22 B/row), write the padded blocks
     alg = n * (KL + VL) + n * 22 + data_bytes
     achieved = alg / (ph["pack"] * 1e-3) / 1e9
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = min(16, os.cpu_count() or 1)
-        sample = min(n, 8_000_000)
-        host = {k: rows[k][:sample].cpu().numpy() for k in ("key_off", "key_len", "val_off",
-                                                             "val_len")}
-        host["key_off"] = host["key_off"].view(np.uint64)
-        host["val_off"] = host["val_off"].view(np.uint64)
-        host["key_len"] = host["key_len"].view(np.uint16)
-        host["val_len"] = host["val_len"].view(np.uint32)
-        host["key_arena"] = rows["key_arena"][:sample * KL].cpu().numpy()
-        host["val_arena"] = rows["val_arena"][:sample * VL].cpu().numpy()
-        res = {}
-        for nth, ns in ((1, min(sample, 1_000_000)), (threads, sample)):
-            n_pass, t_cpu, fb = 0, 0.0, 0
-            while t_cpu < args.cpu_seconds / 2:
-                t2 = time.perf_counter()
-                fb += coracle.encode_go(host, ns, th, bs, False, nth)
-                t_cpu += time.perf_counter() - t2
-                n_pass += 1
-            res[nth] = (ns * n_pass / t_cpu, fb / t_cpu / 2**30, ns, n_pass, t_cpu)
-        v1, vN = res[1], res[threads]
-        cpu = {"value": round(vN[1], 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-               "rows_per_s": round(vN[0]), "single_thread_value": round(v1[1], 4),
-               "single_thread_rows_per_s": round(v1[0]),
-               "sample": (f"{vN[2]} rows x {vN[3]} passes ({vN[4]:.1f}s) as {threads} "
-                          f"key-range segments on {threads} threads; 1 thread: {v1[2]} rows x "
-                          f"{v1[3]} passes ({v1[4]:.1f}s); C restatement of Go "
-                          f"WriteRow+Close with per-row rowBuf allocation (Go toolchain "
-                          f"unavailable); host CPU: {cpu_model()}")}
+        cpu = cpu_encode_baseline(args, rows, n, th, bs)
 
     line = {
         "metric": ENC_METRIC, "value": round(data_bytes * world / t_step / 2**30, 3),
@@ -406,23 +587,51 @@ def run_encode(args, torch, okv, dist, world, rank, local, dev):
         "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": desc, "rows_total": total_rows, "rows_per_gpu": n,
                    "blocks_per_gpu": nb, "data_bytes_per_gpu": data_bytes,
-                   "meta_bytes_per_gpu": meta_bytes, "threshold": th, "block_size": bs,
+                   "meta_bytes_per_gpu": meta_bytes, "file_bytes_per_gpu": file_bytes,
+                   "threshold": th, "block_size": bs,
                    "parallelism": f"{world} key-range shards, one segment each (no collective)"},
         "rows_per_s": round(total_rows / t_step),
         "mrows_per_s": round(total_rows / t_step / 1e6, 3),
+        "per_rank_ms_per_step": [round(1e3 * p / args.steps, 4) for p in per],
+        "device_only_ms_per_step": round(1e3 * t_dev / args.steps, 4),
         "kernel_ms": {k: round(v, 4) for k, v in ph.items()},
-        "close_ms": round(close_ms, 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                      "kernel": "okv_enc_pack_lds_kernel (pack + block XXH64)",
                      "algorithmic_bytes_per_launch": int(alg)},
         "cpu_baseline": cpu,
+        "verify": ver,
+        "dist": D.info(),
     }
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+    emit(D, line)
     enc.close()
-    if dist:
-        dist.destroy_process_group()
+
+
+def cpu_encode_baseline(args, rows, n, th, bs):
+    """The C writer restatement with Go's per-row rowBuf allocation, threads
+    writing key-range shards as separate segments."""
+    from oracle import coracle
+    sample = min(n, 8_000_000)
+    host = {k: rows[k][:sample].cpu().numpy() for k in ("key_off", "key_len", "val_off",
+                                                         "val_len")}
+    host["key_off"] = host["key_off"].view(np.uint64)
+    host["val_off"] = host["val_off"].view(np.uint64)
+    host["key_len"] = host["key_len"].view(np.uint16)
+    host["val_len"] = host["val_len"].view(np.uint32)
+    host["key_arena"] = rows["key_arena"][:sample * 16].cpu().numpy()
+    host["val_arena"] = rows["val_arena"][:sample * 64].cpu().numpy()
+
+    def once(nth):
+        ns = min(sample, 1_000_000 * nth)
+        return coracle.encode_go(host, ns, th, bs, False, nth)
+    res = sweep(once, args.cpu_seconds / len(thread_counts()))
+    return sweep_summary(res, 1 / 2**30, "GiB/s", "port",
+                         f"min({sample}, 1 M x threads) rows per pass as one key-range segment "
+                         f"per thread; C restatement of Go WriteRow+Close with per-row rowBuf "
+                         f"allocation (Go toolchain unavailable); segment bytes written / s")
+
+
+# ---- compaction (CM) -----------------------------------------------------------------
 
 
 def _fixed_vals(seed, r0, n, vl=64):
@@ -436,7 +645,7 @@ def _fixed_vals(seed, r0, n, vl=64):
     return z.astype("<u8").view(np.uint8).reshape(n, vl)
 
 
-def run_compact(args, torch, okv, dist, world, rank, local, dev):
+def run_compact(args, torch, okv, D):
     """CM: one compaction step on device-resident segments -- the compactor the
     reference leaves as a stub (sst/compactor.go:3-6) over its own merge rule
     (GetRange: newest L0 segment owns a key, snapshot_reader.go:294-331).
@@ -449,10 +658,11 @@ def run_compact(args, torch, okv, dist, world, rank, local, dev):
     from objectkv_amd import _lib
     from objectkv_amd.snapshot import _Addr
     _, seed0, n, th, bs, desc = CONFIGS["cm"]
+    rank, world, dev = D.rank, D.world, D.dev
     K, KL, VL = 4, 16, 64
     seed0 += 100 * rank
     stream = torch.cuda.current_stream(dev)
-    enc = okv.Encoder(local, stream=stream.cuda_stream)
+    enc = okv.Encoder(D.local, stream=stream.cuda_stream)
     per_block = -(-th // (6 + KL + VL))
 
     def out_for(rows):
@@ -493,7 +703,7 @@ def run_compact(args, torch, okv, dist, world, rank, local, dev):
                           val_len=torch.empty(r, dtype=torch.int32, device=dev),
                           key_arena=torch.empty(max(kb, 16), dtype=torch.uint8, device=dev),
                           val_arena=torch.empty(max(vb, 16), dtype=torch.uint8, device=dev),
-                          rows=r))
+                          rows=r, kb=kb, vb=vb))
     n_in = sum(d["rows"] for d in douts)
     order = list(range(K - 1, -1, -1))  # newest (highest s) first
     kb0 = min(douts[s]["key_arena"].data_ptr() for s in order)
@@ -555,27 +765,29 @@ def run_compact(args, torch, okv, dist, world, rank, local, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    t_elapsed = time.perf_counter() - t_start
-    if dist:
-        dist.barrier()
-    t_max = t_elapsed
-    if dist:
-        tdev = dev if args.dist_backend == "nccl" else "cpu"
-        tt = torch.tensor([t_elapsed], dtype=torch.float64, device=tdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
+    enc.profile(True)
+    t_max, per = D.timed(step, args.steps)
+    kern_ms, calls = enc.profile_read()  # the K decodes of every step
+    enc.profile(False)
     t_step = t_max / args.steps
     ph = np.zeros(3)  # untimed diagnostic pass: per-stage wall time
     for _ in range(2):
         step(ph)
     ph *= 1e3 / 2
+    # roofline of the decode stage's gather kernel (the largest kernel of the
+    # step): per step K launches over all input blocks
+    gather_ms = kern_ms["copy"] / max(calls, 1) * K
+    orig = 0
+    for seg_t, fb, d_t, nb in segs:
+        orig += int(d_t[:, 2].sum().item())
+    alg = orig + sum(d["kb"] + d["vb"] for d in douts) + n_in * 22 + \
+        sum(nb for *_x, nb in segs) * 28
+    achieved = alg / (gather_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_compact_baseline(args, segs, n, per_block, th, bs, K)
+
     line = {
         "metric": CMP_METRIC, "value": round(in_bytes * world / t_step / 2**30, 3),
         "unit": "GiB/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -587,16 +799,144 @@ def run_compact(args, torch, okv, dist, world, rank, local, dev):
                    "parallelism": f"{world} independent compactions (no collective)"},
         "rows_per_s": round(n_in * world / t_step),
         "mrows_per_s": round(n_in * world / t_step / 1e6, 3),
+        "per_rank_ms_per_step": [round(1e3 * p / args.steps, 4) for p in per],
         "stage_ms": {"decode": round(ph[0], 4), "merge": round(ph[1], 4),
                      "encode": round(ph[2], 4)},
-        "roofline": None, "cpu_baseline": None,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": f"okv_gather_kernel (decode stage, {K} launches per step)",
+                     "algorithmic_bytes_per_launch": int(alg / K),
+                     "kernel_ms_per_step": round(gather_ms, 4)},
+        "cpu_baseline": cpu,
+        "dist": D.info(),
     }
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+    emit(D, line)
     enc.close()
-    if dist:
-        dist.destroy_process_group()
+
+
+def cpu_compact_baseline(args, segs, n, per_block, th, bs, K):
+    """The compaction step on the host: every sampled block of the K segments
+    decoded with ReadBlockWithStat's semantics, merged newest-first, written
+    with the Go writer (oref_compact_go).  Sample: the blocks of each segment
+    that hold global rows [n/2 + n/8, n/2 + n/8 + m) -- a key range covered
+    by two or three segments, so the merge resolves real overlaps."""
+    from oracle import coracle
+    m = 200_000
+    x0 = n // 2 + n // 8
+    host = []
+    for s in range(K - 1, -1, -1):  # newest first
+        seg_t, fb, d_t, nb = segs[s]
+        lo_row = s * n // 2
+        r0, r1 = max(x0, lo_row), min(x0 + m, lo_row + n)
+        if r0 >= r1:
+            continue
+        b0, b1 = (r0 - lo_row) // per_block, -(-(r1 - lo_row) // per_block)
+        d = d_t[b0:b1].cpu().numpy().view(np.uint64).copy()
+        base = int(d[0, 0])
+        end = int(d[-1, 0] + d[-1, 1])
+        part = seg_t[base:end].cpu().numpy()
+        d[:, 0] -= base
+        host.append((part, d.view(coracle.DESC_DTYPE).reshape(-1)))
+    in_b = sum(int(d["block_size"].sum()) for _p, d in host)
+    out_rows = {}
+
+    def once(nth):
+        out_rows[nth], _ob = coracle.compact_go(host, th, bs, nth)
+        return in_b * nth
+    res = sweep(once, args.cpu_seconds / len(thread_counts()))
+    return sweep_summary(res, 1 / 2**30, "GiB/s", "port",
+                         f"{len(host)} segments' blocks holding rows [{x0}, {x0 + m}) "
+                         f"({in_b} B in, {out_rows[1]} rows out) per compaction, one "
+                         f"independent compaction per thread; C restatement: "
+                         f"ReadBlockWithStat per block, newest-wins merge, Go writer (the "
+                         f"reference's compactor is a stub)")
+
+
+# ---- C1 round trip ---------------------------------------------------------------------
+
+
+def run_roundtrip(args, torch, okv, D):
+    """C1: 10 000 16/64 rows -> one segment -> a full ascending read.  GPU: the
+    rows resident in HBM, okv_encode_rows (Close included) then okv_decode_blocks
+    of every block of the new segment (a batched RowIter's reads); CPU: the C
+    restatement of WriteRow/Close + ReadBlockWithStat with Go's allocations, on
+    1 thread and as independent round trips on every core.  Segment bytes
+    (992 878 B) are the MB/s numerator."""
+    _, seed, n, th, bs, desc = CONFIGS["c1"]
+    rank, world, dev = D.rank, D.world, D.dev
+    stream = torch.cuda.current_stream(dev)
+    enc = okv.Encoder(D.local, stream=stream.cuda_stream)
+    rows = dict(key_arena=torch.empty(n * 16, dtype=torch.uint8, device=dev),
+                key_off=torch.empty(n, dtype=torch.int64, device=dev),
+                key_len=torch.empty(n, dtype=torch.int16, device=dev),
+                val_arena=torch.empty(n * 64, dtype=torch.uint8, device=dev),
+                val_off=torch.empty(n, dtype=torch.int64, device=dev),
+                val_len=torch.empty(n, dtype=torch.int32, device=dev))
+    enc.synth_fixed_device(seed, 0, n, 16, 64, rows)
+    nb = -(-n // 42)
+    out = dict(seg=torch.empty(nb * bs + (nb + 1) * 58 + 4096, dtype=torch.uint8, device=dev),
+               desc=torch.empty((nb + 1, 4), dtype=torch.int64, device=dev))
+    eo = enc.encode_device(rows, n, out, threshold=th, block_size=bs, strict_go=True)
+    fb = int(eo.file_bytes)
+    r, kb, vb = enc.plan_device(out["seg"], fb, out["desc"], nb)
+    dout = dict(row_start=torch.empty(nb + 1, dtype=torch.int64, device=dev),
+                key_base=torch.empty(nb, dtype=torch.int64, device=dev),
+                val_base=torch.empty(nb, dtype=torch.int64, device=dev),
+                status=torch.empty(nb, dtype=torch.int32, device=dev),
+                key_off=torch.empty(r, dtype=torch.int64, device=dev),
+                key_len=torch.empty(r, dtype=torch.int16, device=dev),
+                val_off=torch.empty(r, dtype=torch.int64, device=dev),
+                val_len=torch.empty(r, dtype=torch.int32, device=dev),
+                key_arena=torch.empty(max(kb, 16), dtype=torch.uint8, device=dev),
+                val_arena=torch.empty(max(vb, 16), dtype=torch.uint8, device=dev))
+
+    def step():
+        e = enc.encode_device(rows, n, out, threshold=th, block_size=bs, strict_go=True)
+        enc.decode_device(out["seg"], int(e.file_bytes), out["desc"], nb, dout, sync=False)
+
+    step()
+    torch.cuda.synchronize(dev)
+    assert r == n and torch.equal(dout["key_arena"][:n * 16], rows["key_arena"])
+    assert torch.equal(dout["val_arena"][:n * 64], rows["val_arena"])
+    from oracle import coracle
+    host = {k: v.cpu().numpy() for k, v in rows.items()}
+    for k, dt in (("key_off", np.uint64), ("val_off", np.uint64), ("key_len", np.uint16),
+                  ("val_len", np.uint32)):
+        host[k] = host[k].view(dt)
+    want = coracle.encode_soa(host, n, th, bs)
+    assert want.rc == 0 and out["seg"][:fb].cpu().numpy().tobytes() == want.file.tobytes()
+    for _ in range(args.warmup):
+        step()
+    t_max, per = D.timed(step, args.steps)
+    t_step = t_max / args.steps
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        def once(nth):
+            _r, b_ = coracle.roundtrip_go(host, n, th, bs, nth)
+            return b_
+        res = sweep(once, args.cpu_seconds / len(thread_counts()))
+        cpu = sweep_summary(res, 1e-6, "MB/s", "port",
+                            "the whole C1 round trip per pass, one independent segment per "
+                            "thread; C restatement of Go WriteRow/Close + ReadBlockWithStat "
+                            "with Go allocations")
+    line = {
+        "metric": RT_METRIC, "value": round(fb * world / t_step / 1e6, 3), "unit": "MB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(t_step * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": desc, "rows": n, "blocks": nb, "file_bytes": fb,
+                   "parallelism": f"{world} independent round trips (no collective)"},
+        "rows_per_s": round(n * world / t_step),
+        "per_rank_ms_per_step": [round(1e3 * p / args.steps, 4) for p in per],
+        "roofline": None,
+        "cpu_baseline": cpu,
+        "verify": {"verified": "segment == oracle writer; decoded arenas == input rows"},
+        "dist": D.info(),
+    }
+    emit(D, line)
+    enc.close()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

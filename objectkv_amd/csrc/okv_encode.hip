@@ -103,7 +103,8 @@ struct EncScratch {
   size_t cap_in = 0;
   uint8_t* d_outseg = nullptr;
   size_t cap_outseg = 0;
-  std::vector<uint8_t> meta_host;
+  uint8_t* close_buf[2] = {nullptr, nullptr};  // pinned D2H chunks of the meta block (Close)
+  hipEvent_t close_ev[2] = {nullptr, nullptr};
   // profiling (okv_encode_profile_read): cut, pack, hash, meta
   std::vector<hipEvent_t> ev;
   size_t ev_used = 0;
@@ -120,6 +121,10 @@ void enc_release(okv_ctx* ctx) {
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->h_tot) (void)hipHostFree(e->h_tot);
+  for (int i = 0; i < 2; ++i) {
+    if (e->close_buf[i]) (void)hipHostFree(e->close_buf[i]);
+    if (e->close_ev[i]) (void)hipEventDestroy(e->close_ev[i]);
+  }
   for (hipEvent_t v : e->ev) (void)hipEventDestroy(v);
   delete e;
   ctx->enc = nullptr;
@@ -1567,13 +1572,92 @@ void trailer_bytes(uint64_t meta_off, uint64_t meta_hash, uint8_t t[25]) {
   t[16] = 1;
 }
 
+// XXH64 over a byte stream fed in 32-byte-multiple pieces (segment_writer.go:248
+// hashes the meta block with xxhash.Sum64: canonical XXH64, seed 0).
+struct Xxh64Stream {
+  static constexpr uint64_t P1 = 11400714785074694791ULL, P2 = 14029467366897019727ULL,
+                            P3 = 1609587929392839161ULL, P4 = 9650029242287828579ULL,
+                            P5 = 2870177450012600261ULL;
+  uint64_t v[4] = {P1 + P2, P2, 0, 0 - P1};
+  uint64_t len = 0;
+  static uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+  static uint64_t rd64(const uint8_t* p) {
+    uint64_t x;
+    memcpy(&x, p, 8);
+    return x;
+  }
+  static uint64_t xr(uint64_t acc, uint64_t in) { return rotl(acc + in * P2, 31) * P1; }
+  void stripes(const uint8_t* p, uint64_t n) {  // n % 32 == 0
+    uint64_t a = v[0], b = v[1], c = v[2], d = v[3];
+    for (const uint8_t* end = p + n; p < end; p += 32) {
+      a = xr(a, rd64(p));
+      b = xr(b, rd64(p + 8));
+      c = xr(c, rd64(p + 16));
+      d = xr(d, rd64(p + 24));
+    }
+    v[0] = a, v[1] = b, v[2] = c, v[3] = d;
+    len += n;
+  }
+  uint64_t finish(const uint8_t* p, uint64_t n) {  // the last n < 32 bytes
+    const uint64_t total = len + n;
+    uint64_t h;
+    if (len) {
+      h = rotl(v[0], 1) + rotl(v[1], 7) + rotl(v[2], 12) + rotl(v[3], 18);
+      for (uint64_t x : v) h = (h ^ xr(0, x)) * P1 + P4;
+    } else {
+      h = P5;
+    }
+    h += total;
+    const uint8_t* end = p + n;
+    for (; p + 8 <= end; p += 8) h = rotl(h ^ xr(0, rd64(p)), 27) * P1 + P4;
+    if (p + 4 <= end) {
+      uint32_t w;
+      memcpy(&w, p, 4);
+      h = rotl(h ^ (uint64_t(w) * P1), 23) * P2 + P3;
+      p += 4;
+    }
+    for (; p < end; ++p) h = rotl(h ^ (uint64_t(*p) * P5), 11) * P1;
+    h ^= h >> 33;
+    h *= P2;
+    h ^= h >> 29;
+    h *= P3;
+    h ^= h >> 32;
+    return h;
+  }
+};
+
+// Close (segment_writer.go:226-276) on a device segment: the meta block comes
+// back in pinned 8 MiB pieces on the context stream, double-buffered so the
+// next piece's D2H overlaps this piece's XXH64; then the 25-byte trailer.
 int close_device(okv_ctx* ctx, EncScratch* e, okv_encode_out* out) {
+  constexpr uint64_t kPiece = 8ull << 20;  // multiple of 32 (XXH64 stripes)
   uint8_t* meta = out->seg + out->data_bytes;
-  e->meta_host.resize(out->meta_bytes);
-  OKV_HIP(hipMemcpyAsync(e->meta_host.data(), meta, out->meta_bytes, hipMemcpyDeviceToHost,
-                         ctx->stream));
-  OKV_HIP(hipStreamSynchronize(ctx->stream));
-  out->meta_hash = okv_xxh64(e->meta_host.data(), e->meta_host.size(), 0);  // :248
+  for (int i = 0; i < 2; ++i) {
+    if (!e->close_buf[i]) OKV_HIP(hipHostMalloc(reinterpret_cast<void**>(&e->close_buf[i]),
+                                                kPiece, 0));
+    if (!e->close_ev[i]) OKV_HIP(hipEventCreateWithFlags(&e->close_ev[i],
+                                                         hipEventDisableTiming));
+  }
+  const uint64_t mb = out->meta_bytes, np = (mb + kPiece - 1) / kPiece;
+  auto issue = [&](uint64_t k) -> int {
+    const uint64_t o = k * kPiece, n = std::min(kPiece, mb - o);
+    OKV_HIP(hipMemcpyAsync(e->close_buf[k & 1], meta + o, n, hipMemcpyDeviceToHost,
+                           ctx->stream));
+    OKV_HIP(hipEventRecord(e->close_ev[k & 1], ctx->stream));
+    return OKV_OK;
+  };
+  Xxh64Stream xs;
+  int rc;
+  if (np && (rc = issue(0))) return rc;
+  for (uint64_t k = 0; k < np; ++k) {
+    OKV_HIP(hipEventSynchronize(e->close_ev[k & 1]));
+    if (k + 1 < np && (rc = issue(k + 1))) return rc;
+    const uint64_t n = std::min(kPiece, mb - k * kPiece);
+    const uint64_t whole = k + 1 < np ? n : n & ~uint64_t(31);
+    xs.stripes(e->close_buf[k & 1], whole);
+    if (k + 1 == np) out->meta_hash = xs.finish(e->close_buf[k & 1] + whole, n - whole);
+  }
+  if (!np) out->meta_hash = xs.finish(nullptr, 0);
   static thread_local uint8_t t[25];
   trailer_bytes(out->data_bytes, out->meta_hash, t);
   OKV_HIP(hipMemcpyAsync(meta + out->meta_bytes, t, 25, hipMemcpyHostToDevice, ctx->stream));

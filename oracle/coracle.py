@@ -70,6 +70,11 @@ def lib():
                                      C.POINTER(u64)]
         L.oref_encode_soa.restype = p
         L.oref_encode_soa.argtypes = [p, p, p, p, p, p, u64, u64, u64, C.POINTER(C.c_int)]
+        L.oref_roundtrip_go.restype = u64
+        L.oref_roundtrip_go.argtypes = [p, p, p, p, p, p, u64, u64, u64, C.c_int,
+                                        C.POINTER(u64)]
+        L.oref_compact_go.restype = u64
+        L.oref_compact_go.argtypes = [C.c_int, p, p, p, p, u64, u64, C.c_int, C.POINTER(u64)]
         L.oref_decode_range_go.restype = u64
         L.oref_decode_range_go.argtypes = [p, u64, p, u64, C.c_int, C.c_int, C.POINTER(u64)]
         L.oref_block_counts.argtypes = [p, u64, p, u64, C.c_int, p, p, p, p]
@@ -260,3 +265,28 @@ def encode_go(rows: dict, n, threshold=3584, block_size=4096, lz4=False, threads
     if rc:
         raise RuntimeError(f"oref_encode_go: {rc}")
     return fb.value
+
+
+def roundtrip_go(rows: dict, n, threshold=3584, block_size=4096, threads=1):
+    """CPU baseline of C1 (write + full ascending read, Go semantics) on
+    `threads` concurrent copies; returns (rows read, segment bytes) summed."""
+    fb = C.c_uint64()
+    r = lib().oref_roundtrip_go(_ptr(rows["key_arena"]), _ptr(rows["key_off"]),
+                                _ptr(rows["key_len"]), _ptr(rows["val_arena"]),
+                                _ptr(rows["val_off"]), _ptr(rows["val_len"]), n, threshold,
+                                block_size, threads, C.byref(fb))
+    return r, fb.value
+
+
+def compact_go(segs, threshold=3584, block_size=4096, threads=1):
+    """CPU baseline of one compaction step: segs = [(segment bytes (numpy),
+    descs (DESC_DTYPE array)), ...] newest first; `threads` concurrent copies.
+    Returns (merged rows of one compaction, output bytes summed)."""
+    k = len(segs)
+    sp = (C.c_void_p * k)(*[s.ctypes.data for s, _ in segs])
+    ln = (C.c_uint64 * k)(*[s.nbytes for s, _ in segs])
+    dp = (C.c_void_p * k)(*[d.ctypes.data for _, d in segs])
+    nb = (C.c_uint64 * k)(*[len(d) for _, d in segs])
+    ob = C.c_uint64()
+    r = lib().oref_compact_go(k, sp, ln, dp, nb, threshold, block_size, threads, C.byref(ob))
+    return r, ob.value

@@ -672,6 +672,182 @@ oref_writer *oref_encode_soa(const uint8_t *key_arena, const uint64_t *key_off,
 }
 
 /* ======================================================================= */
+/* CPU baselines for bench.py configs C1 and CM (Go semantics)               */
+/* ======================================================================= */
+/* C1: one segment round trip -- WriteRow x n with Go's per-row rowBuf
+ * (segment_writer.go:121), Close, then a full ascending read block by block
+ * (RowIter.Next -> ReadBlockWithStat, segment_row_iter.go:63-95) with its
+ * per-row copies.  `threads` independent round trips run concurrently. */
+typedef struct {
+  const uint8_t *ka, *va;
+  const uint64_t *ko, *vo;
+  const uint16_t *kl;
+  const uint32_t *vl;
+  uint64_t n, T, D;
+  uint64_t rows, bytes;
+  int rc;
+} rt_job;
+
+static void *rt_run(void *arg) {
+  rt_job *j = (rt_job *)arg;
+  enc_job e = {j->ka, j->va, j->ko, j->vo, j->kl, j->vl, 0, j->n, j->T, j->D, 0, 0, 0};
+  oref_writer *w = oref_writer_new(j->T, j->D, 0, 0);
+  j->rc = 0;
+  for (uint64_t i = 0; i < j->n && !j->rc; i++) {
+    const size_t k = e.kl[i], v = e.vl[i];
+    uint8_t *row = (uint8_t *)malloc(6 + k + v);
+    memcpy(row + 6, e.ka + e.ko[i], k);
+    memcpy(row + 6 + k, e.va + e.vo[i], v);
+    j->rc = oref_writer_write_row(w, row + 6, k, row + 6 + k, v);
+    free(row);
+  }
+  const uint8_t *file = NULL;
+  uint64_t flen = 0;
+  if (!j->rc) j->rc = oref_writer_close(w, &file, &flen, NULL, NULL);
+  j->rows = 0;
+  j->bytes = flen;
+  for (uint64_t b = 0; b < w->nidx && !j->rc; b++) {
+    const oref_stat *st = &w->idx[b];
+    oref_block_desc d = {st->offset, st->block_size, st->original_size, st->compressed_size};
+    oref_rows r = {0, 0, 0};
+    if (oref_read_block(file, flen, &d, 0, &r) == OREF_BLK_OK) j->rows += r.n;
+    oref_rows_free(&r);
+  }
+  oref_writer_free(w);
+  return NULL;
+}
+
+uint64_t oref_roundtrip_go(const uint8_t *key_arena, const uint64_t *key_off,
+                           const uint16_t *key_len, const uint8_t *val_arena,
+                           const uint64_t *val_off, const uint32_t *val_len, uint64_t n,
+                           uint64_t threshold, uint64_t block_size, int threads,
+                           uint64_t *file_bytes) {
+  if (threads < 1) threads = 1;
+  rt_job *jobs = (rt_job *)calloc((size_t)threads, sizeof(rt_job));
+  pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (rt_job){key_arena, val_arena, key_off, val_off, key_len, val_len, n, threshold,
+                       block_size, 0, 0, 0};
+    if (threads > 1)
+      pthread_create(&th[t], NULL, rt_run, &jobs[t]);
+    else
+      rt_run(&jobs[t]);
+  }
+  uint64_t rows = 0, bytes = 0;
+  for (int t = 0; t < threads; t++) {
+    if (threads > 1) pthread_join(th[t], NULL);
+    rows += jobs[t].rc ? 0 : jobs[t].rows;
+    bytes += jobs[t].bytes;
+  }
+  free(jobs);
+  free(th);
+  if (file_bytes) *file_bytes = bytes;
+  return rows;
+}
+
+/* CM: one compaction step -- every block of K input segments decoded with
+ * ReadBlockWithStat's semantics (per-row copies), a k-way merge ascending in
+ * which the first (newest) segment holding a key owns it (the L0 rule of
+ * snapshot_reader.GetRange, snapshot_reader.go:294-331), and the merged rows
+ * written with the Go writer (WriteRow + Close).  `threads` independent
+ * compactions of the same inputs run concurrently.  Returns the merged rows
+ * of one compaction (0 on error); *in_bytes = sum of input BlockSize. */
+typedef struct {
+  int k;
+  const uint8_t *const *segs;
+  const uint64_t *lens;
+  const oref_block_desc *const *descs;
+  const uint64_t *nblks;
+  uint64_t T, D;
+  uint64_t rows_out, bytes_out;
+  int rc;
+} cm_job;
+
+static int kv_less(const oref_kv *a, const oref_kv *b) {
+  const uint64_t n = a->key_len < b->key_len ? a->key_len : b->key_len;
+  const int c = n ? memcmp(a->key, b->key, n) : 0;
+  return c < 0 || (c == 0 && a->key_len < b->key_len);
+}
+static int kv_equal(const oref_kv *a, const oref_kv *b) {
+  return a->key_len == b->key_len && (!a->key_len || !memcmp(a->key, b->key, a->key_len));
+}
+
+static void *cm_run(void *arg) {
+  cm_job *j = (cm_job *)arg;
+  oref_rows *all = (oref_rows *)calloc((size_t)j->k, sizeof(oref_rows));
+  j->rc = 0;
+  for (int s = 0; s < j->k && !j->rc; s++) { /* decode: ReadBlockWithStat per block */
+    for (uint64_t b = 0; b < j->nblks[s] && !j->rc; b++) {
+      oref_rows r = {0, 0, 0};
+      if (oref_read_block(j->segs[s], j->lens[s], &j->descs[s][b], 0, &r) != OREF_BLK_OK) {
+        j->rc = -1;
+      } else {
+        for (uint64_t i = 0; i < r.n; i++) { /* append (the RowIter's rows) */
+          if (all[s].n == all[s].cap) {
+            all[s].cap = all[s].cap ? 2 * all[s].cap : 1024;
+            all[s].rows = (oref_kv *)realloc(all[s].rows, all[s].cap * sizeof(oref_kv));
+          }
+          all[s].rows[all[s].n++] = r.rows[i];
+        }
+        free(r.rows); /* the row copies now belong to all[s] */
+      }
+    }
+  }
+  oref_writer *w = oref_writer_new(j->T, j->D, 0, 0);
+  uint64_t *pos = (uint64_t *)calloc((size_t)j->k, sizeof(uint64_t));
+  j->rows_out = 0;
+  while (!j->rc) { /* k-way merge: smallest key; ties -> lowest (newest) segment */
+    int best = -1;
+    for (int s = 0; s < j->k; s++)
+      if (pos[s] < all[s].n && (best < 0 || kv_less(&all[s].rows[pos[s]], &all[best].rows[pos[best]])))
+        best = s;
+    if (best < 0) break;
+    const oref_kv *kv = &all[best].rows[pos[best]];
+    for (int s = 0; s < j->k; s++) /* shadowed versions of the same key */
+      if (s != best && pos[s] < all[s].n && kv_equal(&all[s].rows[pos[s]], kv)) pos[s]++;
+    j->rc = oref_writer_write_row(w, kv->key, kv->key_len, kv->val, kv->val_len);
+    pos[best]++;
+    j->rows_out++;
+  }
+  uint64_t flen = 0;
+  if (!j->rc) j->rc = oref_writer_close(w, NULL, &flen, NULL, NULL);
+  j->bytes_out = flen;
+  oref_writer_free(w);
+  for (int s = 0; s < j->k; s++) oref_rows_free(&all[s]);
+  free(all);
+  free(pos);
+  return NULL;
+}
+
+uint64_t oref_compact_go(int k, const uint8_t *const *segs, const uint64_t *seg_lens,
+                         const oref_block_desc *const *descs, const uint64_t *nblks,
+                         uint64_t threshold, uint64_t block_size, int threads,
+                         uint64_t *out_bytes) {
+  if (threads < 1) threads = 1;
+  cm_job *jobs = (cm_job *)calloc((size_t)threads, sizeof(cm_job));
+  pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (cm_job){k, segs, seg_lens, descs, nblks, threshold, block_size, 0, 0, 0};
+    if (threads > 1)
+      pthread_create(&th[t], NULL, cm_run, &jobs[t]);
+    else
+      cm_run(&jobs[t]);
+  }
+  uint64_t rows = 0, bytes = 0;
+  int rc = 0;
+  for (int t = 0; t < threads; t++) {
+    if (threads > 1) pthread_join(th[t], NULL);
+    if (jobs[t].rc) rc = jobs[t].rc;
+    rows = jobs[t].rows_out;
+    bytes += jobs[t].bytes_out;
+  }
+  free(jobs);
+  free(th);
+  if (out_bytes) *out_bytes = bytes;
+  return rc ? 0 : rows;
+}
+
+/* ======================================================================= */
 /* SoA restatement of the product output layout                 */
 /* ======================================================================= */
 typedef struct {

@@ -144,6 +144,23 @@ oref_writer *oref_encode_soa(const uint8_t *key_arena, const uint64_t *key_off,
                              const uint64_t *val_off, const uint32_t *val_len, uint64_t n,
                              uint64_t threshold, uint64_t block_size, int *rc);
 
+/* CPU baselines of bench.py configs (Go semantics; `threads` independent
+ * copies of the job run concurrently):
+ * C1 -- WriteRow x n + Close + a full ascending read with ReadBlockWithStat's
+ * per-row copies; returns rows read (all threads), *file_bytes summed. */
+uint64_t oref_roundtrip_go(const uint8_t *key_arena, const uint64_t *key_off,
+                           const uint16_t *key_len, const uint8_t *val_arena,
+                           const uint64_t *val_off, const uint32_t *val_len, uint64_t n,
+                           uint64_t threshold, uint64_t block_size, int threads,
+                           uint64_t *file_bytes);
+/* CM -- decode every block of k segments (newest first), merge ascending with
+ * the newest segment owning a key, write the merge with the Go writer;
+ * returns the merged rows of one compaction (0 on error). */
+uint64_t oref_compact_go(int k, const uint8_t *const *segs, const uint64_t *seg_lens,
+                         const oref_block_desc *const *descs, const uint64_t *nblks,
+                         uint64_t threshold, uint64_t block_size, int threads,
+                         uint64_t *out_bytes);
+
 /* ---- SoA restatement of the product's output layout -------------------- */
 /* Pass 1: per-block (status, rows, key bytes, value bytes). */
 void oref_block_counts(const uint8_t *seg, uint64_t seg_len, const oref_block_desc *d,

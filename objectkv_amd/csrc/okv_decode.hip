@@ -378,8 +378,11 @@ __device__ __forceinline__ void gather_tiles(const Src& src, const GatherSmem& s
   }
 }
 
-// Tiles of a region split over nw waves in contiguous ranges (measured:
-// interleaving the tiles over the waves, 2 or 8 tiles per iteration are slower).
+// Tiles of a region split over nw waves in contiguous ranges.  Measured (C3,
+// DESIGN.md §4): interleaving the tiles over the waves, 2 or 8 tiles per
+// iteration, prefetching a spilling chunk's next-row window with the first
+// (+11 VGPRs: 4 waves/SIMD instead of 5) and forcing 6-8 waves/SIMD (spills)
+// are all slower.
 template <bool kVal, class Src>
 __device__ __forceinline__ void gather_region(const Src& src, const GatherSmem& sm, int rows,
                                               uint8_t* __restrict__ arena, uint64_t dbase,

@@ -2,23 +2,31 @@
 //
 // Replaces the record loop of sst.SegmentReader.ReadBlockWithStat
 // (/root/reference/sst/segment_reader.go:295-355) for many blocks at once.
-// Launches per call (DESIGN.md "Kernels"):
+// Launches per call:
 //   1. okv_count_kernel  -- one lane per block walks the record headers in
 //      HBM, validating exactly what the Go loop validates; per block it emits
 //      (status, rows, key bytes, value bytes, end position), the positions of
-//      its first kRCap records, and a 256-block exclusive scan.  Blocks with
-//      more rows go on the "big block" list.
-//   2. okv_scan_kernel   -- one workgroup scans the tile totals.
+//      its first kRCap records (rec_index layout: 64-byte segments of 16
+//      records, filled by a wave's lockstep stores) and a 256-block exclusive
+//      scan.  Blocks with more rows go on the "big block" list.  Segments of
+//      <= 64 MiB with small blocks first touch every line of their blocks
+//      (prefetch), so the dependent chase hits the caches.  A one-tile launch
+//      (<= 256 blocks) zeroes the big-block counter and writes the totals
+//      itself: no memset, no scan launch.
+//   2. okv_scan_kernel   -- one workgroup scans the tile totals (> 256 blocks).
 //   3. okv_gather_kernel -- one workgroup per block: one wave rebuilds the row
-//      table in parallel (recorded positions + header reads + wave scan),
+//      table in parallel (recorded positions + header reads + wave scans),
 //      writes the SoA row index, then every lane gathers 16-byte destination
 //      chunks of the packed key/value arenas straight from HBM (two aligned
-//      16-byte loads + byte funnel) and stores them whole (dwordx4).  Chunks
-//      spanning a row boundary are assembled lane-per-row.  Tiny LDS, so
-//      occupancy is set by registers, not by block size.
+//      16-byte loads + byte funnel) and stores them whole (dwordx4); chunks
+//      spanning a row boundary are completed in registers.  Tiny LDS, so
+//      occupancy is set by registers (5 waves/SIMD).  256 threads for large
+//      blocks, 64 (one wave per block) when blocks average <= 16 KiB.
 //   4. okv_copy_kernel   -- persistent, over the big-block list only: stages
 //      the block in LDS and chases its headers there (rare: > kRCap rows).
 // OKV_F_INDEX_ONLY writes spans into seg instead of arenas (3 + okv_index_kernel).
+// Measured alternatives to pass 3 (LDS-DMA staging, pipelined loader/gatherer,
+// persistent streaming, tile-major, ...) are in DESIGN.md §4; all slower.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

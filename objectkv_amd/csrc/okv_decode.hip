@@ -340,6 +340,7 @@ __device__ __forceinline__ void gather_tiles(const Src& src, const GatherSmem& s
   const uint32_t last = uint32_t(rows) - 1;
   uint32_t r = 0;
   bool searched = false;
+  const uint32_t cmax = (N < t1 * 64 ? N : t1 * 64) - 1;  // last chunk of the range (ts == 1)
   for (uint32_t t = t0; t < t1; t += kU * ts) {
     uint4 v[kU];
     uint32_t rr[kU];
@@ -348,7 +349,11 @@ __device__ __forceinline__ void gather_tiles(const Src& src, const GatherSmem& s
     for (uint32_t u = 0; u < kU; ++u) {
       const uint32_t c = (t + u * ts) * 64 + lane;
       const bool ok = (t + u * ts) < t1 && c < N;
-      const uint32_t x = (ok ? c : (t0 * 64 + lane < N ? t0 * 64 + lane : 0)) << 4;
+      // lanes past the range reload the range's last chunk (an address a
+      // valid lane loads in this iteration; x stays monotone for the linear
+      // advance).  Pointing them at the range's first tile with the current
+      // row's bias re-fetched ~40 evicted lines per block (0.32 GB at C3).
+      const uint32_t x = (ok ? c : cmax) << 4;
       if (!searched) {  // binary search: r = #{k in [1, rows] : pre[k] <= x}
         uint32_t pos = 0;
 #pragma unroll

@@ -56,6 +56,7 @@ struct okv_ctx {
   // per-pass event timing (okv_profile)
   uint32_t gather_grid = 0;  // 0: default grid; else workgroups (OKV_GATHER_GRID)
   uint32_t gather_threads = 0;  // 0: by average block size; else 64 or 256 (OKV_GATHER_THREADS)
+  bool gather_staged = true;    // 256-thread pass 3 stages value spans in LDS (OKV_GATHER_STAGED=0: off)
   bool prof = false;
   std::vector<hipEvent_t> ev;  // 5 per timed call
   size_t ev_used = 0;

@@ -506,6 +506,156 @@ __global__ __launch_bounds__(NT) void okv_gather_kernel(CopyParams P) {
 }
 
 // ---------------------------------------------------------------------------
+// Pass 3, wave-staged form (experimental, OKV_GATHER_STAGED=1): the value
+// region's tiles are produced from a per-wave LDS image of the iteration's
+// source span, filled by LDS-DMA (global_load_lds_dwordx4, no VGPR landing):
+// the loads in flight no longer cost registers, and a chunk's spill windows
+// come from the same image (no second trip).  Keys keep the global windows.
+// ---------------------------------------------------------------------------
+#define OKV_LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+constexpr uint32_t kStU = 5;                        // value tiles (1 KiB) per iteration
+template <uint32_t U> struct StCfg { static constexpr uint32_t cap = U * 1024 + 1024; };
+
+// Row holding region byte x (wave-uniform search over the LDS prefix).
+__device__ __forceinline__ uint32_t row_of(const uint32_t* pre, uint32_t last, uint32_t x) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t st = 32; st; st >>= 1) {
+    const uint32_t j = pos + st;
+    if (j <= last && pre[j] <= x) pos = j;
+  }
+  return pos;
+}
+
+// Tile t of a value region through global windows, for the rare tile whose
+// source span does not fit the stage (kept out of line: its registers would
+// otherwise size the whole kernel).
+__device__ __attribute__((noinline)) void gather_value_tile_global(const uint8_t* seg,
+                                                                   uint64_t seg_bytes,
+                                                                   uint64_t off,
+                                                                   const GatherSmem* sm, int rows,
+                                                                   uint8_t* arena, uint64_t dbase,
+                                                                   uint32_t t) {
+  const GlobalWin src{seg, seg_bytes, off};
+  gather_tiles<true, GlobalWin, 1>(src, *sm, rows, arena, dbase, t, t + 1, 1);
+}
+
+template <uint32_t U = kStU>
+__device__ __forceinline__ bool stage_span(const uint32_t* pre, const uint32_t* sb, uint32_t last,
+                                           int64_t off, uint32_t cbeg, uint32_t cend,
+                                           int64_t& A, int64_t& E, uint32_t& np) {
+  const uint32_t rb = row_of(pre, last, cbeg * 16), re = row_of(pre, last, cend * 16 - 1);
+  const int64_t s0 = off + int64_t(sb[rb]) + int64_t(cbeg) * 16;
+  const int64_t s1 = off + int64_t(sb[re]) + int64_t(cend) * 16;
+  A = (s0 & ~int64_t(15)) - 16;
+  E = ((s1 + 15) & ~int64_t(15)) + 16;
+  np = uint32_t((E - A + 1023) >> 10);
+  return A >= 0 && E - A <= int64_t(StCfg<U>::cap);
+}
+
+template <uint32_t kStU>
+__device__ __forceinline__ void gather_values_staged(const GlobalWin& src, const GatherSmem& sm,
+                                                     int rows, uint8_t* __restrict__ arena,
+                                                     uint64_t dbase, uint32_t t0, uint32_t t1,
+                                                     uint4* stage) {
+  const uint32_t* pre = sm.vpre;
+  const uint32_t* sb = sm.vsb;
+  const uint32_t N = (pre[rows] + 15) >> 4;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t last = uint32_t(rows) - 1;
+  const uint32_t climit = N < t1 * 64 ? N : t1 * 64;  // one past the wave's last chunk
+  const int64_t off = int64_t(src.off);
+  const uint64_t lim = round16(src.seg_bytes);
+  uint32_t r = 0;
+  bool searched = false;
+  for (uint32_t t = t0; t * 64 < climit;) {
+    // kStU tiles per iteration; a span too wide for the stage retries one
+    // tile, and a single tile too wide goes through global windows
+    uint32_t n = min(kStU, t1 - t);
+    uint32_t cbeg = t * 64, cend = min(climit, (t + n) * 64);
+    int64_t A, E;
+    uint32_t np;
+    bool ok = stage_span<kStU>(pre, sb, last, off, cbeg, cend, A, E, np);
+    if (!ok && n > 1) {
+      n = 1;
+      cend = min(climit, (t + 1) * 64);
+      ok = stage_span<kStU>(pre, sb, last, off, cbeg, cend, A, E, np);
+    }
+    if (!ok) {
+      gather_value_tile_global(src.seg, src.seg_bytes, src.off, &sm, rows, arena, dbase, t);
+      searched = false;
+      t += 1;
+      continue;
+    }
+    const uint64_t Eu = uint64_t(E) < lim ? uint64_t(E) : lim;
+    for (uint32_t p = 0; p < np; ++p) {
+      uint64_t a = uint64_t(A) + (uint64_t(p) << 10) + (lane << 4);
+      if (a + 16 > Eu) a = uint64_t(A);  // past the span or the segment: bytes never used
+      __builtin_amdgcn_global_load_lds(src.seg + a, OKV_LDS_PTR(stage + p * 64), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (uint32_t u = 0; u < kStU; ++u) {
+      if (u >= n) break;
+      const uint32_t c = cbeg + u * 64 + lane;
+      const bool okc = c < cend;
+      const uint32_t x = (okc ? c : cend - 1) << 4, xe = x + 16;
+      if (!searched) {
+        r = row_of(pre, last, x);
+        searched = true;
+      } else {
+        while (r < last && pre[r + 1] <= x) ++r;
+      }
+      uint4 out = load16_lds_b128(stage, uint32_t(off + int64_t(sb[r]) + int64_t(x) - A));
+      if (okc) {
+        if (xe > pre[r + 1]) {
+          out = merge_bytes(make_uint4(0, 0, 0, 0), out, 0, int32_t(pre[r + 1] - x));
+          for (uint32_t j = r + 1; j <= last && pre[j] < xe; ++j) {
+            const uint32_t q0 = pre[j], q1 = pre[j + 1];
+            if (q1 == q0) continue;
+            const uint4 w =
+                load16_lds_b128(stage, uint32_t(off + int64_t(sb[j]) + int64_t(x) - A));
+            out = merge_bytes(out, w, int32_t(q0 - x), int32_t((q1 < xe ? q1 : xe) - x));
+          }
+        }
+        *reinterpret_cast<uint4*>(arena + dbase + uint64_t(x)) = out;
+      }
+    }
+    t += n;
+  }
+}
+
+template <int NT, uint32_t U = kStU>
+__global__ __launch_bounds__(NT) void okv_gather_staged_kernel(CopyParams P) {
+  __shared__ GatherSmem sm;
+  __shared__ uint4 stage[NT / 64][StCfg<U>::cap / 16 + 2];
+  for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
+    const BlockMeta m = block_meta(P, b);
+    if (block_head(P, b, m)) {
+      const int rows = int(m.c.rows);
+      const GlobalWin src{P.seg, P.seg_bytes, m.off};
+      if (threadIdx.x < 64) {
+        const uint32_t t = threadIdx.x;
+        const uint32_t rec = int(t) < rows ? P.rec_s[rec_index(P.nblk, b, t)] : 0u;
+        build_row_table(src, sm, rows, rec);
+      }
+      __syncthreads();
+      write_row_index(P, sm, m, rows);
+      const uint32_t wave = threadIdx.x >> 6;
+      const uint32_t Tk = (sm.kpre[rows] + 1023) >> 10;
+      gather_tiles<false, GlobalWin, 2>(src, sm, rows, P.key_arena, m.B.kb0,
+                                        uint32_t(uint64_t(Tk) * wave / (NT / 64)),
+                                        uint32_t(uint64_t(Tk) * (wave + 1) / (NT / 64)), 1);
+      const uint32_t T = (sm.vpre[rows] + 1023) >> 10;
+      gather_values_staged<U>(src, sm, rows, P.val_arena, m.B.vb0,
+                           uint32_t(uint64_t(T) * wave / (NT / 64)),
+                           uint32_t(uint64_t(T) * (wave + 1) / (NT / 64)), stage[wave]);
+    }
+    if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Pass 4 (big blocks only): LDS-staged decode with a serial header chase.
 // ---------------------------------------------------------------------------
 struct SlowRows {               // general path: 64-bit positions, batched rows
@@ -1042,7 +1192,9 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   P.val_cap = index_only ? 0 : o->val_cap;
   if (nblk) {
     const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
-    if (gather_threads(ctx, w, nblk) == 64)
+    if (gather_threads(ctx, w, nblk) == 256 && ctx->gather_staged && !index_only)
+      hipLaunchKernelGGL((okv_gather_staged_kernel<kThreads>), g, dim3(kThreads), 0, ctx->stream, P);
+    else if (gather_threads(ctx, w, nblk) == 64)
       hipLaunchKernelGGL(okv_gather_kernel<64>, g, dim3(64), 0, ctx->stream, P);
     else
       hipLaunchKernelGGL(okv_gather_kernel<kThreads>, g, dim3(kThreads), 0, ctx->stream, P);
@@ -1178,6 +1330,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
     }
   }
   if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
+  if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
   if (stream) {
     ctx->stream = static_cast<hipStream_t>(stream);
   } else {

@@ -251,22 +251,68 @@ def _mixed_segment(kinds, seed):
 
 @pytest.fixture(scope="module")
 def decoders_by_width():
-    """One decoder per pass-3 workgroup width (OKV_GATHER_THREADS), so both
-    gather forms run on the same inputs whatever the average block size."""
+    """One decoder per pass-3 form, so every gather runs on the same inputs
+    whatever the average block size: OKV_GATHER_THREADS=64 (one wave per
+    block), 256 (LDS-staged value spans, the default for large blocks) and
+    256 with OKV_GATHER_STAGED=0 (global windows)."""
     import os
     decs = {}
     try:
-        for w in ("64", "256"):
-            os.environ["OKV_GATHER_THREADS"] = w
+        for w in ("64", "256", "256g"):
+            os.environ["OKV_GATHER_THREADS"] = w.rstrip("g")
+            os.environ["OKV_GATHER_STAGED"] = "0" if w.endswith("g") else "1"
             decs[w] = okv.Decoder(0)
     finally:
         os.environ.pop("OKV_GATHER_THREADS", None)
+        os.environ.pop("OKV_GATHER_STAGED", None)
     yield decs
     for d in decs.values():
         d.close()
 
 
-@pytest.mark.parametrize("width", ["64", "256"])
+def _wide_segment(seed, nblk=120):
+    """Large blocks whose value tiles span far more source than values:
+    'W' up to 64 rows of 200-256 B keys and 0-40 B values (a 1 KiB value tile
+    spans > 6 KiB of records: global-window fallback), 'V' 200 B keys with
+    300-600 B values (a 5-tile span overflows the stage: one-tile retry),
+    'L' 1-3 KiB values.  The first block sits at offset 0 (the stage's
+    16-byte lead-in would start before the segment), the others at odd
+    offsets, and the last block ends at the segment's last byte."""
+    rng = np.random.default_rng(seed)
+    seg, descs = bytearray(), []
+    for b in range(nblk):
+        kind = rng.choice(["W", "V", "L"])
+        if kind == "W":
+            shape = [(int(rng.integers(200, 257)), int(rng.integers(0, 41)))
+                     for _ in range(int(rng.integers(40, 65)))]
+        elif kind == "V":
+            shape = [(200, int(rng.integers(300, 601))) for _ in range(int(rng.integers(30, 64)))]
+        else:
+            shape = [(int(rng.integers(8, 257)), int(rng.integers(1000, 3000)))
+                     for _ in range(int(rng.integers(5, 28)))]
+        body = bytearray()
+        for kl, vl in shape:
+            body += kl.to_bytes(2, "little") + vl.to_bytes(4, "little")
+            body += rng.integers(0, 256, kl + vl, dtype=np.uint8).tobytes()
+        pad = 0 if b == nblk - 1 else int(rng.choice([0, 1, 3, 8, 13, 4096]))
+        off = 0 if b == 0 else len(seg) + int(rng.choice([0, 1, 5, 11]))
+        seg += bytes(off - len(seg))
+        seg += body + bytes(pad)
+        descs.append((off, len(body) + pad, len(body), 0))
+    return bytes(seg), np.array(descs, np.uint64).reshape(-1, 4)
+
+
+@pytest.mark.parametrize("width", ["256", "256g", "64"])
+def test_wide_spans_all_gathers(decoders_by_width, width):
+    """Stage overflow (one-tile retry and global fallback), the segment's
+    first and last bytes, odd block offsets: every gather vs the oracle."""
+    for seed in (1, 2):
+        seg, d = _wide_segment(seed)
+        got = decoders_by_width[width].decode(seg, d)
+        _assert_same_as_oracle(got, seg, d, 0, False)
+
+
+@pytest.mark.parametrize("width", ["64", "256", "256g"])
 def test_mixed_blocks_both_gather_widths(decoders_by_width, width):
     """A segment mixing 4 KiB blocks, 64 KiB blocks with few rows and blocks
     over kRCap rows, through the 64- and the 256-thread gather."""

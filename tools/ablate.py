@@ -2,7 +2,7 @@
 (cdna_hip_programming.md §5.4 rule 24), with a bit-equality check of every
 output array between the arms.
 
-usage: python tools/ablate.py [arm ...]     arm = <threads>[:<grid>]
+usage: python tools/ablate.py [arm ...]     arm = <threads>[:<grid>[:<staged>]]  (staged = OKV_GATHER_STAGED: 0 = global-window pass 3)
   threads = 64 | 256 | auto (OKV_GATHER_THREADS), grid = OKV_GATHER_GRID (0: one per block)
 env:   ABL_NBLK (65536), ABL_ROUNDS (5), ABL_KIND (1 = Zipf C3, 0 = fixed C2),
        ABL_BS (65536), ABL_TH (57344)
@@ -30,8 +30,13 @@ dev = torch.device("cuda", 0)
 stream = torch.cuda.current_stream(dev).cuda_stream
 decs = {}
 for a in arms:
-    thr, _, grid = a.partition(":")
+    thr, _, rest = a.partition(":")
+    grid, _, staged = rest.partition(":")
     os.environ["OKV_GATHER_GRID"] = grid or "0"
+    if staged:
+        os.environ["OKV_GATHER_STAGED"] = staged
+    else:
+        os.environ.pop("OKV_GATHER_STAGED", None)
     if thr in ("64", "256"):
         os.environ["OKV_GATHER_THREADS"] = thr
     else:

@@ -655,6 +655,70 @@ __global__ __launch_bounds__(NT) void okv_gather_staged_kernel(CopyParams P) {
   }
 }
 
+// Pass 3, small-block staged form (blocks averaging <= 16 KiB, e.g. 4 KiB
+// blocks): one wave per block DMAs the whole block into its LDS stage right
+// after the metadata arrives, then reads the record headers and assembles
+// every key and value chunk from the stage: two dependent HBM trips per block
+// (metadata + record positions, then the block) instead of four (metadata,
+// positions, headers, key tiles, value tiles).  Blocks that do not fit the
+// stage take the global-window gather (same workgroup, same row table code).
+constexpr uint32_t kSmallStage = 5 * 1024;  // staged bytes per block (DMA pieces of 1 KiB)
+
+// Byte source: a block's LDS stage; block byte x at stage byte bias + x.
+struct StageWin {
+  const uint4* s4;
+  uint32_t bias;
+  __device__ __forceinline__ uint4 at(int64_t rel) const {
+    return load16_lds_b128(s4, uint32_t(int64_t(bias) + rel));
+  }
+  __device__ __forceinline__ void header(uint32_t pos, uint32_t& kl, uint32_t& vl) const {
+    header_lds(reinterpret_cast<const uint32_t*>(s4), bias + pos, kl, vl);
+  }
+};
+
+__global__ __launch_bounds__(64) void okv_gather_small_kernel(CopyParams P) {
+  __shared__ GatherSmem sm;
+  __shared__ uint4 stage[kSmallStage / 16 + 4];
+  const uint32_t lane = threadIdx.x;
+  for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
+    // record positions ride with the metadata (slots exist for every r < kRCap)
+    const uint32_t rec0 = P.rec_s[rec_index(P.nblk, b, lane)];
+    const BlockMeta m = block_meta(P, b);
+    if (block_head(P, b, m)) {
+      const int rows = int(m.c.rows);
+      const uint32_t rec = int(lane) < rows ? rec0 : 0u;
+      const uint32_t shift = uint32_t(m.off & 15);
+      // stage byte 0 = block byte -(16 + shift): a 16-byte lead-in for
+      // windows that begin before a row, and 32 bytes of slack at the end
+      const uint32_t need = 16 + shift + uint32_t(m.c.pend) + 32;
+      if (need <= kSmallStage && !P.index_only) {
+        const int64_t D = int64_t(m.off) - int64_t(shift) - 16;
+        const int64_t lim = int64_t(round16(P.seg_bytes));
+        const uint32_t np = (need + 1023) >> 10;
+        for (uint32_t p = 0; p < np; ++p) {
+          int64_t a = D + (int64_t(p) << 10) + int64_t(lane << 4);
+          if (a < 0 || a + 16 > lim) a = int64_t(m.off) & ~int64_t(15);  // bytes never used
+          __builtin_amdgcn_global_load_lds(P.seg + a, OKV_LDS_PTR(stage + p * 64), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const StageWin src{stage, 16 + shift};
+        build_row_table(src, sm, rows, rec);
+        write_row_index(P, sm, m, rows);
+        gather_region<false>(src, sm, rows, P.key_arena, m.B.kb0, 0, 1);
+        gather_region<true>(src, sm, rows, P.val_arena, m.B.vb0, 0, 1);
+      } else {
+        const GlobalWin src{P.seg, P.seg_bytes, m.off};
+        build_row_table(src, sm, rows, rec);
+        write_row_index(P, sm, m, rows);
+        if (!P.index_only) {
+          gather_region<false>(src, sm, rows, P.key_arena, m.B.kb0, 0, 1);
+          gather_region<true>(src, sm, rows, P.val_arena, m.B.vb0, 0, 1);
+        }
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Pass 4 (big blocks only): LDS-staged decode with a serial header chase.
 // ---------------------------------------------------------------------------
@@ -1194,6 +1258,8 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
     const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
     if (gather_threads(ctx, w, nblk) == 256 && ctx->gather_staged && !index_only)
       hipLaunchKernelGGL((okv_gather_staged_kernel<kThreads>), g, dim3(kThreads), 0, ctx->stream, P);
+    else if (gather_threads(ctx, w, nblk) == 64 && ctx->gather_staged)
+      hipLaunchKernelGGL(okv_gather_small_kernel, g, dim3(64), 0, ctx->stream, P);
     else if (gather_threads(ctx, w, nblk) == 64)
       hipLaunchKernelGGL(okv_gather_kernel<64>, g, dim3(64), 0, ctx->stream, P);
     else

@@ -253,12 +253,13 @@ def _mixed_segment(kinds, seed):
 def decoders_by_width():
     """One decoder per pass-3 form, so every gather runs on the same inputs
     whatever the average block size: OKV_GATHER_THREADS=64 (one wave per
-    block), 256 (LDS-staged value spans, the default for large blocks) and
-    256 with OKV_GATHER_STAGED=0 (global windows)."""
+    block, whole block staged in LDS), 256 (LDS-staged value spans, the
+    default for large blocks), and both with OKV_GATHER_STAGED=0 (global
+    windows): 64g, 256g."""
     import os
     decs = {}
     try:
-        for w in ("64", "256", "256g"):
+        for w in ("64", "64g", "256", "256g"):
             os.environ["OKV_GATHER_THREADS"] = w.rstrip("g")
             os.environ["OKV_GATHER_STAGED"] = "0" if w.endswith("g") else "1"
             decs[w] = okv.Decoder(0)
@@ -302,7 +303,7 @@ def _wide_segment(seed, nblk=120):
     return bytes(seg), np.array(descs, np.uint64).reshape(-1, 4)
 
 
-@pytest.mark.parametrize("width", ["256", "256g", "64"])
+@pytest.mark.parametrize("width", ["256", "256g", "64", "64g"])
 def test_wide_spans_all_gathers(decoders_by_width, width):
     """Stage overflow (one-tile retry and global fallback), the segment's
     first and last bytes, odd block offsets: every gather vs the oracle."""
@@ -312,7 +313,7 @@ def test_wide_spans_all_gathers(decoders_by_width, width):
         _assert_same_as_oracle(got, seg, d, 0, False)
 
 
-@pytest.mark.parametrize("width", ["64", "256", "256g"])
+@pytest.mark.parametrize("width", ["64", "64g", "256", "256g"])
 def test_mixed_blocks_both_gather_widths(decoders_by_width, width):
     """A segment mixing 4 KiB blocks, 64 KiB blocks with few rows and blocks
     over kRCap rows, through the 64- and the 256-thread gather."""

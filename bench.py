@@ -395,12 +395,15 @@ def run_decode(args, torch, okv, D):
         step()
     torch.cuda.synchronize(dev)
 
-    # ---- timed region ----------------------------------------------------------
-    dec.profile(True)
+    # ---- timed region (no instrumentation: per-pass events cost ~5 us each in
+    # the stream, 40 % of a C2 step) -----------------------------------------------
     t_max, per = D.timed(step, args.steps)
+    ms_per_step = 1e3 * t_max / args.steps
+    # per-pass kernel times from a second, event-instrumented run of the same steps
+    dec.profile(True)
+    D.timed(step, args.steps)
     kern_ms, calls = dec.profile_read()
     dec.profile(False)
-    ms_per_step = 1e3 * t_max / args.steps
 
     # ---- roofline for the dominant kernel ------------------------------------------
     ms = {k: v / max(calls, 1) for k, v in kern_ms.items()}
@@ -416,10 +419,15 @@ def run_decode(args, torch, okv, D):
         # read OriginalSize per block; write payload (padded arenas) + 22 B/row
         # SoA (u64 key_off, u16 key_len, u64 val_off, u32 val_len) + 28 B/block
         alg = orig_bytes + payload + rows * 22 + nblk * 28
-        roof_kernel, roof_ms = "okv_gather_kernel", ms["copy"]
+        roof_kernel = ("okv_decode_fused_kernel (passes 1-3) + okv_copy_kernel"
+                       if nblk <= 512 and in_bytes / max(nblk, 1) <= 16384 else
+                       "okv_gather_small_kernel + okv_copy_kernel"
+                       if in_bytes / max(nblk, 1) <= 16384 else
+                       "okv_gather_staged_kernel + okv_copy_kernel")
+        roof_ms = ms["copy"]
     achieved = alg / (roof_ms * 1e-3) / 1e9
     traffic, traffic_src = (None, None) if comp else pmc_traffic(args.config, args.mode,
-                                                                 "okv_gather_kernel")
+                                                                 roof_kernel.split()[0])
 
     # ---- CPU baseline (rank 0, N = 1 only) ---------------------------------------
     cpu = None
@@ -455,8 +463,8 @@ def run_decode(args, torch, okv, D):
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": roof_kernel,
                      "algorithmic_bytes_per_launch": int(alg),
-                     "timing": "HIP events around the kernel on its stream, averaged over the "
-                               "timed steps",
+                     "timing": "HIP events around the kernel on its stream, averaged over a "
+                               "second run of the same steps (the timed run carries no events)",
                      "traffic_source": traffic_src, "decode_source_sha": source_sha()},
         "cpu_baseline": cpu,
         "verify": ver,

@@ -42,6 +42,15 @@ struct okv_ctx {
   uint32_t* d_rec = nullptr;       // nblk x kRCap record positions (pass 1, rec_index)
   uint32_t* d_big = nullptr;       // big-block list + its counter (d_big[nblk])
   size_t cap_blocks = 0;
+  // single-pass small-block decode (okv_decode_fused_kernel)
+  bool fused = true;               // OKV_DECODE_FUSED=0: passes 1-3 as separate launches
+  uint32_t* f_flag = nullptr;      // [nblk] look-back flags, tagged with f_epoch
+  okv::Prefix* f_agg = nullptr;
+  okv::Prefix* f_incl = nullptr;
+  unsigned long long* f_ctr = nullptr;  // block-index counter, f_base at the next call
+  unsigned long long f_base = 0;
+  uint32_t f_epoch = 0;
+  size_t f_cap = 0;
   okv::Totals* d_tot = nullptr;
   okv::Totals* h_tot = nullptr;  // pinned
   // host-mode staging buffers (device side)

@@ -251,8 +251,8 @@ struct CopyParams {
   const Prefix* tile_pre;
   const uint32_t* rec_s;      // pass-1 record positions (u32, block-major) or headers
                               // (u64 klen << 32 | vlen): see okv_count_kernel
-  const uint32_t* big_list;   // blocks with > kRCap rows (or >= 4 GiB walks)
-  const uint32_t* big_count;
+  uint32_t* big_list;         // blocks with > kRCap rows (or >= 4 GiB walks)
+  uint32_t* big_count;
   uint64_t* row_start;
   uint64_t* key_base;
   uint64_t* val_base;
@@ -715,6 +715,216 @@ __global__ __launch_bounds__(64) void okv_gather_small_kernel(CopyParams P) {
           gather_region<true>(src, sm, rows, P.val_arena, m.B.vb0, 0, 1);
         }
       }
+    }
+  }
+}
+
+// Single-pass decode for small batches of small blocks (<= kFusedMaxBlocks
+// blocks averaging <= 16 KiB): passes 1-3 in ONE launch.  One wave per block
+// takes the next block index from a counter, DMAs the whole block into LDS,
+// walks its record headers there exactly as the Go loop does (lane 0;
+// statuses as in okv_count_kernel) and publishes the block's (rows, key
+// bytes, value bytes, bad); the block whose arrival is counted last scans all
+// of them and publishes every block's exclusive prefix (sc1 stores and loads,
+// flags tagged with the call's epoch so nothing is reset between calls);
+// every block then gathers its rows from its stage.  (A decoupled look-back
+// measured slower: its chain deepens with the blocks in flight.)  Blocks with more than kRCap rows, or too
+// large to stage, get their counts the same way (a global-memory walk) and go
+// to okv_copy_kernel through the big-block list, with cnt / lp / tile_pre
+// written as passes 1-2 would.
+constexpr uint32_t kFusedMaxBlocks = 512;  // every block of the grid resident at once
+struct FusedParams {
+  const int32_t* pre;     // zstd-stage statuses or null
+  BlockCount* cnt;        // what passes 1-2 write, for okv_copy_kernel
+  Prefix* lp;
+  Prefix* tile_pre;
+  uint32_t* flag;         // [nblk] (epoch << 2) | 1 aggregate, | 2 inclusive
+  Prefix* agg;            // [nblk]
+  Prefix* incl;           // [nblk]
+  unsigned long long* ctr;  // block-index counter (monotone across calls)
+  unsigned long long* arr;  // arrival counter (monotone across calls, same base)
+  unsigned long long base;  // its value at this call's start
+  uint32_t epoch;
+  Totals* tot;
+};
+
+// Hand-off without release/acquire fences (an agent-scope release writes back
+// the whole L2, an acquire invalidates it -- per block, that swamps the
+// kernel): payload and flag go through coherent (sc1) stores, the payload
+// drained before the flag, and the reader polls and reads with sc1 loads
+// (cdna_hip_programming.md G16, valid forms).
+__device__ __forceinline__ void publish(uint32_t* f, Prefix* slot, const Prefix& v, uint32_t tag) {
+  __hip_atomic_store(&slot->rows, v.rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&slot->kb, v.kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&slot->vb, v.vb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&slot->bad, v.bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(f, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t flag_peek(const uint32_t* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ Prefix prefix_peek(const Prefix* slot) {
+  Prefix v;
+  v.rows = __hip_atomic_load(&slot->rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  v.kb = __hip_atomic_load(&slot->kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  v.vb = __hip_atomic_load(&slot->vb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  v.bad = __hip_atomic_load(&slot->bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, FusedParams F) {
+  __shared__ GatherSmem sm;
+  __shared__ uint4 stage[kSmallStage / 16 + 4];
+  __shared__ uint32_t s_b;
+  const uint32_t lane = threadIdx.x;
+  if (lane == 0) s_b = uint32_t(atomicAdd(F.ctr, 1ull) - F.base);
+  __syncthreads();
+  const uint32_t b = s_b;
+  if (b >= P.nblk) return;
+  const uint32_t tag = F.epoch << 2;
+  // ---- pass 1 for this block (okv_count_kernel's rules) ----
+  const Desc d = P.descs[b];
+  const uint64_t len = (P.comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
+  const uint32_t shift = uint32_t(d.offset & 15);
+  int32_t st = OKV_BLK_OK;
+  {
+    const int32_t pre = F.pre ? F.pre[b] : int32_t(OKV_BLK_OK);
+    if (pre != OKV_BLK_OK) st = pre;  // outcome of the zstd stage
+    else if (int64_t(d.offset) < 0 || d.offset >= P.seg_bytes) st = OKV_BLK_EOF;  // :303-313
+    else if (P.seg_bytes - d.offset < d.block_size) st = OKV_BLK_SHORT;          // :314-316
+    else if (P.comp == OKV_COMP_ZSTD) st = OKV_BLK_UNSUPPORTED;
+  }
+  const uint32_t need = 16 + shift + uint32_t(len < kSmallStage ? len : kSmallStage) + 32;
+  const bool staged = st == OKV_BLK_OK && len + 16 + shift + 32 <= kSmallStage;
+  if (staged && len) {  // the whole block (BlockSize bytes) into the stage
+    const int64_t D = int64_t(d.offset) - int64_t(shift) - 16;
+    const int64_t lim = int64_t(round16(P.seg_bytes));
+    const uint32_t np = (need + 1023) >> 10;
+    for (uint32_t p = 0; p < np; ++p) {
+      int64_t a = D + (int64_t(p) << 10) + int64_t(lane << 4);
+      if (a < 0 || a + 16 > lim) a = int64_t(d.offset) & ~int64_t(15);  // bytes never used
+      __builtin_amdgcn_global_load_lds(P.seg + a, OKV_LDS_PTR(stage + p * 64), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  const StageWin lsrc{stage, 16 + shift};
+  uint64_t rows = 0, kb = 0, vb = 0, p = 0;
+  if (lane == 0 && st == OKV_BLK_OK) {
+    const uint64_t orig = d.original_size;
+    while (p < orig) {  // :340
+      if (len - p < 6) { st = OKV_BLK_PANIC; break; }  // :342-345
+      uint32_t kl, vl;
+      if (staged) lsrc.header(uint32_t(p), kl, vl);
+      else header_global(P.seg, d.offset + p, kl, vl);
+      const uint64_t room = len - p - 6;
+      if (kl > room || vl > room - kl) { st = OKV_BLK_PANIC; break; }  // :346-349
+      if (rows < kRCap) sm.rec[rows] = uint32_t(p);
+      rows++;
+      kb += kl;
+      vb += vl;
+      p += 6 + uint64_t(kl) + uint64_t(vl);
+    }
+    if (st != OKV_BLK_OK) rows = kb = vb = 0;
+  }
+  __syncthreads();  // the walk's record positions (sm.rec) are read by every lane below
+  st = __shfl(st, 0, 64);
+  rows = __shfl(rows, 0, 64);
+  kb = __shfl(kb, 0, 64);
+  vb = __shfl(vb, 0, 64);
+  p = __shfl(p, 0, 64);
+  // ---- pass 2: the last block to arrive scans every block's counts ----
+  // (every block of the grid is resident: the fused form runs for small
+  // batches only, kFusedMaxBlocks << the chip's resident capacity)
+  const Prefix mine{rows, round16(kb), round16(vb), uint64_t(st != OKV_BLK_OK)};
+  uint32_t last_arrival = 0;
+  if (lane == 0) {
+    publish(&F.flag[b], &F.agg[b], mine, tag | 1u);  // sc1 payload, drained, then the flag
+    last_arrival = uint32_t(atomicAdd(F.arr, 1ull) - F.base) == P.nblk - 1;
+  }
+  if (__shfl(last_arrival, 0, 64)) {
+    // exclusive scan over all blocks, 64 at a time (sc1 loads: the adds that
+    // came before ours each followed their block's drained sc1 stores)
+    Prefix carry{0, 0, 0, 0};
+    for (uint32_t c0 = 0; c0 < P.nblk; c0 += 64) {
+      const uint32_t k = c0 + lane;
+      const Prefix v = k < P.nblk ? prefix_peek(&F.agg[k]) : Prefix{0, 0, 0, 0};
+      const uint64_t ir = wave_incl_scan(v.rows, lane), ik = wave_incl_scan(v.kb, lane);
+      const uint64_t iv = wave_incl_scan(v.vb, lane), ib = wave_incl_scan(v.bad, lane);
+      if (k < P.nblk)
+        __hip_atomic_store(&F.incl[k].rows, carry.rows + ir - v.rows, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      const Prefix ex_k{carry.rows + ir - v.rows, carry.kb + ik - v.kb, carry.vb + iv - v.vb,
+                        carry.bad + ib - v.bad};
+      if (k < P.nblk) {
+        __hip_atomic_store(&F.incl[k].kb, ex_k.kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&F.incl[k].vb, ex_k.vb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&F.incl[k].bad, ex_k.bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      carry.rows += __shfl(ir, 63, 64);
+      carry.kb += __shfl(ik, 63, 64);
+      carry.vb += __shfl(iv, 63, 64);
+      carry.bad += __shfl(ib, 63, 64);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (uint32_t k = lane; k < P.nblk; k += 64)
+      __hip_atomic_store(&F.flag[k], tag | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+      *F.tot = Totals{carry.rows, carry.kb, carry.vb, carry.bad};
+      P.row_start[P.nblk] = carry.rows;
+    }
+  }
+  // every block: wait for its exclusive prefix (F.incl holds exclusive values)
+  if (lane == 0)
+    while (flag_peek(&F.flag[b]) != (tag | 2u)) __builtin_amdgcn_s_sleep(1);
+  Prefix ex{0, 0, 0, 0};
+  if (lane == 0) ex = prefix_peek(&F.incl[b]);
+  ex.rows = __shfl(ex.rows, 0, 64);
+  ex.kb = __shfl(ex.kb, 0, 64);
+  ex.vb = __shfl(ex.vb, 0, 64);
+  ex.bad = __shfl(ex.bad, 0, 64);
+  // ---- what passes 1-2 leave for okv_copy_kernel, and the totals ----
+  if (lane == 0) {
+    BlockCount c;
+    c.rows = rows;
+    c.kbytes = kb;
+    c.vbytes = vb;
+    c.pend = p;
+    c.status = st;
+    c.pad = 0;
+    F.cnt[b] = c;
+    F.lp[b] = ex;
+    if (b % kTile == 0) F.tile_pre[b / kTile] = Prefix{0, 0, 0, 0};
+    if (st == OKV_BLK_OK && (rows > kRCap || p >= (uint64_t(1) << 32)))
+      P.big_list[atomicAdd(P.big_count, 1u)] = b;
+  }
+  // ---- pass 3 ----
+  BlockMeta m;
+  m.c = BlockCount{rows, kb, vb, p, st, 0};
+  m.B = block_base_of(P, m.c, ex, Prefix{0, 0, 0, 0});
+  m.off = d.offset;
+  if (!block_head(P, b, m)) return;
+  const int nr = int(rows);
+  const uint32_t rec = int(lane) < nr ? sm.rec[lane] : 0u;
+  if (staged) {
+    build_row_table(lsrc, sm, nr, rec);
+    write_row_index(P, sm, m, nr);
+    if (!P.index_only) {
+      gather_region<false>(lsrc, sm, nr, P.key_arena, m.B.kb0, 0, 1);
+      gather_region<true>(lsrc, sm, nr, P.val_arena, m.B.vb0, 0, 1);
+    }
+  } else {
+    const GlobalWin gsrc{P.seg, P.seg_bytes, m.off};
+    build_row_table(gsrc, sm, nr, rec);
+    write_row_index(P, sm, m, nr);
+    if (!P.index_only) {
+      gather_region<false>(gsrc, sm, nr, P.key_arena, m.B.kb0, 0, 1);
+      gather_region<true>(gsrc, sm, nr, P.val_arena, m.B.vb0, 0, 1);
     }
   }
 }
@@ -1214,6 +1424,30 @@ int read_totals(okv_ctx* ctx, Totals* out) {
   return OKV_OK;
 }
 
+// Scratch of the single-pass small-block decode (flags zeroed once; the epoch
+// tag makes every call's flags fresh).
+int ensure_fused(okv_ctx* ctx, uint32_t nblk) {
+  const size_t n = std::max<size_t>(nblk, 1);
+  if (n <= ctx->f_cap && ctx->f_flag) return OKV_OK;
+  if (ctx->f_flag) {
+    OKV_HIP(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(ctx->f_flag);
+    (void)hipFree(ctx->f_agg);
+    (void)hipFree(ctx->f_incl);
+  }
+  OKV_HIP(hipMalloc(&ctx->f_flag, n * sizeof(uint32_t)));
+  OKV_HIP(hipMemsetAsync(ctx->f_flag, 0, n * sizeof(uint32_t), ctx->stream));
+  OKV_HIP(hipMalloc(&ctx->f_agg, n * sizeof(Prefix)));
+  OKV_HIP(hipMalloc(&ctx->f_incl, n * sizeof(Prefix)));
+  if (!ctx->f_ctr) {
+    OKV_HIP(hipMalloc(&ctx->f_ctr, 2 * sizeof(unsigned long long)));  // blocks, arrivals
+    OKV_HIP(hipMemsetAsync(ctx->f_ctr, 0, 2 * sizeof(unsigned long long), ctx->stream));
+    ctx->f_base = 0;
+  }
+  ctx->f_cap = n;
+  return OKV_OK;
+}
+
 int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
                   uint32_t nblk, int comp, okv_decode_out* o, uint32_t flags) {
   const bool index_only = flags & OKV_F_INDEX_ONLY;
@@ -1226,8 +1460,18 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   int rc = prepare(ctx, seg, seg_bytes, descs, nblk, comp, index_only, &w);
   if (rc) return rc;
   prof_mark(ctx, 1);
-  rc = launch_plan(ctx, w, nblk, o->row_start, true);
-  if (rc) return rc;
+  // small blocks: passes 1-3 in one launch (okv_decode_fused_kernel)
+  const bool fused =
+      ctx->fused && nblk && nblk <= kFusedMaxBlocks && gather_threads(ctx, w, nblk) == 64;
+  if (fused) {
+    if ((rc = ensure_blocks(ctx, nblk)) || (rc = ensure_fused(ctx, nblk))) return rc;
+    OKV_HIP(hipMemsetAsync(ctx->d_big + nblk, 0, sizeof(uint32_t), ctx->stream));
+    prof_mark(ctx, 2);
+    prof_mark(ctx, 3);
+  } else {
+    rc = launch_plan(ctx, w, nblk, o->row_start, true);
+    if (rc) return rc;
+  }
   CopyParams P;
   P.seg = w.seg;
   P.seg_bytes = w.seg_bytes;
@@ -1256,7 +1500,24 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   P.val_cap = index_only ? 0 : o->val_cap;
   if (nblk) {
     const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
-    if (gather_threads(ctx, w, nblk) == 256 && ctx->gather_staged && !index_only)
+    if (fused) {
+      FusedParams F;
+      F.pre = w.pre;
+      F.cnt = ctx->d_cnt;
+      F.lp = ctx->d_lp;
+      F.tile_pre = ctx->d_tile_pre;
+      F.flag = ctx->f_flag;
+      F.agg = ctx->f_agg;
+      F.incl = ctx->f_incl;
+      F.ctr = ctx->f_ctr;
+      F.arr = ctx->f_ctr + 1;
+      F.base = ctx->f_base;
+      ctx->f_epoch = (ctx->f_epoch + 1) & 0x3fffffffu;
+      F.epoch = ctx->f_epoch;
+      F.tot = ctx->d_tot;
+      hipLaunchKernelGGL(okv_decode_fused_kernel, dim3(nblk), dim3(64), 0, ctx->stream, P, F);
+      ctx->f_base += nblk;
+    } else if (gather_threads(ctx, w, nblk) == 256 && ctx->gather_staged && !index_only)
       hipLaunchKernelGGL((okv_gather_staged_kernel<kThreads>), g, dim3(kThreads), 0, ctx->stream, P);
     else if (gather_threads(ctx, w, nblk) == 64 && ctx->gather_staged)
       hipLaunchKernelGGL(okv_gather_small_kernel, g, dim3(64), 0, ctx->stream, P);
@@ -1396,6 +1657,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
     }
   }
   if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
+  if (const char* v = getenv("OKV_DECODE_FUSED")) ctx->fused = atoi(v) != 0;
   if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
   if (stream) {
     ctx->stream = static_cast<hipStream_t>(stream);
@@ -1426,6 +1688,10 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->d_tile_pre);
   (void)hipFree(ctx->d_rec);
   (void)hipFree(ctx->d_big);
+  (void)hipFree(ctx->f_flag);
+  (void)hipFree(ctx->f_agg);
+  (void)hipFree(ctx->f_incl);
+  (void)hipFree(ctx->f_ctr);
   (void)hipFree(ctx->d_tot);
   if (ctx->h_tot) (void)hipHostFree(ctx->h_tot);
   (void)hipFree(ctx->d_seg);

@@ -253,19 +253,21 @@ def _mixed_segment(kinds, seed):
 def decoders_by_width():
     """One decoder per pass-3 form, so every gather runs on the same inputs
     whatever the average block size: OKV_GATHER_THREADS=64 (one wave per
-    block, whole block staged in LDS), 256 (LDS-staged value spans, the
-    default for large blocks), and both with OKV_GATHER_STAGED=0 (global
-    windows): 64g, 256g."""
+    block, whole block staged in LDS; batches of <= 512 blocks in the
+    single-pass fused kernel), 64u (the same with OKV_DECODE_FUSED=0: three
+    launches), 256 (LDS-staged value spans, the default for large blocks), and
+    64 / 256 with OKV_GATHER_STAGED=0 and no fusion (global windows): 64g, 256g."""
     import os
     decs = {}
     try:
-        for w in ("64", "64g", "256", "256g"):
-            os.environ["OKV_GATHER_THREADS"] = w.rstrip("g")
+        for w in ("64", "64u", "64g", "256", "256g"):
+            os.environ["OKV_GATHER_THREADS"] = w.rstrip("gu")
             os.environ["OKV_GATHER_STAGED"] = "0" if w.endswith("g") else "1"
+            os.environ["OKV_DECODE_FUSED"] = "1" if w == "64" else "0"
             decs[w] = okv.Decoder(0)
     finally:
-        os.environ.pop("OKV_GATHER_THREADS", None)
-        os.environ.pop("OKV_GATHER_STAGED", None)
+        for k in ("OKV_GATHER_THREADS", "OKV_GATHER_STAGED", "OKV_DECODE_FUSED"):
+            os.environ.pop(k, None)
     yield decs
     for d in decs.values():
         d.close()
@@ -303,7 +305,7 @@ def _wide_segment(seed, nblk=120):
     return bytes(seg), np.array(descs, np.uint64).reshape(-1, 4)
 
 
-@pytest.mark.parametrize("width", ["256", "256g", "64", "64g"])
+@pytest.mark.parametrize("width", ["256", "256g", "64", "64u", "64g"])
 def test_wide_spans_all_gathers(decoders_by_width, width):
     """Stage overflow (one-tile retry and global fallback), the segment's
     first and last bytes, odd block offsets: every gather vs the oracle."""
@@ -313,7 +315,7 @@ def test_wide_spans_all_gathers(decoders_by_width, width):
         _assert_same_as_oracle(got, seg, d, 0, False)
 
 
-@pytest.mark.parametrize("width", ["64", "64g", "256", "256g"])
+@pytest.mark.parametrize("width", ["64", "64u", "64g", "256", "256g"])
 def test_mixed_blocks_both_gather_widths(decoders_by_width, width):
     """A segment mixing 4 KiB blocks, 64 KiB blocks with few rows and blocks
     over kRCap rows, through the 64- and the 256-thread gather."""

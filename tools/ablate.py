@@ -3,6 +3,7 @@
 output array between the arms.
 
 usage: python tools/ablate.py [arm ...]     arm = <threads>[:<grid>[:<staged>]]  (staged = OKV_GATHER_STAGED: 0 = global-window pass 3)
+  fused = OKV_DECODE_FUSED (0: small blocks decode in 3 launches)  arm = <t>:<grid>:<staged>:<fused>
   threads = 64 | 256 | auto (OKV_GATHER_THREADS), grid = OKV_GATHER_GRID (0: one per block)
 env:   ABL_NBLK (65536), ABL_ROUNDS (5), ABL_KIND (1 = Zipf C3, 0 = fixed C2),
        ABL_BS (65536), ABL_TH (57344)
@@ -31,7 +32,12 @@ stream = torch.cuda.current_stream(dev).cuda_stream
 decs = {}
 for a in arms:
     thr, _, rest = a.partition(":")
-    grid, _, staged = rest.partition(":")
+    grid, _, rest = rest.partition(":")
+    staged, _, fused = rest.partition(":")
+    if fused:
+        os.environ["OKV_DECODE_FUSED"] = fused
+    else:
+        os.environ.pop("OKV_DECODE_FUSED", None)
     os.environ["OKV_GATHER_GRID"] = grid or "0"
     if staged:
         os.environ["OKV_GATHER_STAGED"] = staged
@@ -85,5 +91,5 @@ for a in arms:
     ct = sorted(x[1] for x in res[a])
     med = cp[len(cp) // 2]
     print(f"arm={a:16s} gather_ms median={med:.4f} min={cp[0]:.4f} "
-          f"count_ms median={ct[len(ct) // 2]:.4f}  alg {alg / med / 1e6:.0f} GB/s "
+          f"count_ms median={ct[len(ct) // 2]:.4f} sum={med + ct[len(ct) // 2]:.4f}  alg {alg / med / 1e6:.0f} GB/s "
           f"frac {alg / med / 1e6 / 8000:.3f}", flush=True)

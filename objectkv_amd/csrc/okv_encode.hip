@@ -93,6 +93,7 @@ struct EncScratch {
   uint64_t* bsl = nullptr;       // [nb] tile-local inclusive BlockSize scan
   uint64_t* esl = nullptr;       // [nb] tile-local inclusive meta entry size scan
   uint64_t* moff = nullptr;      // [nb] meta entry offsets (relative to the meta block)
+  uint64_t* pbase = nullptr;     // [nb] P(first row - 1): the block's start in the row prefix
   size_t cap_blocks = 0;
   uint64_t* btile = nullptr;     // [4][nbtiles]: BlockSize tot/pre, entry tot/pre
   size_t cap_btiles = 0;
@@ -116,8 +117,8 @@ void enc_release(okv_ctx* ctx) {
   EncScratch* e = ctx->enc;
   if (!e) return;
   void* ps[] = {e->pl, e->nx, e->tile_tot, e->tile_pre, e->jt, e->jb, e->entry, e->kbase,
-                e->first, e->desc, e->hash, e->bsl, e->esl, e->moff, e->btile, e->d_tot,
-                e->d_in, e->d_outseg};
+                e->first, e->desc, e->hash, e->bsl, e->esl, e->moff, e->pbase, e->btile,
+                e->d_tot, e->d_in, e->d_outseg};
   for (void* p : ps)
     if (p) (void)hipFree(p);
   if (e->h_tot) (void)hipHostFree(e->h_tot);
@@ -134,9 +135,13 @@ void enc_release(okv_ctx* ctx) {
 // Shared device helpers
 // ---------------------------------------------------------------------------
 // P(i) = sum of record sizes of rows 0..i (P(-1) = 0).
+// Branch-free (the loads of index 0 stand in for P(-1)), so a caller's other
+// independent loads are not held behind a divergent block's wait.
 __device__ __forceinline__ uint64_t Pg(const uint64_t* __restrict__ pl,
                                        const uint64_t* __restrict__ tile_pre, int64_t i) {
-  return i < 0 ? 0 : pl[i] + tile_pre[uint64_t(i) / kETile];
+  const uint64_t j = i < 0 ? 0 : uint64_t(i);
+  const uint64_t v = pl[j] + tile_pre[j / kETile];
+  return i < 0 ? 0 : v;
 }
 
 // Workgroup exclusive scan of one u64 per thread (kThreads threads); also
@@ -156,6 +161,18 @@ __device__ __forceinline__ uint64_t wg_excl_scan(uint64_t v, uint64_t* sm, uint6
   __syncthreads();
   total = tot;
   return before + inc - v;
+}
+
+// rotl64(x, 31) as two independent alignbit ops (the shift/or form is two deep)
+__device__ __forceinline__ uint64_t rotl31(uint64_t x) {
+  const uint32_t lo = uint32_t(x), hi = uint32_t(x >> 32);
+  return uint64_t(__builtin_amdgcn_alignbit(lo, hi, 1)) |
+         (uint64_t(__builtin_amdgcn_alignbit(hi, lo, 1)) << 32);
+}
+// XXH64 round with its input already multiplied by PRIME64_2 (xp = in * XP2):
+// the accumulator chain is add, rotate, multiply.
+__device__ __forceinline__ uint64_t xround_pre(uint64_t acc, uint64_t xp) {
+  return rotl31(acc + xp) * XP1;
 }
 
 __device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
@@ -537,6 +554,7 @@ struct StatParams {
   uint64_t nb, D;
   int lz4;
   Desc* desc;
+  uint64_t* pbase;
   uint64_t* bsl;
   uint64_t* esl;
   uint64_t* btile_tot;
@@ -554,7 +572,9 @@ __global__ __launch_bounds__(kThreads) void okv_enc_stat_kernel(StatParams P) {
     const uint64_t k = base + i;
     if (k < P.nb) {
       const uint64_t r0 = P.first[k], r1 = P.first[k + 1];
-      const uint64_t raw = Pg(P.pl, P.tp, int64_t(r1) - 1) - Pg(P.pl, P.tp, int64_t(r0) - 1);
+      const uint64_t p0 = Pg(P.pl, P.tp, int64_t(r0) - 1);
+      const uint64_t raw = Pg(P.pl, P.tp, int64_t(r1) - 1) - p0;
+      P.pbase[k] = p0;
       const uint64_t bs = (raw / P.D + 1) * P.D;
       const uint64_t es = 42u + P.key_len[r0];
       Desc d;
@@ -626,6 +646,7 @@ struct PackParams {
   const uint64_t* tp;
   const uint64_t* first;
   const Desc* desc;
+  const uint64_t* pbase;  // [nb] P(first row - 1) (okv_enc_stat_kernel)
   uint8_t* seg;
   uint64_t* hash;  // BlockStat.Hash, written by kernels that hash in LDS
 };
@@ -931,11 +952,13 @@ __device__ __forceinline__ void lds_copy_field(uint32_t* img, uint32_t d, const 
   }
 }
 
-template <uint32_t IMG>
+template <uint32_t IMG, int V = 0>  // V: diagnostic ablation (OKV_ENC_VARIANT 4: no hash,
+                                   // 5: headers only, 6: loads without LDS writes)
 __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb,
                                                                     uint32_t G) {
   __shared__ uint4 img4[IMG / 16];
   __shared__ uint64_t bfirst[kMaxRegion + 1], brel[kMaxRegion], bbase[kMaxRegion];
+  __shared__ uint32_t slim[kMaxRegion], blen[kMaxRegion];  // end of whole stripes, BlockSize
   uint32_t* img = reinterpret_cast<uint32_t*>(img4);
   const uint64_t k0 = uint64_t(blockIdx.x) * G;
   const uint32_t g = uint32_t(std::min<uint64_t>(G, nb - k0));
@@ -948,8 +971,11 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P
     const uint64_t f = P.first[k0 + t];
     bfirst[t] = f;
     if (t < g) {
-      brel[t] = P.desc[k0 + t].offset - O0;
-      bbase[t] = Pg(P.pl, P.tp, int64_t(f) - 1);
+      const Desc dt = P.desc[k0 + t];
+      brel[t] = dt.offset - O0;
+      blen[t] = uint32_t(dt.block_size);
+      slim[t] = uint32_t(dt.offset - O0 + (dt.block_size & ~uint64_t(31)));
+      bbase[t] = P.pbase[k0 + t];  // one trip with first[] and desc[]
     }
   }
   __syncthreads();
@@ -966,12 +992,21 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P
     const uint32_t d = uint32_t(brel[lo] + Pg(P.pl, P.tp, int64_t(r) - 1) - bbase[lo]);
     const uint32_t kl = P.key_len[r], vl = P.val_len[r];
     const uint64_t ko = P.key_off[r], vo = P.val_off[r];
-    if (kl <= 64 && vl <= 64) {  // all source lines of the record in flight at once
+    if (V == 5) {
+      lds_or16(img, d, make_uint4(kl | (vl << 16), vl >> 16, 0, 0));
+    } else if (V == 6 && kl <= 64 && vl <= 64) {
       const Lines5 K = load_lines5(P.key_arena + ko, kl);
-      const Lines5 V = load_lines5(P.val_arena + vo, vl);
+      const Lines5 Vl = load_lines5(P.val_arena + vo, vl);
+      uint32_t x = 0;
+#pragma unroll
+      for (int t = 0; t < 5; ++t) x ^= K.l[t].x ^ K.l[t].w ^ Vl.l[t].y ^ Vl.l[t].z;
+      lds_or16(img, d, make_uint4(kl | (vl << 16), vl >> 16, x == 0x9e3779b9u ? 1u : 0u, 0));
+    } else if (kl <= 64 && vl <= 64) {  // all source lines of the record in flight at once
+      const Lines5 K = load_lines5(P.key_arena + ko, kl);
+      const Lines5 Vl = load_lines5(P.val_arena + vo, vl);
       lds_or16(img, d, make_uint4(kl | (vl << 16), vl >> 16, 0, 0));
       lds_put5(img, d + 6, K, kl);
-      if (vl) lds_put5(img, d + 6 + kl, V, vl);
+      if (vl) lds_put5(img, d + 6 + kl, Vl, vl);
     } else {
       lds_or16(img, d, make_uint4(kl | (vl << 16), vl >> 16, 0, 0));
       lds_copy_field(img, d + 6, P.key_arena + ko, kl);
@@ -979,26 +1014,52 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P
     }
   }
   __syncthreads();
+  // Store the image; each 16 bytes lying in whole 32-byte stripes of its block
+  // are then replaced in place (same lane, so no barrier between) by their two
+  // XXH64 round inputs x * PRIME64_2, computed by all 256 lanes: the four
+  // hashing lanes per block are left with add, rotate, multiply per round.
   uint4* dst = reinterpret_cast<uint4*>(P.seg + O0);
-  for (uint32_t q = threadIdx.x; q < nq; q += kThreads) dst[q] = img4[q];
+  for (uint32_t q = threadIdx.x; q < nq; q += kThreads) {
+    const uint4 v = img4[q];
+    dst[q] = v;
+    if (V == 4) continue;
+    const uint32_t p = q << 4;
+    uint32_t lo = 0, hi = g;  // block holding byte p
+    while (hi - lo > 1) {
+      const uint32_t m = (lo + hi) >> 1;
+      if (uint32_t(brel[m]) <= p)
+        lo = m;
+      else
+        hi = m;
+    }
+    if (p + 16 <= slim[lo]) {
+      const uint64_t a = ((uint64_t(v.y) << 32) | v.x) * XP2;
+      const uint64_t c = ((uint64_t(v.w) << 32) | v.z) * XP2;
+      img4[q] = make_uint4(uint32_t(a), uint32_t(a >> 32), uint32_t(c), uint32_t(c >> 32));
+    }
+  }
+  if (V == 4) return;
+  // only LDS has to be ordered here (a __syncthreads would also wait for the
+  // image's global stores)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   // BlockStat.Hash = XXH64 of the padded block (segment_writer.go:185), from
   // the image: four lanes per block own XXH64's four accumulators.
   if (threadIdx.x < 4 * g) {
     const uint32_t b = threadIdx.x >> 2, q = threadIdx.x & 3;
     const uint32_t boff = uint32_t(brel[b]);
-    const uint64_t len = P.desc[k0 + b].block_size;
+    const uint64_t len = blen[b];
     const uint64_t* w64 = reinterpret_cast<const uint64_t*>(img4) + (boff >> 3);
     uint64_t acc = (q == 0) ? XP1 + XP2 : (q == 1) ? XP2 : (q == 2) ? 0 : 0 - XP1;
     const uint32_t nstripe = uint32_t(len / 32);
     uint32_t st = 0;
-    for (; st + 8 <= nstripe; st += 8) {  // 8 LDS reads ahead of the multiply chain
+    for (; st + 8 <= nstripe; st += 8) {  // 8 LDS reads ahead of the round chain
       uint64_t x[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) x[u] = w64[4 * (st + u) + q];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc = xround(acc, x[u]);
+      for (int u = 0; u < 8; ++u) acc = xround_pre(acc, x[u]);
     }
-    for (; st < nstripe; ++st) acc = xround(acc, w64[4 * st + q]);
+    for (; st < nstripe; ++st) acc = xround_pre(acc, w64[4 * st + q]);
     const int lane = threadIdx.x & 63;
     const uint64_t a1 = __shfl(acc, (lane & ~3) + 1, 64);
     const uint64_t a2 = __shfl(acc, (lane & ~3) + 2, 64);
@@ -1335,6 +1396,7 @@ int ensure_blocks_enc(okv_ctx* ctx, EncScratch* e, uint64_t nb) {
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->bsl), c * 8))) return rc;
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->esl), c * 8))) return rc;
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->moff), c * 8))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->pbase), c * 8))) return rc;
     e->cap_blocks = c;
   }
   if (nbt > e->cap_btiles || !e->btile) {
@@ -1439,6 +1501,7 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   sp.D = D;
   sp.lz4 = o.compression == OKV_COMP_LZ4;
   sp.desc = e->desc;
+  sp.pbase = e->pbase;
   sp.bsl = e->bsl;
   sp.esl = e->esl;
   sp.btile_tot = btot;
@@ -1482,6 +1545,7 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   pp.tp = e->tile_pre;
   pp.first = e->first;
   pp.desc = e->desc;
+  pp.pbase = e->pbase;
   pp.seg = seg;
   pp.hash = e->hash;
   bool hashed = false;
@@ -1491,7 +1555,9 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   // record-major LDS assembly pays off for small records (most chunks would
   // mix fields); large records take the chunk-major kernels
   const char* eimg = getenv("OKV_ENC_IMAGE");  // diagnostic: LDS image bytes (16384 / 32768)
-  const uint32_t img = (eimg && atoi(eimg) == 32768) ? 32768u : kImage;
+  const int eimg_v = eimg ? atoi(eimg) : 0;
+  const uint32_t img = (eimg_v == 32768 || eimg_v == 8192 || eimg_v == 12288) ? uint32_t(eimg_v)
+                                                                              : kImage;
   const uint64_t GL = std::min<uint64_t>(kMaxRegion, img / std::max<uint64_t>(pl.bmax, 1));
   const bool aligned = o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0;
   const char* evar = getenv("OKV_ENC_VARIANT");
@@ -1500,7 +1566,19 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
     if (img == 32768)
       hipLaunchKernelGGL(okv_enc_pack_lds_kernel<32768>, dim3(ceil_div(pl.nb, GL)),
                          dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
-    else
+    else if (img == 8192)
+      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<8192>, dim3(ceil_div(pl.nb, GL)),
+                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
+    else if (img == 12288)
+      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<12288>, dim3(ceil_div(pl.nb, GL)),
+                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
+    else if (EV >= 4 && EV <= 6) {
+      auto* kern = EV == 4   ? okv_enc_pack_lds_kernel<kImage, 4>
+                   : EV == 5 ? okv_enc_pack_lds_kernel<kImage, 5>
+                             : okv_enc_pack_lds_kernel<kImage, 6>;
+      hipLaunchKernelGGL(kern, dim3(ceil_div(pl.nb, GL)), dim3(kThreads), 0, ctx->stream, pp,
+                         pl.nb, uint32_t(GL));
+    } else
       hipLaunchKernelGGL(okv_enc_pack_lds_kernel<kImage>, dim3(ceil_div(pl.nb, GL)),
                          dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
     hashed = true;

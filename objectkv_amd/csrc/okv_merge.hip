@@ -80,6 +80,8 @@ struct Scratch {
   uint32_t* escan = nullptr;  // [N + 1] emit flags, then their exclusive scan
   uint32_t cap_blk = 0;
   uint32_t* bsum = nullptr;   // scan block sums
+  uint64_t* split = nullptr;  // [ceil(N / 256)][K][2] rank-kernel search windows
+  size_t cap_split = 0;
   Src* d_src = nullptr;
   uint64_t* d_base = nullptr;  // [K + 1] stream offsets in the global row numbering
   uint8_t* d_bound = nullptr;
@@ -110,8 +112,23 @@ __device__ __forceinline__ uint64_t be_word(const uint8_t* k, uint32_t len, uint
   return p;
 }
 
+// The first 16 bytes from the aligned line(s) holding them (the second only
+// when the key runs into it: a line holding a valid byte never crosses the
+// allocation), bytes past len zeroed, then byte-swapped to big-endian words.
 __device__ __forceinline__ Key16 be_prefix(const uint8_t* k, uint32_t len) {
-  return Key16{be_word(k, len, 0), be_word(k, len, 8)};
+  if (len == 0) return Key16{0, 0};
+  const uintptr_t a = reinterpret_cast<uintptr_t>(k);
+  const uint4* line = reinterpret_cast<const uint4*>(a & ~uintptr_t(15));
+  const uint32_t sh = uint32_t(a & 15), n = len < 16 ? len : 16;
+  const uint4 x = line[0];
+  const uint4 y = sh + n > 16 ? line[1] : make_uint4(0, 0, 0, 0);
+  uint4 v = funnel32(x, y, sh);
+  v.x &= byte_mask(0, int32_t(n), 0);
+  v.y &= byte_mask(0, int32_t(n), 1);
+  v.z &= byte_mask(0, int32_t(n), 2);
+  v.w &= byte_mask(0, int32_t(n), 3);
+  return Key16{__builtin_bswap64(uint64_t(v.x) | (uint64_t(v.y) << 32)),
+               __builtin_bswap64(uint64_t(v.z) | (uint64_t(v.w) << 32))};
 }
 
 // bytes.Compare of two keys given their prefixes, lengths and addresses.
@@ -171,30 +188,80 @@ __device__ __forceinline__ uint64_t rank_in(const Key16* __restrict__ pfx,
 // 2. merged position and ownership of every row.  A row's rank in stream j
 // is monotone along its own stream, so when a workgroup's rows all come from
 // one stream the ranks of its first and last row bound every lane's search
-// window in stream j (a few cached steps instead of a full-range search).
+// window in stream j.  Those windows (prefix, length, address per row) are
+// staged in LDS when they fit, so the lanes' searches run at LDS latency;
+// otherwise the searches read the windows from HBM / L2.
+constexpr uint32_t kRankWin = 1024;  // staged window rows per workgroup (28 KiB)
+
+// 2a. the windows: for every rank workgroup (256 rows) the ranks of its first
+// and last row in every other stream, one full-range search per lane (the
+// searches are independent, so they overlap instead of holding a workgroup).
+__global__ __launch_bounds__(256) void okv_merge_split_kernel(
+    const uint64_t* __restrict__ base, uint32_t k, uint64_t n, const uint64_t* __restrict__ kaddr,
+    const mrg::Key16* __restrict__ pfx, const uint32_t* __restrict__ klen,
+    uint64_t* __restrict__ split) {
+  const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t nwg = (n + 255) / 256;
+  if (t >= nwg * 2 * k) return;
+  const uint64_t wg = t / (2 * k);
+  const uint32_t q = uint32_t(t % (2 * k)), j = q >> 1;
+  const uint64_t g0 = wg * 256, g1 = (g0 + 256 < n ? g0 + 256 : n) - 1;
+  const uint64_t ge = (q & 1) ? g1 : g0;
+  const uint32_t i = mrg::find_src(base, k, ge);
+  split[t] = j == i ? 0
+                    : mrg::rank_in(pfx, klen, kaddr, base[j], base[j + 1], pfx[ge], klen[ge],
+                                   reinterpret_cast<const uint8_t*>(kaddr[ge]), j < i);
+}
+
 __global__ __launch_bounds__(256) void okv_merge_rank_kernel(
     const uint64_t* __restrict__ base, uint32_t k, uint64_t n, const uint64_t* __restrict__ kaddr,
     const mrg::Key16* __restrict__ pfx, const uint32_t* __restrict__ klen,
-    uint64_t* __restrict__ pos, uint8_t* __restrict__ own) {
+    const uint64_t* __restrict__ split, int stage, uint64_t* __restrict__ pos,
+    uint8_t* __restrict__ own) {
   __shared__ uint64_t s_lo[mrg::kMaxSrc], s_hi[mrg::kMaxSrc];
+  __shared__ uint32_t w_at[mrg::kMaxSrc + 1];
+  __shared__ mrg::Key16 w_pfx[kRankWin];
+  __shared__ uint64_t w_addr[kRankWin];
+  __shared__ uint32_t w_len[kRankWin];
   const uint64_t g0 = uint64_t(blockIdx.x) * blockDim.x;
   const uint64_t g1 = (g0 + blockDim.x < n ? g0 + blockDim.x : n) - 1;
   const uint32_t i0 = mrg::find_src(base, k, g0), i1 = mrg::find_src(base, k, g1);
   const bool one = i0 == i1;
   if (one) {
     for (uint32_t t = threadIdx.x; t < 2 * k; t += blockDim.x) {
-      const uint32_t j = t >> 1;
-      if (j == i0) continue;
-      const uint64_t ge = (t & 1) ? g1 : g0;
-      const uint64_t r = mrg::rank_in(pfx, klen, kaddr, base[j], base[j + 1], pfx[ge], klen[ge],
-                                      reinterpret_cast<const uint8_t*>(kaddr[ge]), j < i0);
+      const uint64_t r = split[uint64_t(blockIdx.x) * 2 * k + t];
       if (t & 1)
-        s_hi[j] = r;
+        s_hi[t >> 1] = r;
       else
-        s_lo[j] = r;
+        s_lo[t >> 1] = r;
     }
   }
   __syncthreads();
+  bool staged = false;
+  if (one && stage) {
+    if (threadIdx.x == 0) {
+      uint64_t tot = 0;
+      for (uint32_t j = 0; j < k; ++j) {
+        w_at[j] = uint32_t(tot < kRankWin ? tot : kRankWin);
+        tot += s_hi[j] - s_lo[j];
+      }
+      w_at[k] = uint32_t(tot <= kRankWin ? tot : kRankWin + 1);  // > kRankWin: not staged
+    }
+    __syncthreads();
+    staged = w_at[k] <= kRankWin;
+    if (staged) {
+      for (uint32_t j = 0; j < k; ++j) {
+        const uint64_t lo = s_lo[j];
+        const uint32_t w = uint32_t(s_hi[j] - lo), o = w_at[j];
+        for (uint32_t t = threadIdx.x; t < w; t += blockDim.x) {
+          w_pfx[o + t] = pfx[lo + t];
+          w_len[o + t] = klen[lo + t];
+          w_addr[o + t] = kaddr[lo + t];
+        }
+      }
+    }
+    __syncthreads();
+  }
   const uint64_t g = g0 + threadIdx.x;
   if (g >= n) return;
   const uint32_t i = one ? i0 : mrg::find_src(base, k, g);
@@ -205,15 +272,40 @@ __global__ __launch_bounds__(256) void okv_merge_rank_kernel(
   uint8_t owner = 1;
   for (uint32_t j = 0; j < k; ++j) {
     if (j == i) continue;
-    // count of stream-j keys <= key (j < i: earlier streams own ties) or < key
-    const uint64_t lo = one ? s_lo[j] : base[j], hi = one ? s_hi[j] : base[j + 1];
-    const uint64_t r = mrg::rank_in(pfx, klen, kaddr, lo, hi, p0, l0, k0, j < i);
+    const bool le = j < i;  // earlier streams own ties: count keys <= key
+    uint64_t r;
+    if (staged) {
+      const uint32_t o = w_at[j];
+      uint32_t lo = 0, hi = uint32_t(s_hi[j] - s_lo[j]);
+      while (lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        const int c = mrg::key_cmp(w_pfx[o + m], w_len[o + m],
+                                   reinterpret_cast<const uint8_t*>(w_addr[o + m]), p0, l0, k0);
+        if (c < 0 || (c == 0 && le))
+          lo = m + 1;
+        else
+          hi = m;
+      }
+      r = s_lo[j] + lo;
+      // an earlier stream holding the key owns it: its row r - 1 equals the key
+      if (le && r > base[j]) {
+        const bool in = lo > 0;
+        const int c = in ? mrg::key_cmp(w_pfx[o + lo - 1], w_len[o + lo - 1],
+                                        reinterpret_cast<const uint8_t*>(w_addr[o + lo - 1]), p0,
+                                        l0, k0)
+                         : mrg::key_cmp(pfx[r - 1], klen[r - 1],
+                                        reinterpret_cast<const uint8_t*>(kaddr[r - 1]), p0, l0, k0);
+        if (c == 0) owner = 0;
+      }
+    } else {
+      const uint64_t lo = one ? s_lo[j] : base[j], hi = one ? s_hi[j] : base[j + 1];
+      r = mrg::rank_in(pfx, klen, kaddr, lo, hi, p0, l0, k0, le);
+      if (le && r > base[j] &&
+          mrg::key_cmp(pfx[r - 1], klen[r - 1], reinterpret_cast<const uint8_t*>(kaddr[r - 1]),
+                       p0, l0, k0) == 0)
+        owner = 0;
+    }
     rank += r - base[j];
-    // an earlier stream holding the key owns it: its row r - 1 equals the key
-    if (j < i && r > base[j] &&
-        mrg::key_cmp(pfx[r - 1], klen[r - 1], reinterpret_cast<const uint8_t*>(kaddr[r - 1]), p0,
-                     l0, k0) == 0)
-      owner = 0;
   }
   pos[g] = rank;
   own[g] = owner;
@@ -482,7 +574,8 @@ void merge_release(okv_ctx* ctx) {
                   static_cast<void*>(m->own), static_cast<void*>(m->mg),
                   static_cast<void*>(m->mown), static_cast<void*>(m->uniq),
                   static_cast<void*>(m->ev), static_cast<void*>(m->escan),
-                  static_cast<void*>(m->bsum), static_cast<void*>(m->d_src),
+                  static_cast<void*>(m->bsum), static_cast<void*>(m->split),
+                  static_cast<void*>(m->d_src),
                   static_cast<void*>(m->d_base), static_cast<void*>(m->d_bound),
                   static_cast<void*>(m->d_misc)})
     (void)hipFree(p);
@@ -534,8 +627,20 @@ int okv_merge_rows(okv_ctx* ctx, const okv_merge_src* srcs, uint32_t nsrc,
   if (n == 0) return OKV_OK;
   hipLaunchKernelGGL(okv_merge_pfx_kernel, gn, b256, 0, s, m->d_src, m->d_base, nsrc, n, m->kaddr,
                      m->pfx, m->klen);
+  if ((rc = grow(ctx, reinterpret_cast<void**>(&m->split), &m->cap_split,
+                 8 * 2 * nsrc * ((n + 255) / 256))))
+    return rc;
+  {
+    const uint64_t ns = 2 * nsrc * ((n + 255) / 256);
+    hipLaunchKernelGGL(okv_merge_split_kernel, dim3(uint32_t((ns + 255) / 256)), b256, 0, s,
+                       m->d_base, nsrc, n, m->kaddr, m->pfx, m->klen, m->split);
+  }
+  static const int stage = [] {
+    const char* e = getenv("OKV_MERGE_STAGE");  // A/B knob: 0 = windows searched in HBM / L2
+    return e ? atoi(e) : 1;
+  }();
   hipLaunchKernelGGL(okv_merge_rank_kernel, gn, b256, 0, s, m->d_base, nsrc, n, m->kaddr, m->pfx,
-                     m->klen, m->pos, m->own);
+                     m->klen, m->split, stage, m->pos, m->own);
   hipLaunchKernelGGL(okv_merge_scatter_kernel, gn, b256, 0, s, n, m->pos, m->own, m->mg, m->mown);
   OKV_HIP(hipMemsetAsync(m->mown + n, 0, 4, s));
   uint32_t* d_tot = reinterpret_cast<uint32_t*>(m->d_misc + 2 + mrg::kMaxSrc);

@@ -66,6 +66,14 @@ struct okv_ctx {
   uint32_t gather_grid = 0;  // 0: default grid; else workgroups (OKV_GATHER_GRID)
   uint32_t gather_threads = 0;  // 0: by average block size; else 64 or 256 (OKV_GATHER_THREADS)
   bool gather_staged = true;    // 256-thread pass 3 stages value spans in LDS (OKV_GATHER_STAGED=0: off)
+  uint32_t value_sweep = 0;     // 0: values in the per-block pass 3; 1/2: okv_value_sweep_kernel
+                                // with 1 or 2 tiles per workgroup (OKV_VALUE_SWEEP)
+  void* d_hdr = nullptr;        // [nblk x kRCap] pass-1 headers (sweep)
+  size_t cap_hdr = 0;
+  void* d_vsrc = nullptr;       // [row] value sources (sweep hand-off)
+  size_t cap_vsrc = 0;
+  void* d_vtile = nullptr;      // [value-arena tile] owning rows
+  size_t cap_vtile = 0;
   bool prof = false;
   std::vector<hipEvent_t> ev;  // 5 per timed call
   size_t ev_used = 0;

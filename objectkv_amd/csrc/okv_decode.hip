@@ -63,7 +63,7 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     uint32_t* __restrict__ big_count, const int32_t* __restrict__ pre_status, int prefetch,
 
     Prefix* __restrict__ single_pre, Totals* __restrict__ single_tot,
-    uint64_t* __restrict__ single_row_start) {
+    uint64_t* __restrict__ single_row_start, uint64_t* __restrict__ hdr_s) {
   const uint32_t tid = threadIdx.x;
   const uint32_t b = blockIdx.x * kTile + tid;
   uint64_t rows = 0, kb = 0, vb = 0, p = 0;
@@ -119,6 +119,9 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
         }
         if (rows < kRCap) {
           rec_s[rec_index(nblk, b, uint32_t(rows))] = uint32_t(p);
+          // the value sweep's row pass takes the headers from here (one HBM
+          // trip fewer than reading them again at the positions)
+          if (hdr_s) hdr_s[rec_index(nblk, b, uint32_t(rows))] = (uint64_t(kl) << 32) | vl;
         }
         rows++;
         kb += kl;
@@ -264,7 +267,23 @@ struct CopyParams {
   uint8_t* key_arena;
   uint8_t* val_arena;
   uint64_t row_cap, key_cap, val_cap;
+  // value sweep hand-off (okv_value_sweep_kernel; null: pass 3 gathers values itself)
+  uint64_t* vsrc;             // [row] segment position of the row's value
+  uint32_t* vtile;            // [value-arena tile] row owning the tile's first byte
+  uint4* bchunk;              // [row] the chunk holding the end of the row's value
+  const uint64_t* hdr_s;      // pass-1 headers (klen << 32 | vlen), rec_index layout
+  const Totals* tot;          // call totals (pass 1 / pass 2)
 };
+
+// The value sweep runs when every row's index is written by the per-block
+// pass 3 and the value arena is gap-free: no big block (okv_copy_kernel's
+// rows) and no capacity failure.  Every workgroup of both kernels reads the
+// same scalars, so they agree.
+constexpr uint32_t kSwTile = 4096;  // value-arena bytes per sweep tile
+__device__ __forceinline__ bool sweep_safe(const Totals& T, uint32_t nbig, uint64_t row_cap,
+                                           uint64_t key_cap, uint64_t val_cap) {
+  return nbig == 0 && T.rows <= row_cap && T.kb <= key_cap && T.vb <= val_cap;
+}
 
 // Global row / arena bases of block b and its final status (capacity check).
 struct BlockBase {
@@ -476,6 +495,45 @@ __device__ __forceinline__ void write_row_index(const CopyParams& P, const Gathe
   }
 }
 
+// Value-sweep hand-off (lane r = row r): each row's value source, the row
+// owning each value-arena tile that starts inside its value, and the row's
+// boundary chunk.  A 16-byte chunk holding the end of row r's value (end not
+// 16-aligned) mixes rows (or the block's zero padding); the lane of the row
+// owning its first byte assembles it from the block's row table into
+// bchunk[row], and the sweep stores it with its tile (whole lines).  The
+// loads are issued first (with the key loads in flight: see okv_rows_kernel).
+__device__ __forceinline__ uint4 boundary_chunk(const CopyParams& P, const GatherSmem& sm,
+                                                const BlockMeta& m, int rows) {
+  const uint32_t t = threadIdx.x;
+  uint4 out = make_uint4(0, 0, 0, 0);
+  if (int(t) >= rows) return out;
+  const uint32_t v0 = sm.vpre[t], e = sm.vpre[t + 1];
+  const uint32_t C = e & ~15u;
+  if (e == v0 || (e & 15) == 0 || v0 > C) return out;  // no chunk of mine to assemble
+  out = merge_bytes(out, window16(P.seg, P.seg_bytes, int64_t(m.off + sm.vsb[t] + C)), 0,
+                    int32_t(e - C));
+  for (uint32_t j = t + 1; int(j) < rows && sm.vpre[j] < C + 16; ++j) {
+    const uint32_t q0 = sm.vpre[j], q1 = sm.vpre[j + 1];
+    if (q1 == q0) continue;
+    const uint4 w = window16(P.seg, P.seg_bytes, int64_t(m.off + sm.vsb[j] + C));
+    out = merge_bytes(out, w, int32_t(q0 - C), int32_t(min(q1, C + 16) - C));
+  }
+  return out;
+}
+__device__ __forceinline__ void sweep_handoff(const CopyParams& P, const GatherSmem& sm,
+                                              const BlockMeta& m, int rows, const uint4& bc) {
+  const uint32_t t = threadIdx.x;
+  if (int(t) >= rows) return;
+  const uint64_t g = m.B.row0 + t;
+  const uint32_t kl = sm.kpre[t + 1] - sm.kpre[t];
+  const uint32_t v0 = sm.vpre[t], e = sm.vpre[t + 1];
+  P.vsrc[g] = m.off + sm.rec[t] + 6 + kl;
+  P.bchunk[g] = bc;
+  for (uint64_t x = (m.B.vb0 + v0 + kSwTile - 1) & ~uint64_t(kSwTile - 1); x < m.B.vb0 + e;
+       x += kSwTile)
+    P.vtile[x / kSwTile] = uint32_t(g);
+}
+
 // Pass 3: one workgroup per block reads the block straight from HBM.  NT = 64
 // (one wave per block) for small blocks, where a block has only a few 1 KiB
 // tiles and more blocks in flight hide the row-table -> gather latency chain;
@@ -500,6 +558,46 @@ __global__ __launch_bounds__(NT) void okv_gather_kernel(CopyParams P) {
         gather_region<false>(src, sm, rows, P.key_arena, m.B.kb0, threadIdx.x >> 6, NT / 64);
         gather_region<true>(src, sm, rows, P.val_arena, m.B.vb0, threadIdx.x >> 6, NT / 64);
       }
+    }
+    if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
+  }
+}
+
+// Pass 3a of the value sweep: one wave per block writes the row index and
+// the key region and hands the values to okv_value_sweep_kernel.  A latency
+// chain (metadata -> record positions -> headers -> keys), so it is sized for
+// occupancy: one window per lane in flight.  When the sweep is unsafe (big
+// blocks, capacity) it gathers the values itself.
+__global__ __launch_bounds__(64) void okv_rows_kernel(CopyParams P) {
+  __shared__ GatherSmem sm;
+  const bool sweep = sweep_safe(*P.tot, *P.big_count, P.row_cap, P.key_cap, P.val_cap);
+  for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
+    // record positions and headers with the metadata (one trip; the slots
+    // exist for every block, only the first `rows` are meaningful)
+    const uint32_t t = threadIdx.x;
+    const uint32_t rec = P.rec_s[rec_index(P.nblk, b, t)];
+    const uint64_t hdr = P.hdr_s ? P.hdr_s[rec_index(P.nblk, b, t)] : 0;
+    const BlockMeta m = block_meta(P, b);
+    if (block_head(P, b, m)) {
+      const int rows = int(m.c.rows);
+      const GlobalWin src{P.seg, P.seg_bytes, m.off};
+      if (P.hdr_s) {
+        const bool live = int(t) < rows;
+        fill_row_table(sm, rows, live ? rec : 0u, live ? uint32_t(hdr >> 32) : 0u,
+                       live ? uint32_t(hdr) : 0u);
+      } else {
+        build_row_table(src, sm, rows, int(t) < rows ? rec : 0u);
+      }
+      __syncthreads();
+      write_row_index(P, sm, m, rows);
+      const uint4 bc = sweep ? boundary_chunk(P, sm, m, rows) : make_uint4(0, 0, 0, 0);
+      gather_tiles<false, GlobalWin, 1>(src, sm, rows, P.key_arena, m.B.kb0, 0,
+                                        (sm.kpre[rows] + 1023) >> 10, 1);
+      if (sweep)
+        sweep_handoff(P, sm, m, rows, bc);
+      else
+        gather_tiles<true, GlobalWin, 1>(src, sm, rows, P.val_arena, m.B.vb0, 0,
+                                         (sm.vpre[rows] + 1023) >> 10, 1);
     }
     if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
   }
@@ -648,10 +746,152 @@ __global__ __launch_bounds__(NT) void okv_gather_staged_kernel(CopyParams P) {
                                         uint32_t(uint64_t(Tk) * (wave + 1) / (NT / 64)), 1);
       const uint32_t T = (sm.vpre[rows] + 1023) >> 10;
       gather_values_staged<U>(src, sm, rows, P.val_arena, m.B.vb0,
-                           uint32_t(uint64_t(T) * wave / (NT / 64)),
-                           uint32_t(uint64_t(T) * (wave + 1) / (NT / 64)), stage[wave]);
+                              uint32_t(uint64_t(T) * wave / (NT / 64)),
+                              uint32_t(uint64_t(T) * (wave + 1) / (NT / 64)), stage[wave]);
     }
     if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 3b, value sweep: the value arena in address order, one short-lived
+// workgroup per kU x 4 KiB of destination (dispatch order = address order, so
+// the chip's loads and stores stay in one compact window of source and
+// destination -- the one-shot copy shape).  Lane l of tile t
+// produces the 16-byte chunk at X = 4096 t + 16 l: the owning row (the last
+// with val_off <= X) comes from the tile's rows [vtile[t], vtile[t + kU]],
+// staged in LDS; its bytes from two aligned 16-byte loads + the funnel; bytes
+// past its value from the following rows (val_off < X + 16); the rest zero.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSwRows = 256;  // rows of a sweep workgroup held in LDS
+struct SweepParams {
+  const uint8_t* seg;
+  uint64_t seg_bytes;
+  const uint64_t* val_off;
+  const uint32_t* val_len;
+  const uint64_t* vsrc;
+  const uint32_t* vtile;
+  const uint4* bchunk;
+  uint8_t* val_arena;
+  const Totals* tot;
+  const uint32_t* big_count;
+  uint64_t row_cap, key_cap, val_cap;
+};
+
+// Rows of a sweep workgroup in LDS, relative to its first byte X0: value
+// start and end (clamped to +-2^30: only their order against chunk positions
+// in [0, kU x 4096) matters) and the source bias (segment position of arena
+// byte X = bias + X).
+struct SweepRows {
+  int32_t rel[kSwRows];
+  int32_t end[kSwRows];
+  int64_t bias[kSwRows];
+};
+__device__ __forceinline__ int32_t clamp_rel(int64_t v) {
+  return int32_t(v < -(int64_t(1) << 30) ? -(int64_t(1) << 30)
+                                         : (v > (int64_t(1) << 30) ? (int64_t(1) << 30) : v));
+}
+
+// Workgroups whose rows overflow the LDS window (tiny values): rows past the
+// window come from HBM.
+__device__ __noinline__ uint4 sweep_chunk_any(const uint8_t* seg, uint64_t seg_bytes,
+                                              const uint64_t* val_off, const uint32_t* val_len,
+                                              const uint64_t* vsrc, uint64_t r0, uint64_t r1,
+                                              uint64_t rows, uint64_t X) {
+  uint64_t lo = r0, hi = r1;  // invariant: val_off[lo] <= X
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi + 1) >> 1;
+    if (val_off[mid] <= X) lo = mid; else hi = mid - 1;
+  }
+  uint64_t k = lo;
+  uint64_t ko = val_off[k];
+  uint32_t kl = val_len[k];
+  const uint4 w = window16(seg, seg_bytes, int64_t(vsrc[k] + (X - ko)));
+  uint4 out = merge_bytes(make_uint4(0, 0, 0, 0), w, 0, int32_t(min<uint64_t>(16, ko + kl - X)));
+  for (++k; k < rows; ++k) {
+    ko = val_off[k];
+    if (ko >= X + 16) break;
+    kl = val_len[k];
+    if (kl == 0) continue;
+    const uint4 v = window16(seg, seg_bytes, int64_t(vsrc[k]) - int64_t(ko - X));
+    out = merge_bytes(out, v, int32_t(ko - X), int32_t(min<uint64_t>(16, ko + kl - X)));
+  }
+  return out;
+}
+
+template <uint32_t kU>
+__global__ __launch_bounds__(256) void okv_value_sweep_kernel(SweepParams S) {
+  __shared__ SweepRows R;
+  const uint64_t tile0 = uint64_t(blockIdx.x) * kU;
+  // one trip for every scalar: the totals, the big-block count and the two
+  // tile entries (tile0 + kU <= tiles launched + 1: inside the table)
+  const Totals T = *S.tot;
+  const uint32_t nbig = *S.big_count;
+  const uint32_t e0 = S.vtile[tile0], e1 = S.vtile[tile0 + kU];
+  if (!sweep_safe(T, nbig, S.row_cap, S.key_cap, S.val_cap)) return;
+  const uint64_t X0 = tile0 * kSwTile;
+  if (X0 >= T.vb) return;
+  const uint64_t ntile = (T.vb + kSwTile - 1) / kSwTile;
+  // rows [r0, r1] cover the workgroup's bytes; r1 + 1 ends the last spill
+  // check.  (Clamped into [0, rows): every index stays inside the row arrays
+  // whatever the table holds.)
+  const uint64_t r0 = min<uint64_t>(e0, T.rows - 1);
+  const uint64_t r1 =
+      tile0 + kU < ntile ? min<uint64_t>(max<uint64_t>(e1, r0), T.rows - 1) : T.rows - 1;
+  const uint64_t rend = min<uint64_t>(r1 + 1, T.rows - 1);
+  const bool full = rend - r0 + 1 <= kSwRows;  // uniform
+  const uint32_t nw = uint32_t(min<uint64_t>(rend - r0 + 1, kSwRows));
+  const uint32_t tid = threadIdx.x;
+  if (tid < nw) {
+    const int64_t off = int64_t(S.val_off[r0 + tid]);
+    const uint32_t len = S.val_len[r0 + tid];
+    const int64_t src = int64_t(S.vsrc[r0 + tid]);
+    R.rel[tid] = clamp_rel(off - int64_t(X0));
+    R.end[tid] = clamp_rel(off + int64_t(len) - int64_t(X0));
+    R.bias[tid] = src - off;
+  }
+  __syncthreads();
+  uint4 out[kU];
+  bool put[kU];
+  // every load issued before any is used
+#pragma unroll
+  for (uint32_t u = 0; u < kU; ++u) {
+    const int32_t xr = int32_t(u * kSwTile + 16u * tid);
+    const uint64_t X = X0 + uint32_t(xr);
+    out[u] = make_uint4(0, 0, 0, 0);
+    put[u] = X < T.vb;
+    if (!full || !put[u]) continue;
+    // owner: last local row with rel <= xr (rel is non-decreasing)
+    uint32_t o = 0;
+    if (nw <= 8) {
+      for (uint32_t j = 1; j < nw; ++j) o = R.rel[j] <= xr ? j : o;
+    } else {
+      uint32_t hi = nw - 1;
+      while (o < hi) {
+        const uint32_t mid = (o + hi + 1) >> 1;
+        if (R.rel[mid] <= xr) o = mid; else hi = mid - 1;
+      }
+    }
+    // one unaligned 16-byte load inside the owner's value, or the owner's
+    // boundary chunk (okv_rows_kernel)
+    if (xr + 16 <= R.end[o])
+      out[u] = *reinterpret_cast<const uint4*>(S.seg + (R.bias[o] + int64_t(X)));
+    else
+      out[u] = S.bchunk[r0 + o];
+  }
+  if (!full) {
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint64_t X = X0 + uint64_t(u) * kSwTile + 16u * tid;
+      if (put[u])
+        out[u] = sweep_chunk_any(S.seg, S.seg_bytes, S.val_off, S.val_len, S.vsrc, r0, r1, T.rows,
+                                 X);
+    }
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < kU; ++u) {
+    const uint64_t X = X0 + uint64_t(u) * kSwTile + 16u * tid;
+    if (put[u]) *reinterpret_cast<uint4*>(S.val_arena + X) = out[u];
   }
 }
 
@@ -1392,7 +1632,7 @@ uint32_t gather_threads(const okv_ctx* ctx, const Work& w, uint32_t nblk) {
 
 // Launch passes 1 and 2 on device inputs.
 int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_start,
-                bool timed = false) {
+                bool timed = false, uint64_t* d_hdr = nullptr) {
   int rc = ensure_blocks(ctx, nblk);
   if (rc) return rc;
   const uint32_t ntiles = (nblk + kTile - 1) / kTile;
@@ -1406,7 +1646,7 @@ int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_star
                        w.seg_bytes, w.descs, nblk, w.comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
                        ctx->d_rec, ctx->d_big, ctx->d_big + nblk, w.pre, prefetch,
                        single ? ctx->d_tile_pre : nullptr, single ? ctx->d_tot : nullptr,
-                       single ? d_row_start : nullptr);
+                       single ? d_row_start : nullptr, d_hdr);
   if (timed) prof_mark(ctx, 2);
   if (!single)
     hipLaunchKernelGGL(okv_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_tile_tot,
@@ -1463,13 +1703,23 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   // small blocks: passes 1-3 in one launch (okv_decode_fused_kernel)
   const bool fused =
       ctx->fused && nblk && nblk <= kFusedMaxBlocks && gather_threads(ctx, w, nblk) == 64;
+  // values by the address-ordered sweep (256-thread staged pass 3 only; the
+  // kernels fall back to the per-block value gather on device when it is unsafe)
+  const bool sweep = ctx->value_sweep && nblk && !fused && !index_only && ctx->gather_staged &&
+                     gather_threads(ctx, w, nblk) == 256 && o->row_cap < (uint64_t(1) << 32);
+  if (sweep) {
+    if ((rc = ensure_blocks(ctx, nblk)) ||
+        (rc = grow(ctx, &ctx->d_hdr, &ctx->cap_hdr, size_t(nblk) * kRCap * 8)))
+      return rc;
+  }
   if (fused) {
     if ((rc = ensure_blocks(ctx, nblk)) || (rc = ensure_fused(ctx, nblk))) return rc;
     OKV_HIP(hipMemsetAsync(ctx->d_big + nblk, 0, sizeof(uint32_t), ctx->stream));
     prof_mark(ctx, 2);
     prof_mark(ctx, 3);
   } else {
-    rc = launch_plan(ctx, w, nblk, o->row_start, true);
+    rc = launch_plan(ctx, w, nblk, o->row_start, true,
+                     sweep ? static_cast<uint64_t*>(ctx->d_hdr) : nullptr);
     if (rc) return rc;
   }
   CopyParams P;
@@ -1498,6 +1748,23 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   P.row_cap = o->row_cap;
   P.key_cap = index_only ? 0 : o->key_cap;
   P.val_cap = index_only ? 0 : o->val_cap;
+  P.vsrc = nullptr;
+  P.vtile = nullptr;
+  P.bchunk = nullptr;
+  P.hdr_s = sweep ? static_cast<const uint64_t*>(ctx->d_hdr) : nullptr;
+  P.tot = ctx->d_tot;
+  uint64_t sw_tiles = 0;
+  if (sweep) {
+    sw_tiles = (o->val_cap + kSwTile - 1) / kSwTile;
+    if ((rc = grow(ctx, &ctx->d_vsrc, &ctx->cap_vsrc, std::max<uint64_t>(o->row_cap, 1) * 24 + 256)) ||
+        (rc = grow(ctx, &ctx->d_vtile, &ctx->cap_vtile, (sw_tiles + 4) * 4)))
+      return rc;
+    // [row] u64 sources, then [row] 16-byte boundary chunks
+    P.vsrc = static_cast<uint64_t*>(ctx->d_vsrc);
+    P.bchunk = reinterpret_cast<uint4*>(static_cast<uint8_t*>(ctx->d_vsrc) +
+                                        ((std::max<uint64_t>(o->row_cap, 1) * 8 + 255) & ~255ull));
+    P.vtile = static_cast<uint32_t*>(ctx->d_vtile);
+  }
   if (nblk) {
     const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
     if (fused) {
@@ -1517,9 +1784,26 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       F.tot = ctx->d_tot;
       hipLaunchKernelGGL(okv_decode_fused_kernel, dim3(nblk), dim3(64), 0, ctx->stream, P, F);
       ctx->f_base += nblk;
-    } else if (gather_threads(ctx, w, nblk) == 256 && ctx->gather_staged && !index_only)
+    } else if (sweep) {
+      // per-block rows + keys (one wave per block), then the value sweep
+      hipLaunchKernelGGL(okv_rows_kernel, g, dim3(64), 0, ctx->stream, P);
+      if (sw_tiles) {
+        SweepParams S{w.seg, w.seg_bytes, o->val_off, o->val_len, P.vsrc, P.vtile, P.bchunk,
+                      o->val_arena,
+                      ctx->d_tot, P.big_count, o->row_cap, o->key_cap, o->val_cap};
+        if (ctx->value_sweep == 4)
+          hipLaunchKernelGGL(okv_value_sweep_kernel<4>, dim3(uint32_t((sw_tiles + 3) / 4)),
+                             dim3(256), 0, ctx->stream, S);
+        else if (ctx->value_sweep == 2)
+          hipLaunchKernelGGL(okv_value_sweep_kernel<2>, dim3(uint32_t((sw_tiles + 1) / 2)),
+                             dim3(256), 0, ctx->stream, S);
+        else
+          hipLaunchKernelGGL(okv_value_sweep_kernel<1>, dim3(uint32_t(sw_tiles)), dim3(256), 0,
+                             ctx->stream, S);
+      }
+    } else if (gather_threads(ctx, w, nblk) == 256 && ctx->gather_staged && !index_only) {
       hipLaunchKernelGGL((okv_gather_staged_kernel<kThreads>), g, dim3(kThreads), 0, ctx->stream, P);
-    else if (gather_threads(ctx, w, nblk) == 64 && ctx->gather_staged)
+    } else if (gather_threads(ctx, w, nblk) == 64 && ctx->gather_staged)
       hipLaunchKernelGGL(okv_gather_small_kernel, g, dim3(64), 0, ctx->stream, P);
     else if (gather_threads(ctx, w, nblk) == 64)
       hipLaunchKernelGGL(okv_gather_kernel<64>, g, dim3(64), 0, ctx->stream, P);
@@ -1659,6 +1943,13 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
   if (const char* v = getenv("OKV_DECODE_FUSED")) ctx->fused = atoi(v) != 0;
   if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
+  if (const char* v = getenv("OKV_VALUE_SWEEP")) {
+    ctx->value_sweep = uint32_t(atoi(v));
+    if (ctx->value_sweep > 4 || ctx->value_sweep == 3) {
+      delete ctx;
+      return nullptr;
+    }
+  }
   if (stream) {
     ctx->stream = static_cast<hipStream_t>(stream);
   } else {
@@ -1698,6 +1989,9 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->d_desc);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_hash);
+  (void)hipFree(ctx->d_vsrc);
+  (void)hipFree(ctx->d_hdr);
+  (void)hipFree(ctx->d_vtile);
   (void)hipFree(ctx->z_cap_off);
   (void)hipFree(ctx->z_dec_len);
   (void)hipFree(ctx->z_status);

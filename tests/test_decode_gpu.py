@@ -255,18 +255,22 @@ def decoders_by_width():
     whatever the average block size: OKV_GATHER_THREADS=64 (one wave per
     block, whole block staged in LDS; batches of <= 512 blocks in the
     single-pass fused kernel), 64u (the same with OKV_DECODE_FUSED=0: three
-    launches), 256 (LDS-staged value spans, the default for large blocks), and
-    64 / 256 with OKV_GATHER_STAGED=0 and no fusion (global windows): 64g, 256g."""
+    launches), 256 (LDS-staged value spans, the default for large blocks),
+    64 / 256 with OKV_GATHER_STAGED=0 and no fusion (global windows): 64g, 256g,
+    and 256 with the values produced by the address-ordered value sweep
+    (OKV_VALUE_SWEEP=1 / 2 tiles per workgroup): 256s, 256s2."""
     import os
     decs = {}
     try:
-        for w in ("64", "64u", "64g", "256", "256g"):
-            os.environ["OKV_GATHER_THREADS"] = w.rstrip("gu")
+        for w in ("64", "64u", "64g", "256", "256g", "256s", "256s2"):
+            os.environ["OKV_GATHER_THREADS"] = w[:3].rstrip("gus")
             os.environ["OKV_GATHER_STAGED"] = "0" if w.endswith("g") else "1"
             os.environ["OKV_DECODE_FUSED"] = "1" if w == "64" else "0"
+            os.environ["OKV_VALUE_SWEEP"] = {"256s": "1", "256s2": "2"}.get(w, "0")
             decs[w] = okv.Decoder(0)
     finally:
-        for k in ("OKV_GATHER_THREADS", "OKV_GATHER_STAGED", "OKV_DECODE_FUSED"):
+        for k in ("OKV_GATHER_THREADS", "OKV_GATHER_STAGED", "OKV_DECODE_FUSED",
+                  "OKV_VALUE_SWEEP"):
             os.environ.pop(k, None)
     yield decs
     for d in decs.values():
@@ -305,7 +309,7 @@ def _wide_segment(seed, nblk=120):
     return bytes(seg), np.array(descs, np.uint64).reshape(-1, 4)
 
 
-@pytest.mark.parametrize("width", ["256", "256g", "64", "64u", "64g"])
+@pytest.mark.parametrize("width", ["256", "256g", "256s", "256s2", "64", "64u", "64g"])
 def test_wide_spans_all_gathers(decoders_by_width, width):
     """Stage overflow (one-tile retry and global fallback), the segment's
     first and last bytes, odd block offsets: every gather vs the oracle."""
@@ -315,7 +319,7 @@ def test_wide_spans_all_gathers(decoders_by_width, width):
         _assert_same_as_oracle(got, seg, d, 0, False)
 
 
-@pytest.mark.parametrize("width", ["64", "64u", "64g", "256", "256g"])
+@pytest.mark.parametrize("width", ["64", "64u", "64g", "256", "256g", "256s", "256s2"])
 def test_mixed_blocks_both_gather_widths(decoders_by_width, width):
     """A segment mixing 4 KiB blocks, 64 KiB blocks with few rows and blocks
     over kRCap rows, through the 64- and the 256-thread gather."""
@@ -343,3 +347,91 @@ def test_single_tile_and_scan_paths(decoder, decoders_by_width, nblk):
     again = decoder.decode(seg, d)
     assert again.val_arena.tobytes() == outs[0].val_arena.tobytes()
     assert np.array_equal(again.row_start, outs[0].row_start)
+
+
+def _tiny_value_segment(seed, nblk=300):
+    """Blocks of <= 64 rows with 0-3 byte values: a 4 KiB value-sweep tile
+    holds thousands of rows (past the sweep's LDS row window)."""
+    rng = np.random.default_rng(seed)
+    seg, descs = bytearray(), []
+    for b in range(nblk):
+        body = bytearray()
+        for _ in range(int(rng.integers(0, 65))):
+            kl, vl = int(rng.integers(0, 9)), int(rng.integers(0, 4))
+            body += kl.to_bytes(2, "little") + vl.to_bytes(4, "little")
+            body += rng.integers(0, 256, kl + vl, dtype=np.uint8).tobytes()
+        off = len(seg) + int(rng.choice([0, 1, 7]))
+        seg += bytes(off - len(seg)) + body + bytes(int(rng.choice([0, 3, 100])))
+        descs.append((off, len(seg) - off, len(body), 0))
+    return bytes(seg), np.array(descs, np.uint64).reshape(-1, 4)
+
+
+@pytest.mark.parametrize("width", ["256s", "256s2"])
+def test_value_sweep(decoders_by_width, width):
+    """The value sweep vs the oracle: C3 blocks, wide spans, tiny values (row
+    window overflow), a fuzz of corrupt/truncated blocks (statuses with rows
+    of other blocks around them), and an undersized value arena (capacity:
+    the kernels fall back to the per-block gather on device)."""
+    dec = decoders_by_width[width]
+    w = okv.synth_segment(okv.sst.SYNTH_ZIPF, 7, nblocks=96, threshold=57344, block_size=65536)
+    seg, d = w.data(), w.descs()
+    _assert_same_as_oracle(dec.decode(seg, d), seg, d, 0, False)
+    for seed in (3, 4):
+        seg, d = _tiny_value_segment(seed)
+        _assert_same_as_oracle(dec.decode(seg, d), seg, d, 0, False)
+    rng = np.random.default_rng(77)
+    for trial in range(12):
+        seg = bytearray()
+        descs = []
+        for b in range(int(rng.integers(1, 40))):
+            body = bytearray()
+            for _ in range(int(rng.integers(0, 30))):
+                kl = int(rng.choice([0, 1, 5, 16, 100, 300]))
+                vl = int(rng.choice([0, 1, 7, 64, 500, 3000, 9000]))
+                body += kl.to_bytes(2, "little") + vl.to_bytes(4, "little")
+                body += rng.integers(0, 256, kl + vl, dtype=np.uint8).tobytes()
+            orig = len(body)
+            if rng.random() < 0.3 and body:
+                orig = int(rng.integers(0, len(body) + 1))
+            if rng.random() < 0.2 and len(body) > 3:
+                body[int(rng.integers(0, len(body)))] = int(rng.integers(0, 256))
+            bsize = len(body) + int(rng.choice([0, 1, 5, 64, 4096]))
+            off = len(seg) + int(rng.choice([0, 0, 1, 3, 8]))
+            seg += bytes(off - len(seg))
+            seg += body + bytes(bsize - len(body))
+            descs.append((off, bsize, orig, 0))
+        d = np.array(descs, np.uint64).reshape(-1, 4)
+        _assert_same_as_oracle(dec.decode(bytes(seg), d), bytes(seg), d, 0, False)
+    # device path with an undersized value arena: the blocks past it report
+    # OKV_BLK_CAPACITY (sweep unsafe: the per-block gather runs), the blocks
+    # before it match the oracle
+    import torch
+    w = okv.synth_segment(okv.sst.SYNTH_ZIPF, 8, nblocks=64, threshold=57344, block_size=65536)
+    seg, d = w.data(), w.descs()[:64]
+    ref = dec.decode(seg, d)
+    dev = torch.device("cuda", 0)
+    seg_t = torch.from_numpy(seg).to(dev)
+    d_t = torch.from_numpy(d.view(np.int64)).to(dev)
+    rows, kb, vb = dec.plan_device(seg_t, seg.size, d_t, 64)
+    out = dict(row_start=torch.zeros(65, dtype=torch.int64, device=dev),
+               key_base=torch.zeros(64, dtype=torch.int64, device=dev),
+               val_base=torch.zeros(64, dtype=torch.int64, device=dev),
+               status=torch.zeros(64, dtype=torch.int32, device=dev),
+               key_off=torch.zeros(rows, dtype=torch.int64, device=dev),
+               key_len=torch.zeros(rows, dtype=torch.int16, device=dev),
+               val_off=torch.zeros(rows, dtype=torch.int64, device=dev),
+               val_len=torch.zeros(rows, dtype=torch.int32, device=dev),
+               key_arena=torch.zeros(kb, dtype=torch.uint8, device=dev),
+               val_arena=torch.zeros(vb // 2, dtype=torch.uint8, device=dev))
+    with pytest.raises(Exception):
+        dec.decode_device(seg_t, seg.size, d_t, 64, out, sync=True)
+    st = out["status"].cpu().numpy()
+    assert (st != 0).any() and (st == 0).any()
+    arena = out["val_arena"].cpu().numpy()
+    vbase = ref.val_base
+    for b in range(64):
+        if st[b] != 0:
+            continue
+        lo = int(vbase[b])
+        hi = int(vbase[b + 1]) if b + 1 < 64 else vb
+        assert arena[lo:hi].tobytes() == ref.val_arena[lo:hi].tobytes()

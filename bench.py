@@ -899,12 +899,15 @@ def cpu_compact_baseline(args, segs, n, per_block, th, bs, K):
     out_rows = {}
 
     def once(nth):
-        out_rows[nth], _ob = coracle.compact_go(host, th, bs, nth)
+        out_rows[nth] = coracle.compact_go(host, th, bs, nth)
         return in_b * nth
     res = sweep(once, args.cpu_seconds / len(thread_counts()))
+    n_out, ob = out_rows[1]
+    q1 = ("; Go's Close panics after the last WriteRow flushes (SURVEY Q1): the rows are "
+          "written first and counted" if n_out and not ob else "")
     return sweep_summary(res, 1 / 2**30, "GiB/s", "port",
                          f"{len(host)} segments' blocks holding rows [{x0}, {x0 + m}) "
-                         f"({in_b} B in, {out_rows[1]} rows out) per compaction, one "
+                         f"({in_b} B in, {n_out} rows merged and written{q1}) per compaction, one "
                          f"independent compaction per thread; C restatement: "
                          f"ReadBlockWithStat per block, newest-wins merge, Go writer (the "
                          f"reference's compactor is a stub)")

@@ -25,9 +25,6 @@
 //   4. okv_copy_kernel   -- persistent, over the big-block list only: stages
 //      the block in LDS and chases its headers there (rare: > kRCap rows).
 // OKV_F_INDEX_ONLY writes spans into seg instead of arenas (3 + okv_index_kernel).
-// OKV_VALUE_SWEEP=1|2|4 (measured alternative): pass 3 as
-// okv_rows_kernel (row index, keys, hand-off) + okv_value_sweep_kernel (the
-// value arena in address order, one-shot 4 KiB tiles).
 // Measured alternatives to pass 3 (LDS-DMA staging, pipelined loader/gatherer,
 // persistent streaming, tile-major, ...) are in DESIGN.md §4; all slower.
 #include <hip/hip_runtime.h>

@@ -1657,65 +1657,55 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
         }
         __syncthreads();
         PMARK(1);
-        // each byte's immediate source (eight bytes per lane per step: the map and
-        // record reads of a step are all issued before any is used)
-        for (uint32_t x0 = lane; x0 < osum; x0 += 64 * 8) {
+        // each byte's source, resolved to a terminal (a literal or output before
+        // the chunk) in byte order, 64 bytes (one per lane) at a time: a source
+        // before the group is already terminal, one read; a source inside the
+        // group (match offset < 64) is resolved by pointer jumping within the
+        // group.  Eight groups' immediate sources are computed first (their map
+        // and record reads all in flight); LDS operations of one wave complete
+        // in order, so each group sees the previous groups' writes.
+        uint32_t rounds = 0;
+        for (uint32_t x0 = 0; x0 < osum; x0 += 64 * 8) {
           uint32_t kk[8];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            const uint32_t x = x0 + 64 * u;
+            const uint32_t x = x0 + 64 * u + lane;
             kk[u] = x < osum ? map[x] : 0;
           }
           uint4 R[8];
 #pragma unroll
           for (int u = 0; u < 8; ++u) R[u] = rec[kk[u]];
+          uint32_t sv[8];
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            const uint32_t x = x0 + 64 * u;
+            const uint32_t x = x0 + 64 * u + lane;
             const uint32_t in = x - R[u].x;
-            uint32_t sv;
             if (in < R[u].y) {
-              sv = zst::kTerm | zst::kLit | (lp + R[u].w + in);
+              sv[u] = zst::kTerm | zst::kLit | (lp + R[u].w + in);
             } else {
               const uint32_t t = in - R[u].y, off = R[u].z;
               const uint32_t mo = t < off ? t : t % off;
               const int32_t sx = int32_t(R[u].x + R[u].y + mo) - int32_t(off);
-              sv = sx < 0 ? (zst::kTerm | uint32_t(int32_t(O) + sx)) : uint32_t(sx);
+              sv[u] = sx < 0 ? (zst::kTerm | uint32_t(int32_t(O) + sx)) : uint32_t(sx);
             }
-            if (x < osum) srcx[x] = sv;
+            if (x >= osum) sv[u] = zst::kTerm;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const uint32_t g0 = x0 + 64 * u;
+            if (g0 >= osum) break;
+            const uint32_t x = g0 + lane;
+            if (!(sv[u] & zst::kTerm) && sv[u] < g0) sv[u] = srcx[sv[u]];
+            if (x < osum) srcx[x] = sv[u];
+            while (__any(!(sv[u] & zst::kTerm))) {
+              if (!(sv[u] & zst::kTerm)) sv[u] = srcx[sv[u]];
+              if (x < osum) srcx[x] = sv[u];
+              ++rounds;
+            }
           }
         }
         __syncthreads();
         PMARK(2);
-        uint32_t rounds = 0;
-        // pointer jumping until every byte names a terminal source; a step reads
-        // eight entries, then their targets, then writes (in place: any value
-        // read is an ancestor or a terminal, and sources lie before the byte)
-        for (;;) {
-          bool more = false;
-          for (uint32_t x0 = lane; x0 < osum; x0 += 64 * 8) {
-            uint32_t sv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const uint32_t x = x0 + 64 * u;
-              sv[u] = x < osum ? srcx[x] : zst::kTerm;
-            }
-            uint32_t nv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) nv[u] = (sv[u] & zst::kTerm) ? sv[u] : srcx[sv[u]];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const uint32_t x = x0 + 64 * u;
-              if (!(sv[u] & zst::kTerm)) {
-                srcx[x] = nv[u];
-                more |= !(nv[u] & zst::kTerm);
-              }
-            }
-          }
-          ++rounds;
-          if (!__any(more)) break;
-        }
-        __syncthreads();
         PMARK(3);
         pacc[8] += rounds;
         // gather: lanes own aligned output dwords (four per lane per step, 16

@@ -852,25 +852,17 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       const uint32_t ml = (mls < 32 ? mls + 3 : ML_BASE[mls]) + mlx;
       const uint32_t ll = (lls < 16 ? lls : LL_BASE[lls]) + seqbits_take(br, fse_xb(ell));
       // repeat offsets (3.1.1.5), as libzstd's ZSTD_decodeSequence
-      uint32_t off;
-      if (ofv > 3) {
-        off = ofv - 3;
-        rep2 = rep1;
-        rep1 = rep0;
-        rep0 = off;
-      } else {
-        const uint32_t idx = ofv - 1 + (ll == 0 ? 1 : 0);  // 0..3
-        if (idx == 0) {
-          off = rep0;
-        } else {
-          uint32_t t = idx == 3 ? rep0 - 1 : (idx == 1 ? rep1 : rep2);
-          t += t == 0;  // libzstd: offset 0 is corrupt input, forced to 1
-          if (idx != 1) rep2 = rep1;
-          rep1 = rep0;
-          rep0 = t;
-          off = t;
-        }
-      }
+      // repeat offsets (RFC 8878 3.1.1.5), branch-free: ofv > 3 is a new
+      // offset; else idx = ofv - 1 (+1 when ll == 0) picks rep0/rep1/rep2/rep0-1
+      const bool fresh = ofv > 3;
+      const uint32_t idx = ofv - 1 + (ll == 0 ? 1u : 0u);  // 0..3 when !fresh
+      uint32_t t = idx == 3 ? rep0 - 1 : (idx == 1 ? rep1 : rep2);
+      t += t == 0;  // libzstd: offset 0 is corrupt input, forced to 1
+      const uint32_t off = fresh ? ofv - 3 : (idx == 0 ? rep0 : t);
+      const bool sh1 = fresh || idx != 0, sh2 = fresh || idx >= 2;
+      rep2 = sh2 ? rep1 : rep2;
+      rep1 = sh1 ? rep0 : rep1;
+      rep0 = sh1 ? off : rep0;
       if (i + 1 < nseq) {  // state updates: literals length, match length, offset
         sll = fse_base(ell) + seqbits_take(br, fse_nb(ell));
         sml = fse_base(eml) + seqbits_take(br, fse_nb(eml));
@@ -1336,14 +1328,15 @@ __device__ __forceinline__ uint32_t lb_raw(const LaneBits& b, int32_t d) {
   // a global (not flat) load: it counts in vmcnt only, so LDS waits do not drain it
   return *(const __attribute__((address_space(1))) uint32_t*)(b.ab + 4 * dc);
 }
-// Bytes of dword d outside the stream [s0, s0 + n) read as 0.
+// Bytes of dword d outside the stream [s0, s0 + n) read as 0 (branch-free:
+// lanes are different blocks, so branches would diverge).
 __device__ __forceinline__ uint32_t lb_fix(const LaneBits& b, uint32_t v, int32_t d) {
   const int32_t lo = 4 * d;
-  if (d < 0 || lo >= b.s0 + b.n) return 0;
-  if (lo < b.s0) v &= 0xffffffffu << (8 * (b.s0 - lo));
-  const int32_t hi = b.s0 + b.n - lo;
-  if (hi < 4) v &= (1u << (8 * hi)) - 1;
-  return v;
+  const int32_t cut = min(max(b.s0 - lo, 0), 4);        // bytes below the stream
+  const int32_t keep = min(max(b.s0 + b.n - lo, 0), 4);  // bytes up to the stream end
+  const uint32_t mlo = cut >= 4 ? 0u : (0xffffffffu << (8 * cut));
+  const uint32_t mhi = keep >= 4 ? 0xffffffffu : ((1u << (8 * keep)) - 1u);
+  return v & mlo & mhi;
 }
 __device__ __forceinline__ uint32_t lb_dw(const LaneBits& b, int32_t d) {
   return lb_fix(b, lb_raw(b, d), d);
@@ -1380,17 +1373,18 @@ __device__ __forceinline__ void wb_issue(WinBits& w) {
   w.l1 = lb_raw(w.f, w.wd - 2);
   w.l2 = lb_raw(w.f, w.wd - 3);
 }
+// k <= 31 bits at window bit pos: the two dwords around it (selects, no
+// branches) and one funnel shift.
 __device__ __forceinline__ uint32_t wb_take(WinBits& w, uint32_t k) {
   w.f.P -= int32_t(k);
   const uint32_t pos = uint32_t(w.f.P - 32 * w.wd);  // 0 .. 128 - k
-  uint64_t v;
-  if (pos >= 64) {
-    v = w.hi >> (pos - 64);
-  } else {
-    v = w.lo >> pos;
-    if (pos) v |= w.hi << (64 - pos);
-  }
-  return uint32_t(v) & uint32_t((uint64_t(1) << k) - 1);
+  const uint32_t i = pos >> 5;
+  const uint32_t w0 = uint32_t(w.lo), w1 = uint32_t(w.lo >> 32), w2 = uint32_t(w.hi),
+                 w3 = uint32_t(w.hi >> 32);
+  const uint32_t a = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
+  const uint32_t c = i == 0 ? w1 : i == 1 ? w2 : i == 2 ? w3 : 0u;
+  const uint32_t v = __builtin_amdgcn_alignbit(c, a, pos & 31u);
+  return v & ((1u << k) - 1u);
 }
 // Slide the window down so its top dword holds bit P - 1; by 0..3 dwords.
 __device__ __forceinline__ void wb_slide(WinBits& w) {
@@ -1478,25 +1472,17 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
       const uint32_t llx = zst::wb_take(br, zst::fse_xb(ell));
       const uint32_t ml = mlb[zst::fse_sym(eml)] + mlx;
       const uint32_t ll = llb[zst::fse_sym(ell)] + llx;
-      uint32_t off;
-      if (ofv > 3) {
-        off = ofv - 3;
-        rep2 = rep1;
-        rep1 = rep0;
-        rep0 = off;
-      } else {
-        const uint32_t idx = ofv - 1 + (ll == 0 ? 1 : 0);  // 0..3
-        if (idx == 0) {
-          off = rep0;
-        } else {
-          uint32_t t = idx == 3 ? rep0 - 1 : (idx == 1 ? rep1 : rep2);
-          t += t == 0;  // libzstd: offset 0 is corrupt input, forced to 1
-          if (idx != 1) rep2 = rep1;
-          rep1 = rep0;
-          rep0 = t;
-          off = t;
-        }
-      }
+      // repeat offsets (RFC 8878 3.1.1.5), branch-free: ofv > 3 is a new
+      // offset; else idx = ofv - 1 (+1 when ll == 0) picks rep0/rep1/rep2/rep0-1
+      const bool fresh = ofv > 3;
+      const uint32_t idx = ofv - 1 + (ll == 0 ? 1u : 0u);  // 0..3 when !fresh
+      uint32_t t = idx == 3 ? rep0 - 1 : (idx == 1 ? rep1 : rep2);
+      t += t == 0;  // libzstd: offset 0 is corrupt input, forced to 1
+      const uint32_t off = fresh ? ofv - 3 : (idx == 0 ? rep0 : t);
+      const bool sh1 = fresh || idx != 0, sh2 = fresh || idx >= 2;
+      rep2 = sh2 ? rep1 : rep2;
+      rep1 = sh1 ? rep0 : rep1;
+      rep0 = sh1 ? off : rep0;
       if (i + 1 < z.nseq) {  // state updates: literals length, match length, offset
         sll = zst::fse_base(ell) + zst::wb_take(br, zst::fse_nb(ell));
         sml = zst::fse_base(eml) + zst::wb_take(br, zst::fse_nb(eml));

@@ -397,18 +397,46 @@ __device__ int32_t read_huf_tree(SmemCore& sm, const uint8_t* p, int64_t n, uint
   return used;
 }
 
-// Decode one Huffman stream of `cnt` literals into out (this lane only).
+// Decode one Huffman stream of `cnt` literals into out (this lane only).  The
+// stream is read backward as aligned dwords: a 64-bit container plus eight
+// dwords prefetched below it, so a refill rarely waits on memory (a literal
+// takes <= 11 bits; a fresh load per container refill made the decode a chain
+// of memory round trips).  Bits below the stream read as 0 (RFC 8878 4.2.1.2).
 __device__ bool huf_stream(const SmemCore& sm, uint32_t mb, const uint8_t* p, int64_t n, uint8_t* out,
                            uint32_t cnt) {
-  BitR br;
-  if (!bitr_init(br, p, n)) return cnt == 0 && n == 0;
+  if (n <= 0) return cnt == 0 && n == 0;
+  const uint32_t last = p[n - 1];
+  if (last == 0) return false;  // the final byte holds the end marker
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* ab = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  const int32_t s0 = int32_t(a & 3), B0 = 8 * s0;  // the stream's bit 0, relative to ab
+  int32_t P = B0 + int32_t(n - 1) * 8 + (31 - __builtin_clz(last));
+  int32_t cd = (P >> 5) - 1;  // the container holds dwords cd + 1 : cd
+  auto raw = [&](int32_t d) { return ab[d < 0 ? 0 : d]; };
+  auto fix = [&](uint32_t v, int32_t d) {  // bytes below the stream read as 0
+    const int32_t cut = min(max(s0 - 4 * d, 0), 4);
+    return cut >= 4 ? 0u : (v & (0xffffffffu << (8 * cut)));
+  };
+  uint64_t c = (uint64_t(fix(raw(cd + 1), cd + 1)) << 32) | fix(raw(cd), cd);
+  uint32_t r[8];  // raw dwords cd - 1 - k
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = raw(cd - 1 - k);
   for (uint32_t i = 0; i < cnt; ++i) {
-    const uint32_t idx = bitr_peek(br, mb);
+    // invariant: 32 cd <= P < 32 cd + 64; a literal takes <= mb <= 11 bits
+    if (P - int32_t(mb) < 32 * cd) {
+      c = (c << 32) | fix(r[0], cd - 1);
+      --cd;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) r[k] = r[k + 1];
+      r[7] = raw(cd - 8);
+    }
+    const int32_t p0 = P - int32_t(mb);
+    const uint32_t idx = uint32_t(c >> uint32_t(p0 - 32 * cd)) & ((1u << mb) - 1u);
     const uint32_t e = sm.huf[idx];
     out[i] = uint8_t(e & 0xff);
-    bitr_skip(br, e >> 8);
+    P -= int32_t(e >> 8);
   }
-  return br.pos == 0;
+  return P == B0;
 }
 
 // ---- one zstd block -----------------------------------------------------------

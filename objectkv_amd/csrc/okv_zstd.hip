@@ -1419,8 +1419,13 @@ __device__ __forceinline__ void wb_slide(WinBits& w) {
   const int32_t dtop = ((w.f.P + 31) >> 5) - 1;
   int32_t sft = w.wd + 3 - dtop;
   sft = sft < 0 ? 0 : (sft > 3 ? 3 : sft);
-  const uint32_t c0 = lb_fix(w.f, w.l2, w.wd - 3), c1 = lb_fix(w.f, w.l1, w.wd - 2),
-                 c2 = lb_fix(w.f, w.l0, w.wd - 1);
+  // dwords below the window only meet the stream's low end (its top was
+  // masked when the window was filled): clear the bytes below s0
+  auto low = [&](uint32_t v, int32_t d) {
+    const int32_t cut = min(max(w.f.s0 - 4 * d, 0), 4);
+    return cut >= 4 ? 0u : (v & (0xffffffffu << (8 * cut)));
+  };
+  const uint32_t c0 = low(w.l2, w.wd - 3), c1 = low(w.l1, w.wd - 2), c2 = low(w.l0, w.wd - 1);
   const uint32_t w0 = uint32_t(w.lo), w1 = uint32_t(w.lo >> 32), w2 = uint32_t(w.hi),
                  w3 = uint32_t(w.hi >> 32);
   // C = [c0 c1 c2 w0 w1 w2 w3]; new window k = C[k + 3 - sft]

@@ -1570,14 +1570,25 @@ namespace zst {
 constexpr uint32_t kTerm = 0x80000000u, kLit = 0x40000000u, kIdx = 0x3fffffffu;
 }
 
+// Executor chunk: output bytes covered by one byte map (kEU 16-byte map
+// pieces per lane).  2 KiB keeps the workgroup at 14 KiB of LDS.
+#ifndef OKV_ZSTD_EXEC_OUT
+#define OKV_ZSTD_EXEC_OUT 2048
+#endif
+constexpr uint32_t kExecOut = OKV_ZSTD_EXEC_OUT;
+constexpr int kEU = int(kExecOut / 1024);
+static_assert(kExecOut <= zst::kChunkOut && kExecOut % 1024 == 0, "exec chunk");
+// Executor grid (blocks are strided over it); the profiling slots are sized
+// for the largest grid.
+constexpr uint32_t kExecGridMax = 16384;
 __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
     const zst::ZBlk* __restrict__ zb, uint32_t nblk, const uint64_t* __restrict__ seq_off,
     const uint64_t* __restrict__ seqs, const uint64_t* __restrict__ cap_off,
     uint8_t* __restrict__ dec, uint64_t* __restrict__ dec_len, int32_t* __restrict__ zstatus,
     unsigned long long* __restrict__ prof) {
   __shared__ uint4 rec[zst::kSeqChunk + 1];
-  __shared__ uint32_t srcx[zst::kChunkOut];
-  __shared__ uint8_t map[zst::kChunkOut];
+  __shared__ uint32_t srcx[kExecOut];
+  __shared__ uint8_t map[kExecOut];
   const int lane = threadIdx.x & 63;
   unsigned long long pacc[10] = {};
   for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
@@ -1624,7 +1635,7 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
         rec[k] = make_uint4(opx, ll[u], of[u], lpx);
         lpx += ll[u];
         opx += ll[u] + ml[u];
-        fit += (k < nrem && opx <= zst::kChunkOut) ? 1u : 0u;
+        fit += (k < nrem && opx <= kExecOut) ? 1u : 0u;
       }
       if (lane == 63) rec[256] = make_uint4(opx, 0, 0, lpx);
       for (int d = 32; d; d >>= 1) fit += __shfl_xor(fit, d, 64);
@@ -1636,15 +1647,15 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
         // byte -> sequence map: markers, then a running max
         uint4* m4 = reinterpret_cast<uint4*>(map);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) m4[4 * lane + u] = make_uint4(0, 0, 0, 0);
+        for (int u = 0; u < kEU; ++u) m4[kEU * lane + u] = make_uint4(0, 0, 0, 0);
         __syncthreads();
         for (uint32_t k = lane + 1; k < cnt; k += 64) map[rec[k].x] = uint8_t(k);
         __syncthreads();
-        uint4 v[4];
+        uint4 v[kEU];
         uint32_t mx = 0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          v[u] = m4[4 * lane + u];
+        for (int u = 0; u < kEU; ++u) {
+          v[u] = m4[kEU * lane + u];
           const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
           for (int q = 0; q < 4; ++q)
@@ -1660,7 +1671,7 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
         run = __shfl_up(run, 1, 64);
         if (lane == 0) run = 0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < kEU; ++u) {
           uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -1672,7 +1683,7 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
             }
             w4[q] = outw;
           }
-          m4[4 * lane + u] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+          m4[kEU * lane + u] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
         }
         __syncthreads();
         PMARK(1);
@@ -1924,9 +1935,9 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
   static unsigned long long* eprof_buf = nullptr;
   unsigned long long* eprof = nullptr;
   if (prof) {
-    if (!eprof_buf) (void)hipMalloc(&eprof_buf, 16 * 8 * 4096);
+    if (!eprof_buf) (void)hipMalloc(&eprof_buf, 16 * 8 * kExecGridMax);
     eprof = eprof_buf;
-    (void)hipMemsetAsync(eprof, 0, 16 * 8 * 4096, s);
+    (void)hipMemsetAsync(eprof, 0, 16 * 8 * kExecGridMax, s);
   }
   if (!general) {
     if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_zb), &ctx->z_cap_zb,
@@ -1941,7 +1952,10 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
                    (size_t(nblk) + 1) * 8)))
       return rc;
     zb = reinterpret_cast<zst::ZBlk*>(ctx->z_zb);
-    hipLaunchKernelGGL(okv_zstd_pro_kernel, dim3(std::min<uint32_t>(nblk, 4096)), dim3(64), 0, s,
+    // one workgroup per block (no per-workgroup scratch; OKV_ZSTD_PRO_GRID: A/B)
+    const uint32_t pgrid = getenv("OKV_ZSTD_PRO_GRID") ? uint32_t(atoi(getenv("OKV_ZSTD_PRO_GRID")))
+                                                       : nblk;
+    hipLaunchKernelGGL(okv_zstd_pro_kernel, dim3(std::max(1u, std::min(nblk, pgrid))), dim3(64), 0, s,
                        seg, seg_bytes, descs, nblk, ctx->z_cap_off, ctx->z_dec, ctx->z_dec_len,
                        ctx->z_status, ctx->z_blit, ctx->z_tabs, zb);
     hipLaunchKernelGGL(okv_zstd_seqoff_kernel, dim3(1), dim3(1024), 0, s, zb, nblk,
@@ -1956,8 +1970,13 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
     hipLaunchKernelGGL(okv_zstd_seq_kernel, dim3((nblk + 63) / 64), dim3(64), 0, s, zb, nblk,
                        ctx->z_tabs, ctx->z_seq_off, ctx->z_seqs);
     if (prof) (void)hipEventRecord(ev[2], s);
-    const uint32_t egrid = std::min<uint32_t>(
-        4096, getenv("OKV_ZSTD_EXEC_GRID") ? atoi(getenv("OKV_ZSTD_EXEC_GRID")) : 1536);
+    // one workgroup per block by default: the dispatcher balances blocks of
+    // unequal work better than a grid-stride loop (16 384 x 64 KiB: 3.8 ms vs
+    // 4.6 ms at 4096 workgroups, 5.6 at 2816); profiling caps it at its slots
+    uint32_t egrid = getenv("OKV_ZSTD_EXEC_GRID") ? uint32_t(atoi(getenv("OKV_ZSTD_EXEC_GRID")))
+                                                  : nblk;
+    if (prof) egrid = std::min(egrid, kExecGridMax);
+    egrid = std::max(egrid, 1u);
     hipLaunchKernelGGL(okv_zstd_exec_kernel, dim3(std::min<uint32_t>(nblk, egrid)), dim3(64), 0, s,
                        zb, nblk, ctx->z_seq_off, ctx->z_seqs, ctx->z_cap_off, ctx->z_dec,
                        ctx->z_dec_len, ctx->z_status, eprof);
@@ -1982,10 +2001,10 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
             nblk, t[0], t[1], t[2], t[3]);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
-    static unsigned long long hs[16 * 4096];
+    static unsigned long long hs[16 * kExecGridMax];
     (void)hipMemcpy(hs, eprof, sizeof(hs), hipMemcpyDeviceToHost);
     unsigned long long h[16] = {};
-    for (int w = 0; w < 4096; ++w)
+    for (uint32_t w = 0; w < kExecGridMax; ++w)
       for (int k = 0; k < 16; ++k) h[k] += hs[w * 16 + k];
     const double c = h[9] ? double(h[9]) : 1.0;
     fprintf(stderr,

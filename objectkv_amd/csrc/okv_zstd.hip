@@ -1516,10 +1516,14 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
       rep2 = sh2 ? rep1 : rep2;
       rep1 = sh1 ? rep0 : rep1;
       rep0 = sh1 ? off : rep0;
-      if (i + 1 < z.nseq) {  // state updates: literals length, match length, offset
-        sll = zst::fse_base(ell) + zst::wb_take(br, zst::fse_nb(ell));
-        sml = zst::fse_base(eml) + zst::wb_take(br, zst::fse_nb(eml));
-        sof = zst::fse_base(eof) + zst::wb_take(br, zst::fse_nb(eof));
+      if (i + 1 < z.nseq) {  // state updates: literals length, match length, offset --
+        // read in that order, so one take of all three (<= 9 + 9 + 8 bits) holds
+        // them high to low
+        const uint32_t nl = zst::fse_nb(ell), nm = zst::fse_nb(eml), no = zst::fse_nb(eof);
+        const uint32_t v = zst::wb_take(br, nl + nm + no);
+        sll = zst::fse_base(ell) + (v >> (nm + no));
+        sml = zst::fse_base(eml) + ((v >> no) & ((1u << nm) - 1u));
+        sof = zst::fse_base(eof) + (v & ((1u << no) - 1u));
       }
       zst::wb_slide(br);
       // execution checks (3.1.1.4), in the general kernel's order

@@ -1581,6 +1581,14 @@ constexpr uint32_t kTerm = 0x80000000u, kLit = 0x40000000u, kIdx = 0x3fffffffu;
 #endif
 constexpr uint32_t kExecOut = OKV_ZSTD_EXEC_OUT;
 constexpr int kEU = int(kExecOut / 1024);
+#ifndef OKV_ZSTD_GQ
+#define OKV_ZSTD_GQ 4
+#endif
+#ifndef OKV_ZSTD_GB
+#define OKV_ZSTD_GB 8
+#endif
+constexpr int kGQ = OKV_ZSTD_GQ;  // gather: output dwords per lane per step
+constexpr int kGB = OKV_ZSTD_GB;  // source resolution: 64-byte groups per batch
 static_assert(kExecOut <= zst::kChunkOut && kExecOut % 1024 == 0, "exec chunk");
 // Executor grid (blocks are strided over it); the profiling slots are sized
 // for the largest grid.
@@ -1699,19 +1707,19 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
         // and record reads all in flight); LDS operations of one wave complete
         // in order, so each group sees the previous groups' writes.
         uint32_t rounds = 0;
-        for (uint32_t x0 = 0; x0 < osum; x0 += 64 * 8) {
-          uint32_t kk[8];
+        for (uint32_t x0 = 0; x0 < osum; x0 += 64 * kGB) {
+          uint32_t kk[kGB];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < kGB; ++u) {
             const uint32_t x = x0 + 64 * u + lane;
             kk[u] = x < osum ? map[x] : 0;
           }
-          uint4 R[8];
+          uint4 R[kGB];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) R[u] = rec[kk[u]];
-          uint32_t sv[8];
+          for (int u = 0; u < kGB; ++u) R[u] = rec[kk[u]];
+          uint32_t sv[kGB];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < kGB; ++u) {
             const uint32_t x = x0 + 64 * u + lane;
             const uint32_t in = x - R[u].x;
             if (in < R[u].y) {
@@ -1725,7 +1733,7 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
             if (x >= osum) sv[u] = zst::kTerm;
           }
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < kGB; ++u) {
             const uint32_t g0 = x0 + 64 * u;
             if (g0 >= osum) break;
             const uint32_t x = g0 + lane;
@@ -1747,11 +1755,11 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
         // re-read from the previous chunk's output; tail bytes past the chunk
         // are written as 0 and overwritten by the next chunk the same way.
         const uint32_t g0 = O >> 2, g1 = (O + osum + 3) >> 2;
-        for (uint32_t gb = g0 + lane; gb < g1; gb += 64 * 4) {
-          const uint8_t* ptr[16];
-          uint32_t spec[16];  // 0 load, 1 RLE literal, 2 zero
+        for (uint32_t gb = g0 + lane; gb < g1; gb += 64 * kGQ) {
+          const uint8_t* ptr[4 * kGQ];
+          uint32_t spec[4 * kGQ];  // 0 load, 1 RLE literal, 2 zero
 #pragma unroll
-          for (int u = 0; u < 16; ++u) {
+          for (int u = 0; u < 4 * kGQ; ++u) {
             const uint32_t g = gb + 64 * (u >> 2);
             const uint32_t a = 4 * g + (u & 3);
             const uint32_t x = a - O;
@@ -1762,11 +1770,11 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
             spec[u] = (g >= g1 || (a >= O && !in)) ? 2u : ((lit && rle) ? 1u : 0u);
             ptr[u] = spec[u] ? out : (!in ? out + a : (lit ? lits + idx : out + idx));
           }
-          uint32_t bv[16];
+          uint32_t bv[4 * kGQ];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) bv[u] = *ptr[u];
+          for (int u = 0; u < 4 * kGQ; ++u) bv[u] = *ptr[u];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < kGQ; ++q) {
             const uint32_t g = gb + 64 * q;
             uint32_t w = 0;
 #pragma unroll
@@ -1783,11 +1791,11 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
         // sequence's literals or on output before it; stored as aligned dwords
         const uint4 R = rec[0];
         const uint32_t g0 = O >> 2, g1 = (O + osum + 3) >> 2;
-        for (uint32_t gb = g0 + lane; gb < g1; gb += 64 * 4) {
-          const uint8_t* ptr[16];
-          uint32_t spec[16];
+        for (uint32_t gb = g0 + lane; gb < g1; gb += 64 * kGQ) {
+          const uint8_t* ptr[4 * kGQ];
+          uint32_t spec[4 * kGQ];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) {
+          for (int u = 0; u < 4 * kGQ; ++u) {
             const uint32_t g = gb + 64 * (u >> 2);
             const uint32_t a = 4 * g + (u & 3);
             const uint32_t x = a - O;
@@ -1805,11 +1813,11 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
                              : (!in ? out + a
                                     : (sx >= 0 ? lits + lp + uint32_t(sx) : out + (int32_t(O) + sx)));
           }
-          uint32_t bv[16];
+          uint32_t bv[4 * kGQ];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) bv[u] = *ptr[u];
+          for (int u = 0; u < 4 * kGQ; ++u) bv[u] = *ptr[u];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < kGQ; ++q) {
             const uint32_t g = gb + 64 * q;
             uint32_t w = 0;
 #pragma unroll
@@ -1836,11 +1844,11 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
     {
       const uint32_t tl = lit_total - lp;
       const uint32_t g0 = O >> 2, g1 = (O + tl + 3) >> 2;
-      for (uint32_t gb = g0 + lane; gb < g1; gb += 64 * 4) {
-        uint32_t bv[16];
-        uint32_t spec[16];
+      for (uint32_t gb = g0 + lane; gb < g1; gb += 64 * kGQ) {
+        uint32_t bv[4 * kGQ];
+        uint32_t spec[4 * kGQ];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
+        for (int u = 0; u < 4 * kGQ; ++u) {
           const uint32_t g = gb + 64 * (u >> 2);
           const uint32_t a = 4 * g + (u & 3);
           const bool in = g < g1 && a >= O && a - O < tl;
@@ -1849,7 +1857,7 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
           bv[u] = *ptr;
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < kGQ; ++q) {
           const uint32_t g = gb + 64 * q;
           uint32_t w = 0;
 #pragma unroll

@@ -149,9 +149,11 @@ def pmc_traffic(config, mode, kernel, sources=DECODE_SOURCES):
         d = json.load(f)
     if d.get("source_sha") != source_sha(sources):
         return None, "stale (kernel sources changed since the PMC run)"
-    for name, k in d.get("kernels", {}).items():
-        if kernel in name:
-            return k["hbm_bytes"], os.path.relpath(path, ROOT)
+    names = (kernel,) if isinstance(kernel, str) else tuple(kernel)
+    hits = [k["hbm_bytes"] for name, k in d.get("kernels", {}).items()
+            if any(n in name for n in names)]
+    if hits:  # per launch, summed over the kernels of the pass
+        return sum(hits), os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -456,15 +458,19 @@ def run_decode(args, torch, okv, D):
         # read OriginalSize per block; write payload (padded arenas) + 22 B/row
         # SoA (u64 key_off, u16 key_len, u64 val_off, u32 val_len) + 28 B/block
         alg = orig_bytes + payload + rows * 22 + nblk * 28
+        sweep = os.environ.get("OKV_VALUE_SWEEP", "6") not in ("0", "") and \
+            os.environ.get("OKV_GATHER_STAGED", "1") != "0"
         roof_kernel = ("okv_decode_fused_kernel (passes 1-3) + okv_copy_kernel"
                        if nblk <= 512 and in_bytes / max(nblk, 1) <= 16384 else
                        "okv_gather_small_kernel + okv_copy_kernel"
                        if in_bytes / max(nblk, 1) <= 16384 else
+                       "okv_rows_kernel + okv_value_sweep_kernel + okv_gather_staged_kernel "
+                       "(exits: the sweep was safe) + okv_copy_kernel" if sweep else
                        "okv_gather_staged_kernel + okv_copy_kernel")
         roof_ms = ms["copy"]
     achieved = alg / (roof_ms * 1e-3) / 1e9
-    traffic, traffic_src = (None, None) if comp else pmc_traffic(args.config, args.mode,
-                                                                 roof_kernel.split()[0])
+    pass3 = tuple(w for w in roof_kernel.replace("(", " ").split() if w.startswith("okv_"))
+    traffic, traffic_src = (None, None) if comp else pmc_traffic(args.config, args.mode, pass3)
 
     # ---- CPU baseline (rank 0, N = 1 only) ---------------------------------------
     cpu = None

@@ -570,7 +570,9 @@ __global__ __launch_bounds__(NT) void okv_gather_kernel(CopyParams P) {
 // blocks, capacity) it gathers the values itself.
 __global__ __launch_bounds__(64) void okv_rows_kernel(CopyParams P) {
   __shared__ GatherSmem sm;
-  const bool sweep = sweep_safe(*P.tot, *P.big_count, P.row_cap, P.key_cap, P.val_cap);
+  // unsafe for the sweep (big blocks, capacity): okv_gather_staged_kernel,
+  // launched after the sweep, does the whole pass instead
+  if (!sweep_safe(*P.tot, *P.big_count, P.row_cap, P.key_cap, P.val_cap)) return;
   for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
     // record positions and headers with the metadata (one trip; the slots
     // exist for every block, only the first `rows` are meaningful)
@@ -590,14 +592,10 @@ __global__ __launch_bounds__(64) void okv_rows_kernel(CopyParams P) {
       }
       __syncthreads();
       write_row_index(P, sm, m, rows);
-      const uint4 bc = sweep ? boundary_chunk(P, sm, m, rows) : make_uint4(0, 0, 0, 0);
+      const uint4 bc = boundary_chunk(P, sm, m, rows);
       gather_tiles<false, GlobalWin, 1>(src, sm, rows, P.key_arena, m.B.kb0, 0,
                                         (sm.kpre[rows] + 1023) >> 10, 1);
-      if (sweep)
-        sweep_handoff(P, sm, m, rows, bc);
-      else
-        gather_tiles<true, GlobalWin, 1>(src, sm, rows, P.val_arena, m.B.vb0, 0,
-                                         (sm.vpre[rows] + 1023) >> 10, 1);
+      sweep_handoff(P, sm, m, rows, bc);
     }
     if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
   }
@@ -727,6 +725,8 @@ template <int NT, uint32_t U = kStU>
 __global__ __launch_bounds__(NT) void okv_gather_staged_kernel(CopyParams P) {
   __shared__ GatherSmem sm;
   __shared__ uint4 stage[NT / 64][StCfg<U>::cap / 16 + 2];
+  // after the value sweep (P.vsrc set): only when the sweep was unsafe
+  if (P.vsrc && sweep_safe(*P.tot, *P.big_count, P.row_cap, P.key_cap, P.val_cap)) return;
   for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
     const BlockMeta m = block_meta(P, b);
     if (block_head(P, b, m)) {
@@ -819,7 +819,7 @@ __device__ __noinline__ uint4 sweep_chunk_any(const uint8_t* seg, uint64_t seg_b
   return out;
 }
 
-template <uint32_t kU>
+template <uint32_t kU, bool kAl = false>
 __global__ __launch_bounds__(256) void okv_value_sweep_kernel(SweepParams S) {
   __shared__ SweepRows R;
   const uint64_t tile0 = uint64_t(blockIdx.x) * kU;
@@ -853,6 +853,15 @@ __global__ __launch_bounds__(256) void okv_value_sweep_kernel(SweepParams S) {
   __syncthreads();
   uint4 out[kU];
   bool put[kU];
+  uint4 nxt[kU];        // kAl: the next aligned line, where this lane loads it
+  uint32_t sft[kU];     // kAl: byte offset of the chunk in its line (0: no funnel)
+  bool own[kU];
+#pragma unroll
+  for (uint32_t u = 0; u < kU; ++u) {
+    sft[u] = 0;
+    own[u] = false;
+    nxt[u] = make_uint4(0, 0, 0, 0);
+  }
   // every load issued before any is used
 #pragma unroll
   for (uint32_t u = 0; u < kU; ++u) {
@@ -873,11 +882,36 @@ __global__ __launch_bounds__(256) void okv_value_sweep_kernel(SweepParams S) {
       }
     }
     // one unaligned 16-byte load inside the owner's value, or the owner's
-    // boundary chunk (okv_rows_kernel)
-    if (xr + 16 <= R.end[o])
-      out[u] = *reinterpret_cast<const uint4*>(S.seg + (R.bias[o] + int64_t(X)));
-    else
-      out[u] = S.bchunk[r0 + o];
+    // boundary chunk (okv_rows_kernel).  kAl: the aligned line holding the
+    // chunk's first byte; the next line comes from lane + 1 (the next chunk of
+    // the same row) by a shuffle, or is loaded here when that lane holds no
+    // such chunk (lane 63, the row's last whole chunk)
+    const bool whole = xr + 16 <= R.end[o];
+    if constexpr (kAl) {
+      const int64_t src = R.bias[o] + int64_t(X);
+      sft[u] = whole ? uint32_t(src & 15) : 0u;
+      own[u] = whole && sft[u] && ((tid & 63) == 63 || xr + 32 > R.end[o]);
+      if (whole) {
+        const uint4* line = reinterpret_cast<const uint4*>(S.seg + (src & ~int64_t(15)));
+        out[u] = line[0];
+        if (own[u]) nxt[u] = line[1];
+      } else {
+        out[u] = S.bchunk[r0 + o];
+      }
+    } else {
+      if (whole)
+        out[u] = *reinterpret_cast<const uint4*>(S.seg + (R.bias[o] + int64_t(X)));
+      else
+        out[u] = S.bchunk[r0 + o];
+    }
+  }
+  if constexpr (kAl) {
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint4 nb = make_uint4(__shfl_down(out[u].x, 1, 64), __shfl_down(out[u].y, 1, 64),
+                                  __shfl_down(out[u].z, 1, 64), __shfl_down(out[u].w, 1, 64));
+      if (sft[u]) out[u] = funnel32(out[u], own[u] ? nxt[u] : nb, sft[u]);
+    }
   }
   if (!full) {
 #pragma unroll
@@ -1791,7 +1825,13 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
         SweepParams S{w.seg, w.seg_bytes, o->val_off, o->val_len, P.vsrc, P.vtile, P.bchunk,
                       o->val_arena,
                       ctx->d_tot, P.big_count, o->row_cap, o->key_cap, o->val_cap};
-        if (ctx->value_sweep == 4)
+        if (ctx->value_sweep == 5)
+          hipLaunchKernelGGL((okv_value_sweep_kernel<4, true>), dim3(uint32_t((sw_tiles + 3) / 4)),
+                             dim3(256), 0, ctx->stream, S);
+        else if (ctx->value_sweep == 6)
+          hipLaunchKernelGGL((okv_value_sweep_kernel<2, true>), dim3(uint32_t((sw_tiles + 1) / 2)),
+                             dim3(256), 0, ctx->stream, S);
+        else if (ctx->value_sweep == 4)
           hipLaunchKernelGGL(okv_value_sweep_kernel<4>, dim3(uint32_t((sw_tiles + 3) / 4)),
                              dim3(256), 0, ctx->stream, S);
         else if (ctx->value_sweep == 2)
@@ -1801,6 +1841,10 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
           hipLaunchKernelGGL(okv_value_sweep_kernel<1>, dim3(uint32_t(sw_tiles)), dim3(256), 0,
                              ctx->stream, S);
       }
+      // the whole pass when the sweep is unsafe on device (big blocks,
+      // capacity); otherwise every workgroup returns at once (small grid)
+      hipLaunchKernelGGL((okv_gather_staged_kernel<kThreads>), dim3(std::min<uint32_t>(nblk, 2048)),
+                         dim3(kThreads), 0, ctx->stream, P);
     } else if (gather_threads(ctx, w, nblk) == 256 && ctx->gather_staged && !index_only) {
       hipLaunchKernelGGL((okv_gather_staged_kernel<kThreads>), g, dim3(kThreads), 0, ctx->stream, P);
     } else if (gather_threads(ctx, w, nblk) == 64 && ctx->gather_staged)
@@ -1945,7 +1989,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
   if (const char* v = getenv("OKV_VALUE_SWEEP")) {
     ctx->value_sweep = uint32_t(atoi(v));
-    if (ctx->value_sweep > 4 || ctx->value_sweep == 3) {
+    if (ctx->value_sweep > 6 || ctx->value_sweep == 3) {
       delete ctx;
       return nullptr;
     }

@@ -258,15 +258,16 @@ def decoders_by_width():
     launches), 256 (LDS-staged value spans, the default for large blocks),
     64 / 256 with OKV_GATHER_STAGED=0 and no fusion (global windows): 64g, 256g,
     and 256 with the values produced by the address-ordered value sweep
-    (OKV_VALUE_SWEEP=1 / 2 tiles per workgroup): 256s, 256s2."""
+    (OKV_VALUE_SWEEP=1 / 2 tiles per workgroup, 5: aligned loads + lane shuffles):
+    256s, 256s2, 256a."""
     import os
     decs = {}
     try:
-        for w in ("64", "64u", "64g", "256", "256g", "256s", "256s2"):
+        for w in ("64", "64u", "64g", "256", "256g", "256s", "256s2", "256a"):
             os.environ["OKV_GATHER_THREADS"] = w[:3].rstrip("gus")
             os.environ["OKV_GATHER_STAGED"] = "0" if w.endswith("g") else "1"
             os.environ["OKV_DECODE_FUSED"] = "1" if w == "64" else "0"
-            os.environ["OKV_VALUE_SWEEP"] = {"256s": "1", "256s2": "2"}.get(w, "0")
+            os.environ["OKV_VALUE_SWEEP"] = {"256s": "1", "256s2": "2", "256a": "5"}.get(w, "0")
             decs[w] = okv.Decoder(0)
     finally:
         for k in ("OKV_GATHER_THREADS", "OKV_GATHER_STAGED", "OKV_DECODE_FUSED",
@@ -309,7 +310,7 @@ def _wide_segment(seed, nblk=120):
     return bytes(seg), np.array(descs, np.uint64).reshape(-1, 4)
 
 
-@pytest.mark.parametrize("width", ["256", "256g", "256s", "256s2", "64", "64u", "64g"])
+@pytest.mark.parametrize("width", ["256", "256g", "256s", "256s2", "256a", "64", "64u", "64g"])
 def test_wide_spans_all_gathers(decoders_by_width, width):
     """Stage overflow (one-tile retry and global fallback), the segment's
     first and last bytes, odd block offsets: every gather vs the oracle."""
@@ -319,7 +320,7 @@ def test_wide_spans_all_gathers(decoders_by_width, width):
         _assert_same_as_oracle(got, seg, d, 0, False)
 
 
-@pytest.mark.parametrize("width", ["64", "64u", "64g", "256", "256g", "256s", "256s2"])
+@pytest.mark.parametrize("width", ["64", "64u", "64g", "256", "256g", "256s", "256s2", "256a"])
 def test_mixed_blocks_both_gather_widths(decoders_by_width, width):
     """A segment mixing 4 KiB blocks, 64 KiB blocks with few rows and blocks
     over kRCap rows, through the 64- and the 256-thread gather."""
@@ -366,7 +367,7 @@ def _tiny_value_segment(seed, nblk=300):
     return bytes(seg), np.array(descs, np.uint64).reshape(-1, 4)
 
 
-@pytest.mark.parametrize("width", ["256s", "256s2"])
+@pytest.mark.parametrize("width", ["256s", "256s2", "256a"])
 def test_value_sweep(decoders_by_width, width):
     """The value sweep vs the oracle: C3 blocks, wide spans, tiny values (row
     window overflow), a fuzz of corrupt/truncated blocks (statuses with rows

@@ -458,7 +458,7 @@ def run_decode(args, torch, okv, D):
         # read OriginalSize per block; write payload (padded arenas) + 22 B/row
         # SoA (u64 key_off, u16 key_len, u64 val_off, u32 val_len) + 28 B/block
         alg = orig_bytes + payload + rows * 22 + nblk * 28
-        sweep = os.environ.get("OKV_VALUE_SWEEP", "6") not in ("0", "") and \
+        sweep = os.environ.get("OKV_VALUE_SWEEP", "7") not in ("0", "") and \
             os.environ.get("OKV_GATHER_STAGED", "1") != "0"
         roof_kernel = ("okv_decode_fused_kernel (passes 1-3) + okv_copy_kernel"
                        if nblk <= 512 and in_bytes / max(nblk, 1) <= 16384 else

@@ -66,10 +66,10 @@ struct okv_ctx {
   uint32_t gather_grid = 0;  // 0: default grid; else workgroups (OKV_GATHER_GRID)
   uint32_t gather_threads = 0;  // 0: by average block size; else 64 or 256 (OKV_GATHER_THREADS)
   bool gather_staged = true;    // 256-thread pass 3 stages value spans in LDS (OKV_GATHER_STAGED=0: off)
-  uint32_t value_sweep = 6;     // large blocks: 0 = the per-block staged pass 3; 1/2/4 =
+  uint32_t value_sweep = 7;     // large blocks: 0 = the per-block staged pass 3; 1/2/4 =
                                 // okv_rows_kernel + okv_value_sweep_kernel with 1/2/4 tiles per
-                                // workgroup, unaligned loads; 5/6 = 4/2 tiles, aligned loads and
-                                // lane shuffles (default 6; OKV_VALUE_SWEEP)
+                                // workgroup, unaligned loads; 5/6/7 = 4/2/3 tiles, aligned loads
+                                // and lane shuffles (default 7; OKV_VALUE_SWEEP)
   void* d_hdr = nullptr;        // [nblk x kRCap] pass-1 headers (sweep)
   size_t cap_hdr = 0;
   void* d_vsrc = nullptr;       // [row] value sources (sweep hand-off)

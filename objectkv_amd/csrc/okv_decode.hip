@@ -1828,6 +1828,9 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
         if (ctx->value_sweep == 5)
           hipLaunchKernelGGL((okv_value_sweep_kernel<4, true>), dim3(uint32_t((sw_tiles + 3) / 4)),
                              dim3(256), 0, ctx->stream, S);
+        else if (ctx->value_sweep == 7)
+          hipLaunchKernelGGL((okv_value_sweep_kernel<3, true>), dim3(uint32_t((sw_tiles + 2) / 3)),
+                             dim3(256), 0, ctx->stream, S);
         else if (ctx->value_sweep == 6)
           hipLaunchKernelGGL((okv_value_sweep_kernel<2, true>), dim3(uint32_t((sw_tiles + 1) / 2)),
                              dim3(256), 0, ctx->stream, S);
@@ -1989,7 +1992,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
   if (const char* v = getenv("OKV_VALUE_SWEEP")) {
     ctx->value_sweep = uint32_t(atoi(v));
-    if (ctx->value_sweep > 6 || ctx->value_sweep == 3) {
+    if (ctx->value_sweep > 7 || ctx->value_sweep == 3) {
       delete ctx;
       return nullptr;
     }

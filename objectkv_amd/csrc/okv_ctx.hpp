@@ -66,11 +66,16 @@ struct okv_ctx {
   uint32_t gather_grid = 0;  // 0: default grid; else workgroups (OKV_GATHER_GRID)
   uint32_t gather_threads = 0;  // 0: by average block size; else 64 or 256 (OKV_GATHER_THREADS)
   bool gather_staged = true;    // 256-thread pass 3 stages value spans in LDS (OKV_GATHER_STAGED=0: off)
-  uint32_t value_sweep = 7;     // large blocks: 0 = the per-block staged pass 3; 1/2/4 =
-                                // okv_rows_kernel + okv_value_sweep_kernel with 1/2/4 tiles per
-                                // workgroup, unaligned loads; 5/6/7 = 4/2/3 tiles, aligned loads
-                                // and lane shuffles (default 7; OKV_VALUE_SWEEP)
-  void* d_hdr = nullptr;        // [nblk x kRCap] pass-1 headers (sweep)
+  uint32_t value_sweep = 7;     // large blocks: 8 = okv_tile_kernel (source tiles); 0 = the
+                                // per-block staged pass 3; 1/2/4 = okv_rows_kernel +
+                                // okv_value_sweep_kernel with 1/2/4 tiles per workgroup,
+                                // unaligned loads; 5/6/7 = 4/2/3 tiles, aligned loads and lane
+                                // shuffles (OKV_VALUE_SWEEP)
+  uint32_t tile_kib = 16;       // okv_tile_kernel tile bytes / 1024 (OKV_TILE)
+  bool tile_xcd = true;         // consecutive tiles on one XCD
+  uint32_t tile_threads = 256;  // okv_tile_kernel workgroup width
+  uint32_t tile_seg = 1;        // consecutive destination chunks per lane run
+  void* d_hdr = nullptr;        // [nblk x kRCap] pass-1 record key lengths (u16)
   size_t cap_hdr = 0;
   void* d_vsrc = nullptr;       // [row] value sources (sweep hand-off)
   size_t cap_vsrc = 0;

@@ -42,11 +42,15 @@
 
 namespace okv {
 
-// Record positions from pass 1: record r < kRCap of block b at
-// [r / 16][block][r % 16] -- 64-byte segments of 16 records per block.
-__device__ __forceinline__ uint64_t rec_index(uint32_t nblk, uint32_t b, uint32_t r) {
-  return ((r >> 4) * uint64_t(nblk) + b) * 16 + (r & 15);
+// Record table from pass 1, block-major: record r < kRCap of block b at
+// rt_pos[b * kRCap + r] (u32 position in the block) and rt_kl[b * kRCap + r]
+// (u16 key length).  A consumer wave reads a block's table with one
+// coalesced 256-B (128-B) load.  Pass 1 buffers kRecChunk records per lane
+// in LDS and writes them out as whole 16-byte pieces (see okv_count_kernel).
+__device__ __forceinline__ uint64_t rec_index(uint32_t /*nblk*/, uint32_t b, uint32_t r) {
+  return uint64_t(b) * kRCap + r;
 }
+constexpr uint32_t kRecChunk = 16;  // records per lane between two LDS flushes
 
 // ---------------------------------------------------------------------------
 // Pass 1: header walk in HBM, one lane per block.
@@ -56,14 +60,30 @@ __device__ __forceinline__ uint64_t rec_index(uint32_t nblk, uint32_t b, uint32_
 // once -- so the dependent header chase then hits the caches instead of HBM.
 // A single-tile launch (one workgroup) also zeroes the big-block counter and
 // writes the totals itself (no memset, no scan launch): single_* non-null.
+//
+// Record table: every kRecChunk steps of the walk the workgroup stops at a
+// barrier and writes the slots its lanes recorded since the last stop, as
+// whole 16-byte pieces of the block-major table (4 consecutive lanes write
+// one block's 64 bytes of positions).  Lockstep per-lane stores into a
+// strided table (round 2: [r/16][block][r%16], u32 positions + u64 headers)
+// left partial lines that the walk's own reads evicted between steps: 136 MB
+// written per C3 launch for 50 MB of slots.
+//
+// Big blocks (okv_copy_kernel): more than kRCap rows, a walk ending at or past
+// 4 GiB, or past span_cap (the tile pass's span: okv_tile_kernel).
 __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     const uint8_t* __restrict__ seg, uint64_t seg_bytes, const Desc* __restrict__ descs,
     uint32_t nblk, int comp, BlockCount* __restrict__ cnt, Prefix* __restrict__ lp,
-    Prefix* __restrict__ tile_tot, uint32_t* __restrict__ rec_s, uint32_t* __restrict__ big_list,
-    uint32_t* __restrict__ big_count, const int32_t* __restrict__ pre_status, int prefetch,
-
+    Prefix* __restrict__ tile_tot, uint32_t* __restrict__ rt_pos, uint16_t* __restrict__ rt_kl,
+    uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count,
+    const int32_t* __restrict__ pre_status, int prefetch, uint64_t span_cap,
     Prefix* __restrict__ single_pre, Totals* __restrict__ single_tot,
-    uint64_t* __restrict__ single_row_start, uint64_t* __restrict__ hdr_s) {
+    uint64_t* __restrict__ single_row_start) {
+  // slots of the current chunk: positions [lane][kRecChunk + 1] (odd stride:
+  // the walking lanes' stores hit distinct banks), key lengths [lane][kRecChunk]
+  __shared__ uint32_t s_pos[kThreads * (kRecChunk + 1)];
+  __shared__ __align__(16) uint16_t s_kl[kThreads * kRecChunk];
+  __shared__ uint32_t s_rows[kThreads];
   const uint32_t tid = threadIdx.x;
   const uint32_t b = blockIdx.x * kTile + tid;
   uint64_t rows = 0, kb = 0, vb = 0, p = 0;
@@ -72,6 +92,8 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     if (tid == 0) *big_count = 0;
     __syncthreads();
   }
+  uint64_t len = 0, orig = 0, off = 0;
+  bool walking = false;
   if (b < nblk) {
     const Desc d = descs[b];
     const int32_t pre = pre_status ? pre_status[b] : int32_t(OKV_BLK_OK);
@@ -84,20 +106,19 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     } else if (comp == OKV_COMP_ZSTD) {
       st = OKV_BLK_UNSUPPORTED;  // index-only spans cannot point into decompressed bytes
     } else {
-      const uint64_t len = (comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
-      const uint64_t orig = d.original_size;
-      // position of record r < kRCap for pass 3 at rec_s[rec_index(nblk, b, r)]:
-      // the lanes of a wave (consecutive blocks, same r: they step in
-      // lockstep) fill whole 64-byte segments within 16 steps
+      len = (comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
+      orig = d.original_size;
+      off = d.offset;
+      walking = true;
       if (prefetch && orig && len) {
         // up to 32 lines (4 KiB), all issued before any is waited on;
         // addresses clamped into [offset, offset + min(orig, len))
-        const uint64_t first = d.offset & ~uint64_t(3);
-        const uint64_t last = (d.offset + (orig < len ? orig : len) - 1) & ~uint64_t(3);
+        const uint64_t first = off & ~uint64_t(3);
+        const uint64_t last = (off + (orig < len ? orig : len) - 1) & ~uint64_t(3);
         uint32_t v[32];
 #pragma unroll
         for (int u = 0; u < 32; ++u) {
-          uint64_t a = (d.offset & ~uint64_t(127)) + 128ull * u;
+          uint64_t a = (off & ~uint64_t(127)) + 128ull * u;
           a = a < first ? first : (a > last ? last : a);
           v[u] = *reinterpret_cast<const uint32_t*>(seg + a);
         }
@@ -106,31 +127,72 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
         for (int u = 0; u < 32; ++u) acc ^= v[u];
         asm volatile("" ::"v"(acc));  // keep the loads; their values are unused
       }
-      // The walk is a dependent chain (record i+1 starts where i ends), so
-      // this kernel is bound by HBM latency x the longest block's row count.
-      while (p < orig) {  // :340
+    }
+  }
+  // The walk is a dependent chain (record i+1 starts where i ends), so this
+  // kernel is bound by HBM latency x the longest block's row count.
+  const uint32_t b0 = blockIdx.x * kTile;
+  for (uint32_t c = 0; c < uint32_t(kRCap) / kRecChunk; ++c) {
+    const uint64_t cap = uint64_t(c + 1) * kRecChunk;
+    if (walking) {
+      while (p < orig && rows < cap) {  // :340
         if (len - p < 6) { st = OKV_BLK_PANIC; break; }  // u16/u32 reads (:342-345)
         uint32_t kl, vl;
-        header_global(seg, d.offset + p, kl, vl);
+        header_global(seg, off + p, kl, vl);
         const uint64_t room = len - p - 6;
         if (kl > room || vl > room - kl) {  // zero-length reads always succeed (:490-493)
           st = OKV_BLK_PANIC;                // key/value reads (:346-349)
           break;
         }
-        if (rows < kRCap) {
-          rec_s[rec_index(nblk, b, uint32_t(rows))] = uint32_t(p);
-          // the value sweep's row pass takes the headers from here (one HBM
-          // trip fewer than reading them again at the positions)
-          if (hdr_s) hdr_s[rec_index(nblk, b, uint32_t(rows))] = (uint64_t(kl) << 32) | vl;
-        }
+        const uint32_t slot = uint32_t(rows) & (kRecChunk - 1);
+        s_pos[tid * (kRecChunk + 1) + slot] = uint32_t(p);
+        s_kl[tid * kRecChunk + slot] = uint16_t(kl);
         rows++;
         kb += kl;
         vb += vl;
         p += 6 + uint64_t(kl) + uint64_t(vl);
       }
+      if (st != OKV_BLK_OK) walking = false;
     }
+    s_rows[tid] = st == OKV_BLK_OK ? uint32_t(rows) : 0u;
+    __syncthreads();
+    // slots [c * 16, c * 16 + 16) of the workgroup's blocks, live ones only
+    for (uint32_t q = tid; q < uint32_t(kTile) * 4; q += kThreads) {
+      const uint32_t lb = q >> 2, sub = q & 3, slot = c * kRecChunk + sub * 4;
+      if (b0 + lb < nblk && slot < s_rows[lb]) {
+        const uint32_t* s = &s_pos[lb * (kRecChunk + 1) + sub * 4];
+        *reinterpret_cast<uint4*>(rt_pos + rec_index(nblk, b0 + lb, slot)) =
+            make_uint4(s[0], s[1], s[2], s[3]);
+      }
+    }
+    if (rt_kl) {
+      for (uint32_t q = tid; q < uint32_t(kTile) * 2; q += kThreads) {
+        const uint32_t lb = q >> 1, sub = q & 1, slot = c * kRecChunk + sub * 8;
+        if (b0 + lb < nblk && slot < s_rows[lb])
+          *reinterpret_cast<uint4*>(rt_kl + rec_index(nblk, b0 + lb, slot)) =
+              *reinterpret_cast<const uint4*>(&s_kl[lb * kRecChunk + sub * 8]);
+      }
+    }
+    walking = walking && p < orig;  // (then rows == cap)
+    if (!__syncthreads_or(walking)) break;  // also the barrier before the slots are reused
+  }
+  // blocks with more than kRCap rows: finish the walk without recording
+  if (walking) {
+    while (p < orig) {
+      if (len - p < 6) { st = OKV_BLK_PANIC; break; }
+      uint32_t kl, vl;
+      header_global(seg, off + p, kl, vl);
+      const uint64_t room = len - p - 6;
+      if (kl > room || vl > room - kl) { st = OKV_BLK_PANIC; break; }
+      rows++;
+      kb += kl;
+      vb += vl;
+      p += 6 + uint64_t(kl) + uint64_t(vl);
+    }
+  }
+  if (b < nblk) {
     if (st != OKV_BLK_OK) rows = kb = vb = 0;
-    if (st == OKV_BLK_OK && (rows > kRCap || p >= (uint64_t(1) << 32)))
+    if (st == OKV_BLK_OK && (rows > kRCap || p >= (uint64_t(1) << 32) || p > span_cap))
       big_list[atomicAdd(big_count, 1u)] = b;  // staged path (okv_copy_kernel)
     BlockCount c;
     c.rows = rows;
@@ -154,9 +216,9 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    uint64_t off = 0;
-    for (int w = 0; w < wave; ++w) off += s_w[k][w];
-    inc[k] += off - v[k];  // exclusive
+    uint64_t off2 = 0;
+    for (int w = 0; w < wave; ++w) off2 += s_w[k][w];
+    inc[k] += off2 - v[k];  // exclusive
   }
   if (b < nblk) {
     Prefix e;
@@ -252,8 +314,8 @@ struct CopyParams {
   const BlockCount* cnt;
   const Prefix* lp;
   const Prefix* tile_pre;
-  const uint32_t* rec_s;      // pass-1 record positions (u32, block-major) or headers
-                              // (u64 klen << 32 | vlen): see okv_count_kernel
+  const uint32_t* rt_pos;     // pass-1 record table: positions (block-major, rec_index)
+  const uint16_t* rt_kl;      // ... and key lengths (null unless the pass needs them)
   uint32_t* big_list;         // blocks with > kRCap rows (or >= 4 GiB walks)
   uint32_t* big_count;
   uint64_t* row_start;
@@ -271,8 +333,8 @@ struct CopyParams {
   uint64_t* vsrc;             // [row] segment position of the row's value
   uint32_t* vtile;            // [value-arena tile] row owning the tile's first byte
   uint4* bchunk;              // [row] the chunk holding the end of the row's value
-  const uint64_t* hdr_s;      // pass-1 headers (klen << 32 | vlen), rec_index layout
   const Totals* tot;          // call totals (pass 1 / pass 2)
+  uint64_t span_cap;          // okv_tile_kernel: blocks whose walk ends past it are big
 };
 
 // The value sweep runs when every row's index is written by the per-block
@@ -549,7 +611,7 @@ __global__ __launch_bounds__(NT) void okv_gather_kernel(CopyParams P) {
       const GlobalWin src{P.seg, P.seg_bytes, m.off};
       if (threadIdx.x < 64) {
         const uint32_t t = threadIdx.x;
-        const uint32_t rec = int(t) < rows ? P.rec_s[rec_index(P.nblk, b, t)] : 0u;
+        const uint32_t rec = int(t) < rows ? P.rt_pos[rec_index(P.nblk, b, t)] : 0u;
         build_row_table(src, sm, rows, rec);
       }
       __syncthreads();
@@ -577,16 +639,19 @@ __global__ __launch_bounds__(64) void okv_rows_kernel(CopyParams P) {
     // record positions and headers with the metadata (one trip; the slots
     // exist for every block, only the first `rows` are meaningful)
     const uint32_t t = threadIdx.x;
-    const uint32_t rec = P.rec_s[rec_index(P.nblk, b, t)];
-    const uint64_t hdr = P.hdr_s ? P.hdr_s[rec_index(P.nblk, b, t)] : 0;
+    const uint32_t rec = P.rt_pos[rec_index(P.nblk, b, t)];
+    const uint32_t kl = P.rt_kl ? P.rt_kl[rec_index(P.nblk, b, t)] : 0u;
     const BlockMeta m = block_meta(P, b);
     if (block_head(P, b, m)) {
       const int rows = int(m.c.rows);
       const GlobalWin src{P.seg, P.seg_bytes, m.off};
-      if (P.hdr_s) {
+      if (P.rt_kl) {
+        // value length from the next record's position (the walk's end after the last)
         const bool live = int(t) < rows;
-        fill_row_table(sm, rows, live ? rec : 0u, live ? uint32_t(hdr >> 32) : 0u,
-                       live ? uint32_t(hdr) : 0u);
+        uint32_t nxt = __shfl_down(rec, 1, 64);
+        if (int(t) == rows - 1) nxt = uint32_t(m.c.pend);
+        fill_row_table(sm, rows, live ? rec : 0u, live ? kl : 0u,
+                       live ? nxt - rec - 6 - kl : 0u);
       } else {
         build_row_table(src, sm, rows, int(t) < rows ? rec : 0u);
       }
@@ -734,7 +799,7 @@ __global__ __launch_bounds__(NT) void okv_gather_staged_kernel(CopyParams P) {
       const GlobalWin src{P.seg, P.seg_bytes, m.off};
       if (threadIdx.x < 64) {
         const uint32_t t = threadIdx.x;
-        const uint32_t rec = int(t) < rows ? P.rec_s[rec_index(P.nblk, b, t)] : 0u;
+        const uint32_t rec = int(t) < rows ? P.rt_pos[rec_index(P.nblk, b, t)] : 0u;
         build_row_table(src, sm, rows, rec);
       }
       __syncthreads();
@@ -929,6 +994,207 @@ __global__ __launch_bounds__(256) void okv_value_sweep_kernel(SweepParams S) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pass 3, source tiles (large blocks).  Block b is cut into
+// tiles of kT source bytes, tile t = block bytes [t kT, (t + 1) kT), one
+// short-lived 256-thread workgroup each, dispatched in address order: the
+// whole chip's loads and stores stay in one compact window of the segment
+// and the arenas (the one-shot copy shape).  A workgroup
+//   1. loads the block's metadata and its pass-1 record table (one trip),
+//   2. DMAs its tile (plus a 16-byte lead-in and a guard line) into LDS with
+//      global_load_lds_dwordx4 -- the only read of the record bytes,
+//   3. writes every key and value byte whose SOURCE lies in its tile: the
+//      destination ranges are contiguous (rows are packed in record order),
+//      each 16-byte destination chunk is assembled from the stage (one LDS
+//      window per row piece) and stored whole; the two chunks at a range's
+//      ends that the neighbouring tile shares are stored byte-exactly
+//      (store_partial: disjoint bytes, no read-modify-write).
+// Tile 0 also writes the block's row index (SoA) and its block outputs.  The
+// last tile writes the zero padding of the block's arena regions.  Each
+// source byte is read once and each arena byte written once, so the pass
+// moves its algorithmic bytes: the round-2 row pass + value sweep read the
+// lines values share with headers and keys twice (1.11x).
+// kXcd: consecutive tiles run on one XCD (hardware deals workgroups to the 8
+// XCDs round-robin), so a block's metadata and the chunks two tiles share
+// meet in one L2.
+// ---------------------------------------------------------------------------
+struct TileRows {
+  uint32_t kpre[kRCap + 1];  // exclusive prefix of key lengths (kpre[rows] = total)
+  uint32_t vpre[kRCap + 1];  // ... of value lengths
+  uint32_t ksb[kRCap];       // block position of key-region byte x of row r = ksb[r] + x
+  uint32_t vsb[kRCap];       // likewise for values
+  uint32_t x[4];             // owned key range [x0, x1), value range [x2, x3)
+};
+
+template <uint32_t kT, uint32_t kNT, uint32_t kS, bool kXcd>
+__global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tpb, uint32_t ntile) {
+  __shared__ TileRows R;
+  __shared__ uint4 stage[kT / 16 + 4];
+  uint32_t L = blockIdx.x;
+  if constexpr (kXcd) L = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (L >= ntile) return;
+  // uniform block index (an SGPR: the loads below are scalar, all in one trip)
+  const uint32_t b = __builtin_amdgcn_readfirstlane(L / tpb);
+  const uint32_t t = L - b * tpb;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  // one trip: the block's scalars and (wave 0) its record table
+  uint32_t rec = 0, kl = 0;
+  if (tid < 64) {
+    rec = P.rt_pos[rec_index(P.nblk, b, lane)];
+    kl = P.rt_kl[rec_index(P.nblk, b, lane)];
+  }
+  const uint64_t off = P.descs[b].offset;
+  const BlockCount c = P.cnt[b];
+  const Prefix lpre = P.lp[b], tpre = P.tile_pre[b / kTile];
+  // consume every scalar here: the scheduler otherwise sinks each load to its
+  // first use, one dependent trip after another
+  asm volatile("" ::"s"(off), "s"(c.rows), "s"(c.kbytes), "s"(c.vbytes), "s"(c.pend),
+               "s"(c.status), "s"(lpre.rows), "s"(lpre.kb), "s"(lpre.vb), "s"(tpre.rows),
+               "s"(tpre.kb), "s"(tpre.vb));
+  BlockMeta m;
+  m.c = c;
+  m.off = off;
+  m.B.row0 = tpre.rows + lpre.rows;
+  m.B.kb0 = tpre.kb + lpre.kb;
+  m.B.vb0 = tpre.vb + lpre.vb;
+  const bool fits = m.B.row0 + c.rows <= P.row_cap &&
+                    (P.index_only || (m.B.kb0 + round16(c.kbytes) <= P.key_cap &&
+                                      m.B.vb0 + round16(c.vbytes) <= P.val_cap));
+  m.B.st = (c.status == OKV_BLK_OK && !fits) ? int32_t(OKV_BLK_CAPACITY) : c.status;
+  if (t == 0 && tid == 0) {
+    P.row_start[b] = m.B.row0;
+    if (P.key_base) P.key_base[b] = m.B.kb0;
+    if (P.val_base) P.val_base[b] = m.B.vb0;
+    P.blk_status[b] = m.B.st;
+  }
+  const uint64_t pend = m.c.pend;
+  const uint32_t P0 = t * kT;
+  // big blocks are okv_copy_kernel's (the same test as okv_count_kernel's)
+  if (m.B.st != OKV_BLK_OK || m.c.rows == 0 || m.c.rows > uint64_t(kRCap) || pend > P.span_cap ||
+      pend >= (uint64_t(1) << 32) || P0 >= pend)
+    return;
+  const uint32_t rows = uint32_t(m.c.rows);
+  const uint32_t P1 = uint32_t(min<uint64_t>(uint64_t(P0) + kT, pend));
+  const bool last_tile = P1 == pend;
+  // stage = segment lines [A, E): the line before the one holding the tile's
+  // first byte (windows of a chunk begin up to 15 bytes before its first
+  // owned byte) through the line after the one holding its last byte + 15
+  const int64_t A = int64_t((m.off + P0) & ~uint64_t(15)) - 16;
+  const int64_t E = int64_t((m.off + P1 + 15) & ~uint64_t(15)) + 16;
+  const uint32_t np = uint32_t((E - A) >> 4);
+  if (!P.index_only) {
+    const int64_t lim = int64_t(round16(P.seg_bytes));
+    for (uint32_t k0 = 0; k0 < np; k0 += kNT) {
+      const uint32_t i = k0 + tid;
+      if (i < np) {
+        int64_t a = A + (int64_t(i) << 4);
+        if (a < 0 || a + 16 > lim) a = int64_t(m.off) & ~int64_t(15);  // bytes never used
+        __builtin_amdgcn_global_load_lds(P.seg + a, OKV_LDS_PTR(stage + k0 + (tid & ~63u)), 16,
+                                         0, 0);
+      }
+    }
+  }
+  // row table (wave 0, lane r = row r) while the tile is in flight
+  if (tid < 64) {
+    const bool live = lane < rows;
+    uint32_t nxt = __shfl_down(rec, 1, 64);
+    if (lane == rows - 1) nxt = uint32_t(pend);
+    const uint32_t k = live ? kl : 0u, v = live ? nxt - rec - 6 - kl : 0u;
+    const uint32_t ki = wave_incl_scan32(k, int(lane)), vi = wave_incl_scan32(v, int(lane));
+    const uint32_t kp = ki - k, vp = vi - v;
+    const uint32_t ks = rec + 6, vs = rec + 6 + k;  // block positions of the key / value
+    if (live) {
+      R.kpre[lane] = kp;
+      R.vpre[lane] = vp;
+      R.ksb[lane] = ks - kp;
+      R.vsb[lane] = vs - vp;
+      if (lane == rows - 1) {
+        R.kpre[rows] = ki;
+        R.vpre[rows] = vi;
+      }
+    }
+    if (t == 0 && live) {  // the block's SoA row index
+      const uint64_t g = m.B.row0 + lane;
+      P.key_len[g] = uint16_t(k);
+      P.val_len[g] = v;
+      if (P.index_only) {
+        P.key_off[g] = m.off + ks;
+        P.val_off[g] = m.off + vs;
+      } else {
+        P.key_off[g] = m.B.kb0 + kp;
+        P.val_off[g] = m.B.vb0 + vp;
+      }
+    }
+    // the owned ranges: [first byte whose source is >= P0, same for P1); the
+    // last tile also owns the 16-byte padding after the region
+    const uint32_t KT = __shfl(ki, int(rows - 1), 64), VT = __shfl(vi, int(rows - 1), 64);
+    auto first_at = [&](uint32_t len, uint32_t src, uint32_t pre, uint32_t tot, uint32_t Q) {
+      const uint64_t mk = __ballot(live && len && src + len > Q);
+      if (!mk) return tot;
+      const int j = __ffsll(static_cast<unsigned long long>(mk)) - 1;
+      const uint32_t s = __shfl(src, j, 64), pr = __shfl(pre, j, 64);
+      return Q > s ? pr + (Q - s) : pr;
+    };
+    const uint32_t kx0 = first_at(k, ks, kp, KT, P0), vx0 = first_at(v, vs, vp, VT, P0);
+    const uint32_t kx1 = last_tile ? uint32_t(round16(KT)) : first_at(k, ks, kp, KT, P1);
+    const uint32_t vx1 = last_tile ? uint32_t(round16(VT)) : first_at(v, vs, vp, VT, P1);
+    if (lane == 0) {
+      R.x[0] = kx0;
+      R.x[1] = kx1;
+      R.x[2] = vx0;
+      R.x[3] = vx1;
+    }
+  }
+  if (P.index_only) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const uint32_t kx0 = R.x[0], kx1 = R.x[1], vx0 = R.x[2], vx1 = R.x[3];
+  const uint32_t nk = kx1 > kx0 ? ((kx1 + 15) >> 4) - (kx0 >> 4) : 0u;
+  const uint32_t nv = vx1 > vx0 ? ((vx1 + 15) >> 4) - (vx0 >> 4) : 0u;
+  const int64_t sbias = int64_t(m.off) - A;  // stage byte of block position s = s + sbias
+  const uint32_t lastr = rows - 1;
+  // lane work: kS consecutive destination chunks (one row search per run of
+  // kS chunks; rows only move forward inside it)
+  const uint32_t uk = (nk + kS - 1) / kS, uv = (nv + kS - 1) / kS;
+  for (uint32_t j = tid; j < uk + uv; j += kNT) {
+    const bool isv = j >= uk;
+    const uint32_t* pre = isv ? R.vpre : R.kpre;
+    const uint32_t* sb = isv ? R.vsb : R.ksb;
+    const uint32_t X0 = isv ? vx0 : kx0, X1 = isv ? vx1 : kx1;
+    const uint32_t tot = pre[rows];
+    const uint32_t c0 = (X0 >> 4) + (isv ? j - uk : j) * kS;
+    uint8_t* const arena = isv ? P.val_arena + m.B.vb0 : P.key_arena + m.B.kb0;
+    uint32_t r = row_of(pre, lastr, max(c0 << 4, X0));
+#pragma unroll
+    for (uint32_t k = 0; k < kS; ++k) {
+      const uint32_t x = (c0 + k) << 4;
+      const uint32_t lo = max(x, X0), hi = min(x + 16, X1);
+      if (lo >= hi) break;  // past the owned range
+      const uint32_t dend = min(hi, tot);
+      while (r < lastr && pre[r + 1] <= lo) ++r;
+      uint4 out;
+      if (lo == x && dend == x + 16 && pre[r + 1] >= x + 16) {  // inside row r
+        out = load16_lds_b128(stage, uint32_t(int64_t(sb[r]) + x + sbias));
+      } else {
+        out = make_uint4(0, 0, 0, 0);
+        uint32_t rr = r;
+        for (uint32_t d = lo; d < dend; ++rr) {
+          const uint32_t e = min(dend, pre[rr + 1]);
+          if (e > d) {  // bytes [d, e) of the chunk from row rr
+            const uint4 w = load16_lds_b128(stage, uint32_t(int64_t(sb[rr]) + x + sbias));
+            out = merge_bytes(out, w, int32_t(d - x), int32_t(e - x));
+            d = e;
+          }
+        }
+      }
+      if (lo == x && hi == x + 16)
+        *reinterpret_cast<uint4*>(arena + x) = out;
+      else
+        store_partial(arena + x, out, lo - x, hi - x);
+    }
+  }
+}
+
 // Pass 3, small-block staged form (blocks averaging <= 16 KiB, e.g. 4 KiB
 // blocks): one wave per block DMAs the whole block into its LDS stage right
 // after the metadata arrives, then reads the record headers and assembles
@@ -956,7 +1222,7 @@ __global__ __launch_bounds__(64) void okv_gather_small_kernel(CopyParams P) {
   const uint32_t lane = threadIdx.x;
   for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
     // record positions ride with the metadata (slots exist for every r < kRCap)
-    const uint32_t rec0 = P.rec_s[rec_index(P.nblk, b, lane)];
+    const uint32_t rec0 = P.rt_pos[rec_index(P.nblk, b, lane)];
     const BlockMeta m = block_meta(P, b);
     if (block_head(P, b, m)) {
       const int rows = int(m.c.rows);
@@ -1664,9 +1930,11 @@ uint32_t gather_threads(const okv_ctx* ctx, const Work& w, uint32_t nblk) {
   return nblk && w.seg_bytes / nblk <= 16384 ? 64u : 256u;
 }
 
-// Launch passes 1 and 2 on device inputs.
+// Launch passes 1 and 2 on device inputs.  rt_kl: record key lengths for the
+// tile pass (null: positions only); span_cap: blocks whose walk ends past it
+// go to the big-block list.
 int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_start,
-                bool timed = false, uint64_t* d_hdr = nullptr) {
+                bool timed = false, uint16_t* rt_kl = nullptr, uint64_t span_cap = ~0ull) {
   int rc = ensure_blocks(ctx, nblk);
   if (rc) return rc;
   const uint32_t ntiles = (nblk + kTile - 1) / kTile;
@@ -1678,9 +1946,9 @@ int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_star
   if (ntiles)
     hipLaunchKernelGGL(okv_count_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, w.seg,
                        w.seg_bytes, w.descs, nblk, w.comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
-                       ctx->d_rec, ctx->d_big, ctx->d_big + nblk, w.pre, prefetch,
+                       ctx->d_rec, rt_kl, ctx->d_big, ctx->d_big + nblk, w.pre, prefetch, span_cap,
                        single ? ctx->d_tile_pre : nullptr, single ? ctx->d_tot : nullptr,
-                       single ? d_row_start : nullptr, d_hdr);
+                       single ? d_row_start : nullptr);
   if (timed) prof_mark(ctx, 2);
   if (!single)
     hipLaunchKernelGGL(okv_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_tile_tot,
@@ -1688,6 +1956,55 @@ int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_star
   if (timed) prof_mark(ctx, 3);
   OKV_HIP(hipGetLastError());
   return OKV_OK;
+}
+
+// Tile-pass geometry (okv_tile_kernel): tiles per block from the call's
+// average block span, rounded down to 4 KiB (a segment's meta block and
+// trailer add far less than that per block); blocks whose walk ends past
+// tpb tiles are big blocks (okv_copy_kernel).  Index-only decodes write only
+// the row index: one workgroup per block, no span limit.
+struct TileGeo {
+  uint32_t tpb;
+  uint64_t span_cap;
+};
+TileGeo tile_geo(const okv_ctx* ctx, uint64_t seg_bytes, uint32_t nblk, bool index_only) {
+  if (index_only || !nblk) return {1, ~0ull};
+  const uint64_t kT = uint64_t(ctx->tile_kib) << 10;
+  uint64_t span = (seg_bytes / nblk) & ~uint64_t(4095);
+  if (span < 4096) span = 4096;
+  uint64_t tpb = std::min<uint64_t>(64, (span + kT - 1) / kT);
+  while (tpb > 1 && uint64_t(nblk) * tpb >= (uint64_t(1) << 31)) tpb >>= 1;
+  return {uint32_t(tpb), tpb * kT};
+}
+
+template <uint32_t kT, uint32_t kNT, uint32_t kS, bool kXcd>
+void launch_tile_t(hipStream_t s, const CopyParams& P, uint32_t tpb, uint32_t ntile) {
+  const uint32_t grid = kXcd ? ((ntile + 7u) & ~7u) : ntile;
+  hipLaunchKernelGGL((okv_tile_kernel<kT, kNT, kS, kXcd>), dim3(grid), dim3(kNT), 0, s, P, tpb,
+                     ntile);
+}
+typedef void (*TileLaunch)(hipStream_t, const CopyParams&, uint32_t, uint32_t);
+struct TileForm {
+  uint32_t kib, threads, seg;
+  TileLaunch x, plain;
+};
+#define OKV_TILE_FORM(K, N, S)                                                        \
+  TileForm {                                                                          \
+    K, N, S, launch_tile_t<K * 1024, N, S, true>, launch_tile_t<K * 1024, N, S, false> \
+  }
+const TileForm kTileForms[] = {
+    OKV_TILE_FORM(16, 256, 1), OKV_TILE_FORM(16, 256, 2), OKV_TILE_FORM(16, 256, 4),
+    OKV_TILE_FORM(8, 256, 1),  OKV_TILE_FORM(8, 256, 2),  OKV_TILE_FORM(32, 256, 1),
+    OKV_TILE_FORM(32, 256, 4), OKV_TILE_FORM(16, 512, 1), OKV_TILE_FORM(32, 512, 1),
+    OKV_TILE_FORM(32, 512, 2), OKV_TILE_FORM(4, 256, 1)};
+const TileForm* tile_form(uint32_t kib, uint32_t threads, uint32_t seg) {
+  for (const TileForm& f : kTileForms)
+    if (f.kib == kib && f.threads == threads && f.seg == seg) return &f;
+  return nullptr;
+}
+void launch_tile(okv_ctx* ctx, const CopyParams& P, const TileGeo& g) {
+  const TileForm* f = tile_form(ctx->tile_kib, ctx->tile_threads, ctx->tile_seg);
+  (ctx->tile_xcd ? f->x : f->plain)(ctx->stream, P, g.tpb, P.nblk * g.tpb);
 }
 
 int read_totals(okv_ctx* ctx, Totals* out) {
@@ -1737,14 +2054,19 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   // small blocks: passes 1-3 in one launch (okv_decode_fused_kernel)
   const bool fused =
       ctx->fused && nblk && nblk <= kFusedMaxBlocks && gather_threads(ctx, w, nblk) == 64;
-  // values by the address-ordered sweep (256-thread staged pass 3 only; the
-  // kernels fall back to the per-block value gather on device when it is unsafe)
-  const bool sweep = ctx->value_sweep && nblk && !fused && !index_only && ctx->gather_staged &&
-                     gather_threads(ctx, w, nblk) == 256 && o->row_cap < (uint64_t(1) << 32);
-  if (sweep) {
+  // large blocks: the source-tile pass (okv_tile_kernel); value_sweep 1-7 are
+  // the round-2 forms (row pass + address-ordered value sweep)
+  const bool large = nblk && !fused && gather_threads(ctx, w, nblk) == 256;
+  const bool tile = large && ctx->value_sweep == 8;
+  const bool sweep = large && !tile && ctx->value_sweep && !index_only && ctx->gather_staged &&
+                     o->row_cap < (uint64_t(1) << 32);
+  const TileGeo geo = tile ? tile_geo(ctx, w.seg_bytes, nblk, index_only) : TileGeo{1, ~0ull};
+  uint16_t* rt_kl = nullptr;
+  if (tile || sweep) {
     if ((rc = ensure_blocks(ctx, nblk)) ||
-        (rc = grow(ctx, &ctx->d_hdr, &ctx->cap_hdr, size_t(nblk) * kRCap * 8)))
+        (rc = grow(ctx, &ctx->d_hdr, &ctx->cap_hdr, size_t(nblk) * kRCap * 2)))
       return rc;
+    rt_kl = static_cast<uint16_t*>(ctx->d_hdr);
   }
   if (fused) {
     if ((rc = ensure_blocks(ctx, nblk)) || (rc = ensure_fused(ctx, nblk))) return rc;
@@ -1752,8 +2074,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
     prof_mark(ctx, 2);
     prof_mark(ctx, 3);
   } else {
-    rc = launch_plan(ctx, w, nblk, o->row_start, true,
-                     sweep ? static_cast<uint64_t*>(ctx->d_hdr) : nullptr);
+    rc = launch_plan(ctx, w, nblk, o->row_start, true, rt_kl, geo.span_cap);
     if (rc) return rc;
   }
   CopyParams P;
@@ -1763,7 +2084,9 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   P.nblk = nblk;
   P.comp = w.comp;
   P.index_only = index_only ? 1 : 0;
-  P.rec_s = ctx->d_rec;
+  P.rt_pos = ctx->d_rec;
+  P.rt_kl = rt_kl;
+  P.span_cap = geo.span_cap;
   P.big_list = ctx->d_big;
   P.big_count = ctx->d_big + nblk;
   P.cnt = ctx->d_cnt;
@@ -1785,7 +2108,6 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   P.vsrc = nullptr;
   P.vtile = nullptr;
   P.bchunk = nullptr;
-  P.hdr_s = sweep ? static_cast<const uint64_t*>(ctx->d_hdr) : nullptr;
   P.tot = ctx->d_tot;
   uint64_t sw_tiles = 0;
   if (sweep) {
@@ -1818,6 +2140,8 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       F.tot = ctx->d_tot;
       hipLaunchKernelGGL(okv_decode_fused_kernel, dim3(nblk), dim3(64), 0, ctx->stream, P, F);
       ctx->f_base += nblk;
+    } else if (tile) {
+      launch_tile(ctx, P, geo);
     } else if (sweep) {
       // per-block rows + keys (one wave per block), then the value sweep
       hipLaunchKernelGGL(okv_rows_kernel, g, dim3(64), 0, ctx->stream, P);
@@ -1992,7 +2316,19 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
   if (const char* v = getenv("OKV_VALUE_SWEEP")) {
     ctx->value_sweep = uint32_t(atoi(v));
-    if (ctx->value_sweep > 7 || ctx->value_sweep == 3) {
+    if (ctx->value_sweep > 8 || ctx->value_sweep == 3) {
+      delete ctx;
+      return nullptr;
+    }
+  }
+  if (const char* v = getenv("OKV_TILE")) {  // <KiB>[x][w<threads>][s<chunks per lane run>]
+    ctx->tile_kib = uint32_t(atoi(v));
+    ctx->tile_xcd = strchr(v, 'x') != nullptr;
+    const char* w = strchr(v, 'w');
+    ctx->tile_threads = w ? uint32_t(atoi(w + 1)) : 256u;
+    const char* sg = strchr(v, 's');
+    ctx->tile_seg = sg ? uint32_t(atoi(sg + 1)) : 1u;
+    if (!tile_form(ctx->tile_kib, ctx->tile_threads, ctx->tile_seg)) {
       delete ctx;
       return nullptr;
     }

@@ -472,10 +472,12 @@ def run_decode(args, torch, okv, D):
     pass3 = tuple(w for w in roof_kernel.replace("(", " ").split() if w.startswith("okv_"))
     traffic, traffic_src = (None, None) if comp else pmc_traffic(args.config, args.mode, pass3)
 
-    # ---- CPU baseline (rank 0, N = 1 only) ---------------------------------------
+    # ---- CPU baseline (rank 0, after every rank's timing has finished) ------------
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         cpu = cpu_decode_baseline(args, seg, descs, nblk, comp)
+        if world > 1:
+            cpu["sample"] += f"; run on rank 0 of {world} after the timed region"
 
     e2e = None
     if args.e2e and rank == 0 and world == 1:
@@ -506,6 +508,13 @@ def run_decode(args, torch, okv, D):
         "kernel_ms": {k: round(v, 4) for k, v in ms.items()},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     # the same algorithmic bytes over the whole decode (count + scan +
+                     # pass 3 + launch gaps): one decode at a time, and per step with
+                     # `decodes_in_flight` decodes overlapping (the `value` clock)
+                     "frac_pass3": round(achieved / HBM_PEAK_GBS, 4),
+                     "frac_step": round(alg / (t_one / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                     "frac_step_inflight": round(alg / (t_max / args.steps) / 1e9 /
+                                                 HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": roof_kernel,
                      "algorithmic_bytes_per_launch": int(alg),
                      "timing": "HIP events around the kernel on its stream, averaged over a "

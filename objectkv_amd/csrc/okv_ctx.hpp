@@ -44,6 +44,7 @@ struct okv_ctx {
   size_t cap_blocks = 0;
   // single-pass small-block decode (okv_decode_fused_kernel)
   bool fused = true;               // OKV_DECODE_FUSED=0: passes 1-3 as separate launches
+  uint32_t fused_max = 0;          // largest fused batch: resident-capacity bound (okv_open)
   uint32_t* f_flag = nullptr;      // [nblk] look-back flags, tagged with f_epoch
   okv::Prefix* f_agg = nullptr;
   okv::Prefix* f_incl = nullptr;
@@ -66,7 +67,7 @@ struct okv_ctx {
   uint32_t gather_grid = 0;  // 0: default grid; else workgroups (OKV_GATHER_GRID)
   uint32_t gather_threads = 0;  // 0: by average block size; else 64 or 256 (OKV_GATHER_THREADS)
   bool gather_staged = true;    // 256-thread pass 3 stages value spans in LDS (OKV_GATHER_STAGED=0: off)
-  uint32_t value_sweep = 7;     // large blocks: 8 = okv_tile_kernel (source tiles); 0 = the
+  uint32_t value_sweep = 8;     // large blocks: 8 = okv_tile_kernel (source tiles); 0 = the
                                 // per-block staged pass 3; 1/2/4 = okv_rows_kernel +
                                 // okv_value_sweep_kernel with 1/2/4 tiles per workgroup,
                                 // unaligned loads; 5/6/7 = 4/2/3 tiles, aligned loads and lane
@@ -74,7 +75,7 @@ struct okv_ctx {
   uint32_t tile_kib = 16;       // okv_tile_kernel tile bytes / 1024 (OKV_TILE)
   bool tile_xcd = true;         // consecutive tiles on one XCD
   uint32_t tile_threads = 256;  // okv_tile_kernel workgroup width
-  uint32_t tile_seg = 1;        // consecutive destination chunks per lane run
+  uint32_t tile_diag = 0;       // diagnostic arms (1: no chunk pass, 2: no DMA)
   void* d_hdr = nullptr;        // [nblk x kRCap] pass-1 record key lengths (u16)
   size_t cap_hdr = 0;
   void* d_vsrc = nullptr;       // [row] value sources (sweep hand-off)

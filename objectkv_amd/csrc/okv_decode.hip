@@ -1019,20 +1019,42 @@ __global__ __launch_bounds__(256) void okv_value_sweep_kernel(SweepParams S) {
 // meet in one L2.
 // ---------------------------------------------------------------------------
 struct TileRows {
-  uint32_t kpre[kRCap + 1];  // exclusive prefix of key lengths (kpre[rows] = total)
-  uint32_t vpre[kRCap + 1];  // ... of value lengths
-  uint32_t ksb[kRCap];       // block position of key-region byte x of row r = ksb[r] + x
-  uint32_t vsb[kRCap];       // likewise for values
-  uint32_t x[4];             // owned key range [x0, x1), value range [x2, x3)
+  uint32_t pre[2][kRCap + 1];  // [key, value] exclusive prefix of lengths (pre[rows] = total)
+  uint32_t sb[2][kRCap];       // block position of region byte x of row r = sb[r] + x
+  uint32_t x[4];               // owned key range [x0, x1), value range [x2, x3)
 };
 
-template <uint32_t kT, uint32_t kNT, uint32_t kS, bool kXcd>
+// A destination chunk of a tile whose owned bytes [lo, hi) span rows or
+// padding: each row's piece from a global window (rare; kept out of line).
+__device__ __noinline__ uint4 tile_chunk_pieces(const uint8_t* seg, uint64_t seg_bytes, uint64_t off,
+                                                const uint32_t* pre, const uint32_t* sb,
+                                                uint32_t rows, uint32_t r, uint32_t x,
+                                                uint32_t lo, uint32_t hi) {
+  const uint32_t dend = min(hi, pre[rows]);
+  uint4 out = make_uint4(0, 0, 0, 0);
+  for (uint32_t d = lo; d < dend; ++r) {
+    const uint32_t e = min(dend, pre[r + 1]);
+    if (e > d) {  // bytes [d, e) of the chunk from row r
+      out = merge_bytes(out, window16(seg, seg_bytes, int64_t(off + sb[r] + x)), int32_t(d - x),
+                        int32_t(e - x));
+      d = e;
+    }
+  }
+  return out;
+}
+
+template <uint32_t kT, uint32_t kNT, bool kXcd, int kDiag = 0>
 __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tpb, uint32_t ntile) {
+  constexpr bool kDirect = kDiag == 6;  // no LDS stage: one unaligned global load per chunk
+  constexpr uint32_t kG = kT / 64 + 8;  // 64-byte destination granules per region table
   __shared__ TileRows R;
+  __shared__ uint8_t gt[2][kG];         // row holding byte max(64 g, range start)
   __shared__ uint4 stage[kT / 16 + 4];
   uint32_t L = blockIdx.x;
   if constexpr (kXcd) L = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
   if (L >= ntile) return;
+  uint64_t T[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // kDiag == 3: phase timestamps (sampled workgroups)
+  if constexpr (kDiag >= 3) T[0] = __builtin_amdgcn_s_memrealtime();
   // uniform block index (an SGPR: the loads below are scalar, all in one trip)
   const uint32_t b = __builtin_amdgcn_readfirstlane(L / tpb);
   const uint32_t t = L - b * tpb;
@@ -1051,147 +1073,218 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
   asm volatile("" ::"s"(off), "s"(c.rows), "s"(c.kbytes), "s"(c.vbytes), "s"(c.pend),
                "s"(c.status), "s"(lpre.rows), "s"(lpre.kb), "s"(lpre.vb), "s"(tpre.rows),
                "s"(tpre.kb), "s"(tpre.vb));
-  BlockMeta m;
-  m.c = c;
-  m.off = off;
-  m.B.row0 = tpre.rows + lpre.rows;
-  m.B.kb0 = tpre.kb + lpre.kb;
-  m.B.vb0 = tpre.vb + lpre.vb;
-  const bool fits = m.B.row0 + c.rows <= P.row_cap &&
-                    (P.index_only || (m.B.kb0 + round16(c.kbytes) <= P.key_cap &&
-                                      m.B.vb0 + round16(c.vbytes) <= P.val_cap));
-  m.B.st = (c.status == OKV_BLK_OK && !fits) ? int32_t(OKV_BLK_CAPACITY) : c.status;
+  if constexpr (kDiag >= 3) T[1] = __builtin_amdgcn_s_memrealtime();
+  const uint64_t row0 = tpre.rows + lpre.rows, kb0 = tpre.kb + lpre.kb, vb0 = tpre.vb + lpre.vb;
+  const bool fits = row0 + c.rows <= P.row_cap &&
+                    (P.index_only ||
+                     (kb0 + round16(c.kbytes) <= P.key_cap && vb0 + round16(c.vbytes) <= P.val_cap));
+  const int32_t st = (c.status == OKV_BLK_OK && !fits) ? int32_t(OKV_BLK_CAPACITY) : c.status;
   if (t == 0 && tid == 0) {
-    P.row_start[b] = m.B.row0;
-    if (P.key_base) P.key_base[b] = m.B.kb0;
-    if (P.val_base) P.val_base[b] = m.B.vb0;
-    P.blk_status[b] = m.B.st;
+    P.row_start[b] = row0;
+    if (P.key_base) P.key_base[b] = kb0;
+    if (P.val_base) P.val_base[b] = vb0;
+    P.blk_status[b] = st;
   }
-  const uint64_t pend = m.c.pend;
+  const uint64_t pend = c.pend;
   const uint32_t P0 = t * kT;
   // big blocks are okv_copy_kernel's (the same test as okv_count_kernel's)
-  if (m.B.st != OKV_BLK_OK || m.c.rows == 0 || m.c.rows > uint64_t(kRCap) || pend > P.span_cap ||
+  if (st != OKV_BLK_OK || c.rows == 0 || c.rows > uint64_t(kRCap) || pend > P.span_cap ||
       pend >= (uint64_t(1) << 32) || P0 >= pend)
     return;
-  const uint32_t rows = uint32_t(m.c.rows);
+  const uint32_t rows = uint32_t(c.rows), lastr = rows - 1;
   const uint32_t P1 = uint32_t(min<uint64_t>(uint64_t(P0) + kT, pend));
   const bool last_tile = P1 == pend;
   // stage = segment lines [A, E): the line before the one holding the tile's
-  // first byte (windows of a chunk begin up to 15 bytes before its first
-  // owned byte) through the line after the one holding its last byte + 15
-  const int64_t A = int64_t((m.off + P0) & ~uint64_t(15)) - 16;
-  const int64_t E = int64_t((m.off + P1 + 15) & ~uint64_t(15)) + 16;
+  // first byte (a chunk's window begins up to 15 bytes before its first owned
+  // byte) through the line after the one holding its last byte + 15
+  const int64_t A = int64_t((off + P0) & ~uint64_t(15)) - 16;
+  const int64_t E = int64_t((off + P1 + 15) & ~uint64_t(15)) + 16;
   const uint32_t np = uint32_t((E - A) >> 4);
-  if (!P.index_only) {
+  if (!P.index_only && kDiag != 2 && !kDirect) {
     const int64_t lim = int64_t(round16(P.seg_bytes));
     for (uint32_t k0 = 0; k0 < np; k0 += kNT) {
       const uint32_t i = k0 + tid;
       if (i < np) {
         int64_t a = A + (int64_t(i) << 4);
-        if (a < 0 || a + 16 > lim) a = int64_t(m.off) & ~int64_t(15);  // bytes never used
+        if (a < 0 || a + 16 > lim) a = int64_t(off) & ~int64_t(15);  // bytes never used
         __builtin_amdgcn_global_load_lds(P.seg + a, OKV_LDS_PTR(stage + k0 + (tid & ~63u)), 16,
                                          0, 0);
       }
     }
   }
+  if constexpr (kDiag >= 3) T[2] = __builtin_amdgcn_s_memrealtime();
   // row table (wave 0, lane r = row r) while the tile is in flight
   if (tid < 64) {
     const bool live = lane < rows;
-    uint32_t nxt = __shfl_down(rec, 1, 64);
-    if (lane == rows - 1) nxt = uint32_t(pend);
+    uint32_t nxt = __builtin_amdgcn_update_dpp(0u, rec, 0x130, 0xf, 0xf, false);  // rec[lane + 1]
+    if (lane == lastr) nxt = uint32_t(pend);
     const uint32_t k = live ? kl : 0u, v = live ? nxt - rec - 6 - kl : 0u;
-    const uint32_t ki = wave_incl_scan32(k, int(lane)), vi = wave_incl_scan32(v, int(lane));
+    const uint32_t ki = wave_scan_dpp(k), vi = wave_scan_dpp(v);
     const uint32_t kp = ki - k, vp = vi - v;
     const uint32_t ks = rec + 6, vs = rec + 6 + k;  // block positions of the key / value
     if (live) {
-      R.kpre[lane] = kp;
-      R.vpre[lane] = vp;
-      R.ksb[lane] = ks - kp;
-      R.vsb[lane] = vs - vp;
-      if (lane == rows - 1) {
-        R.kpre[rows] = ki;
-        R.vpre[rows] = vi;
+      R.pre[0][lane] = kp;
+      R.pre[1][lane] = vp;
+      R.sb[0][lane] = ks - kp;
+      R.sb[1][lane] = vs - vp;
+      if (lane == lastr) {
+        R.pre[0][rows] = ki;
+        R.pre[1][rows] = vi;
       }
     }
     if (t == 0 && live) {  // the block's SoA row index
-      const uint64_t g = m.B.row0 + lane;
+      const uint64_t g = row0 + lane;
       P.key_len[g] = uint16_t(k);
       P.val_len[g] = v;
       if (P.index_only) {
-        P.key_off[g] = m.off + ks;
-        P.val_off[g] = m.off + vs;
+        P.key_off[g] = off + ks;
+        P.val_off[g] = off + vs;
       } else {
-        P.key_off[g] = m.B.kb0 + kp;
-        P.val_off[g] = m.B.vb0 + vp;
+        P.key_off[g] = kb0 + kp;
+        P.val_off[g] = vb0 + vp;
       }
     }
-    // the owned ranges: [first byte whose source is >= P0, same for P1); the
-    // last tile also owns the 16-byte padding after the region
-    const uint32_t KT = __shfl(ki, int(rows - 1), 64), VT = __shfl(vi, int(rows - 1), 64);
-    auto first_at = [&](uint32_t len, uint32_t src, uint32_t pre, uint32_t tot, uint32_t Q) {
-      const uint64_t mk = __ballot(live && len && src + len > Q);
-      if (!mk) return tot;
-      const int j = __ffsll(static_cast<unsigned long long>(mk)) - 1;
-      const uint32_t s = __shfl(src, j, 64), pr = __shfl(pre, j, 64);
-      return Q > s ? pr + (Q - s) : pr;
-    };
-    const uint32_t kx0 = first_at(k, ks, kp, KT, P0), vx0 = first_at(v, vs, vp, VT, P0);
-    const uint32_t kx1 = last_tile ? uint32_t(round16(KT)) : first_at(k, ks, kp, KT, P1);
-    const uint32_t vx1 = last_tile ? uint32_t(round16(VT)) : first_at(v, vs, vp, VT, P1);
-    if (lane == 0) {
-      R.x[0] = kx0;
-      R.x[1] = kx1;
-      R.x[2] = vx0;
-      R.x[3] = vx1;
+    if (!P.index_only) {
+      // the owned ranges: [first byte whose source is >= P0, same for P1); the
+      // last tile also owns the 16-byte padding after the region
+      const uint32_t KT = __builtin_amdgcn_readlane(ki, lastr);
+      const uint32_t VT = __builtin_amdgcn_readlane(vi, lastr);
+      auto first_at = [&](uint32_t len, uint32_t src, uint32_t pr, uint32_t tot, uint32_t Q) {
+        const uint64_t mk = __ballot(live && len && src + len > Q);
+        if (!mk) return tot;
+        const uint32_t j = uint32_t(__ffsll(static_cast<unsigned long long>(mk)) - 1);
+        const uint32_t s0 = __builtin_amdgcn_readlane(src, j), p0 = __builtin_amdgcn_readlane(pr, j);
+        return Q > s0 ? p0 + (Q - s0) : p0;
+      };
+      uint32_t X[4];
+      X[0] = first_at(k, ks, kp, KT, P0);
+      X[1] = last_tile ? uint32_t(round16(KT)) : first_at(k, ks, kp, KT, P1);
+      X[2] = first_at(v, vs, vp, VT, P0);
+      X[3] = last_tile ? uint32_t(round16(VT)) : first_at(v, vs, vp, VT, P1);
+      if (lane == 0) {
+        R.x[0] = X[0];
+        R.x[1] = X[1];
+        R.x[2] = X[2];
+        R.x[3] = X[3];
+      }
+      // granule tables: gt[reg][g - (X0 >> 6)] = row holding byte max(64 g, X0);
+      // granules past the last row's bytes (padding) keep the preset lastr
+#pragma unroll
+      for (uint32_t reg = 0; reg < 2; ++reg) {
+        const uint32_t X0 = X[2 * reg], X1 = X[2 * reg + 1];
+        if (X1 <= X0) continue;
+        const uint32_t g0 = X0 >> 6, gl = (X1 - 1) >> 6;
+        for (uint32_t g = g0 + lane; g <= gl; g += 64) gt[reg][g - g0] = uint8_t(lastr);
+        const uint32_t pr = reg ? vp : kp, ln = reg ? v : k;
+        if (live && ln) {
+          const uint32_t e = pr + ln;
+          if (pr <= X0 && X0 < e) gt[reg][0] = uint8_t(lane);
+          const uint32_t gs = max(g0 + 1, (pr + 63) >> 6), ge = min(gl, ((e + 63) >> 6) - 1);
+          for (uint32_t g = gs; g <= ge; ++g) gt[reg][g - g0] = uint8_t(lane);
+        }
+      }
     }
   }
+  if constexpr (kDiag >= 3) T[3] = __builtin_amdgcn_s_memrealtime();
   if (P.index_only) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (kDiag >= 3) T[4] = __builtin_amdgcn_s_memrealtime();
   const uint32_t kx0 = R.x[0], kx1 = R.x[1], vx0 = R.x[2], vx1 = R.x[3];
   const uint32_t nk = kx1 > kx0 ? ((kx1 + 15) >> 4) - (kx0 >> 4) : 0u;
   const uint32_t nv = vx1 > vx0 ? ((vx1 + 15) >> 4) - (vx0 >> 4) : 0u;
-  const int64_t sbias = int64_t(m.off) - A;  // stage byte of block position s = s + sbias
-  const uint32_t lastr = rows - 1;
-  // lane work: kS consecutive destination chunks (one row search per run of
-  // kS chunks; rows only move forward inside it)
-  const uint32_t uk = (nk + kS - 1) / kS, uv = (nv + kS - 1) / kS;
-  for (uint32_t j = tid; j < uk + uv; j += kNT) {
-    const bool isv = j >= uk;
-    const uint32_t* pre = isv ? R.vpre : R.kpre;
-    const uint32_t* sb = isv ? R.vsb : R.ksb;
-    const uint32_t X0 = isv ? vx0 : kx0, X1 = isv ? vx1 : kx1;
-    const uint32_t tot = pre[rows];
-    const uint32_t c0 = (X0 >> 4) + (isv ? j - uk : j) * kS;
-    uint8_t* const arena = isv ? P.val_arena + m.B.vb0 : P.key_arena + m.B.kb0;
-    uint32_t r = row_of(pre, lastr, max(c0 << 4, X0));
+  const uint32_t sbias = uint32_t(int64_t(off) - A);  // stage byte of block position s: s + sbias
+  if (kDiag == 1) return;  // diagnostic: metadata + DMA + row table only
+  if constexpr (kDirect) {
+    constexpr uint32_t kU = (kT / 16 + 8 + kNT - 1) / kNT;  // chunk slots per lane
+    uint4 v[kU];
+    uint32_t xs[kU], los[kU], his[kU], regs[kU];
+    bool slow[kU];
 #pragma unroll
-    for (uint32_t k = 0; k < kS; ++k) {
-      const uint32_t x = (c0 + k) << 4;
+    for (uint32_t u = 0; u < kU; ++u) {  // every load issued before any store
+      const uint32_t j = tid + u * kNT;
+      his[u] = 0;
+      los[u] = 0;
+      slow[u] = false;
+      v[u] = make_uint4(0, 0, 0, 0);
+      if (j >= nk + nv) continue;
+      const uint32_t reg = j >= nk;
+      const uint32_t X0 = reg ? vx0 : kx0, X1 = reg ? vx1 : kx1;
+      const uint32_t x = ((X0 >> 4) + (reg ? j - nk : j)) << 4;
       const uint32_t lo = max(x, X0), hi = min(x + 16, X1);
-      if (lo >= hi) break;  // past the owned range
-      const uint32_t dend = min(hi, tot);
+      const uint32_t* pre = R.pre[reg];
+      uint32_t r = gt[reg][(lo >> 6) - (X0 >> 6)];
       while (r < lastr && pre[r + 1] <= lo) ++r;
-      uint4 out;
-      if (lo == x && dend == x + 16 && pre[r + 1] >= x + 16) {  // inside row r
-        out = load16_lds_b128(stage, uint32_t(int64_t(sb[r]) + x + sbias));
-      } else {
-        out = make_uint4(0, 0, 0, 0);
-        uint32_t rr = r;
-        for (uint32_t d = lo; d < dend; ++rr) {
-          const uint32_t e = min(dend, pre[rr + 1]);
-          if (e > d) {  // bytes [d, e) of the chunk from row rr
-            const uint4 w = load16_lds_b128(stage, uint32_t(int64_t(sb[rr]) + x + sbias));
-            out = merge_bytes(out, w, int32_t(d - x), int32_t(e - x));
-            d = e;
-          }
-        }
-      }
-      if (lo == x && hi == x + 16)
-        *reinterpret_cast<uint4*>(arena + x) = out;
+      xs[u] = x;
+      los[u] = lo;
+      his[u] = hi;
+      regs[u] = reg | (r << 1);
+      if (lo == x && hi == x + 16 && pre[r + 1] >= x + 16)
+        v[u] = *reinterpret_cast<const uint4*>(P.seg + off + R.sb[reg][r] + x);
       else
-        store_partial(arena + x, out, lo - x, hi - x);
+        slow[u] = true;
     }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u)
+      if (slow[u])
+        v[u] = tile_chunk_pieces(P.seg, P.seg_bytes, off, R.pre[regs[u] & 1], R.sb[regs[u] & 1],
+                                 rows, regs[u] >> 1, xs[u], los[u], his[u]);
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      if (his[u] <= los[u]) continue;
+      uint8_t* dst = ((regs[u] & 1) ? P.val_arena + vb0 : P.key_arena + kb0) + xs[u];
+      if (los[u] == xs[u] && his[u] == xs[u] + 16)
+        *reinterpret_cast<uint4*>(dst) = v[u];
+      else
+        store_partial(dst, v[u], los[u] - xs[u], his[u] - xs[u]);
+    }
+  } else
+  for (uint32_t j = tid; j < nk + nv; j += kNT) {
+    const uint32_t reg = j >= nk;
+    const uint32_t X0 = reg ? vx0 : kx0, X1 = reg ? vx1 : kx1;
+    const uint32_t x = ((X0 >> 4) + (reg ? j - nk : j)) << 4;
+    const uint32_t lo = max(x, X0), hi = min(x + 16, X1);
+    const uint32_t* pre = R.pre[reg];
+    const uint32_t* sb = R.sb[reg];
+    uint32_t r = gt[reg][(lo >> 6) - (X0 >> 6)];
+    while (r < lastr && pre[r + 1] <= lo) ++r;
+    uint8_t* dst = (reg ? P.val_arena + vb0 : P.key_arena + kb0) + x;
+    if (lo == x && hi == x + 16 && pre[r + 1] >= x + 16) {  // the common chunk: inside row r
+      if constexpr (kDiag == 5) {  // diagnostic: the lookup, no data read
+        *reinterpret_cast<uint4*>(dst) = make_uint4(r, x, 0, 0);
+        continue;
+      }
+      const uint4 w = load16_lds_b128(stage, sb[r] + x + sbias);
+      if constexpr (kDiag == 4) {  // diagnostic: no stores
+        asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));
+        continue;
+      }
+      *reinterpret_cast<uint4*>(dst) = w;
+      continue;
+    }
+    const uint32_t dend = min(hi, pre[rows]);
+    uint4 out = make_uint4(0, 0, 0, 0);
+    for (uint32_t d = lo; d < dend; ++r) {
+      const uint32_t e = min(dend, pre[r + 1]);
+      if (e > d) {  // bytes [d, e) of the chunk from row r
+        out = merge_bytes(out, load16_lds_b128(stage, sb[r] + x + sbias), int32_t(d - x),
+                          int32_t(e - x));
+        d = e;
+      }
+    }
+    if (lo == x && hi == x + 16)
+      *reinterpret_cast<uint4*>(dst) = out;
+    else
+      store_partial(dst, out, lo - x, hi - x);
+  }
+  if constexpr (kDiag >= 3) {
+    T[5] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    T[6] = __builtin_amdgcn_s_memrealtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    T[7] = __builtin_amdgcn_s_memrealtime();
+    if ((L & 255) == 0 && tid == 0)
+      for (int k = 0; k < 8; ++k) P.vsrc[(L >> 8) * 8 + k] = T[k];
   }
 }
 
@@ -1977,33 +2070,37 @@ TileGeo tile_geo(const okv_ctx* ctx, uint64_t seg_bytes, uint32_t nblk, bool ind
   return {uint32_t(tpb), tpb * kT};
 }
 
-template <uint32_t kT, uint32_t kNT, uint32_t kS, bool kXcd>
+template <uint32_t kT, uint32_t kNT, bool kXcd, int kDiag>
 void launch_tile_t(hipStream_t s, const CopyParams& P, uint32_t tpb, uint32_t ntile) {
   const uint32_t grid = kXcd ? ((ntile + 7u) & ~7u) : ntile;
-  hipLaunchKernelGGL((okv_tile_kernel<kT, kNT, kS, kXcd>), dim3(grid), dim3(kNT), 0, s, P, tpb,
+  hipLaunchKernelGGL((okv_tile_kernel<kT, kNT, kXcd, kDiag>), dim3(grid), dim3(kNT), 0, s, P, tpb,
                      ntile);
 }
 typedef void (*TileLaunch)(hipStream_t, const CopyParams&, uint32_t, uint32_t);
 struct TileForm {
-  uint32_t kib, threads, seg;
+  uint32_t kib, threads, diag;
   TileLaunch x, plain;
 };
-#define OKV_TILE_FORM(K, N, S)                                                        \
-  TileForm {                                                                          \
-    K, N, S, launch_tile_t<K * 1024, N, S, true>, launch_tile_t<K * 1024, N, S, false> \
+#define OKV_TILE_FORM(K, N, D)                                                              \
+  TileForm {                                                                                \
+    K, N, D, launch_tile_t<K * 1024, N, true, D>, launch_tile_t<K * 1024, N, false, D>      \
   }
-const TileForm kTileForms[] = {
-    OKV_TILE_FORM(16, 256, 1), OKV_TILE_FORM(16, 256, 2), OKV_TILE_FORM(16, 256, 4),
-    OKV_TILE_FORM(8, 256, 1),  OKV_TILE_FORM(8, 256, 2),  OKV_TILE_FORM(32, 256, 1),
-    OKV_TILE_FORM(32, 256, 4), OKV_TILE_FORM(16, 512, 1), OKV_TILE_FORM(32, 512, 1),
-    OKV_TILE_FORM(32, 512, 2), OKV_TILE_FORM(4, 256, 1)};
-const TileForm* tile_form(uint32_t kib, uint32_t threads, uint32_t seg) {
+const TileForm kTileForms[] = {OKV_TILE_FORM(16, 256, 0), OKV_TILE_FORM(8, 256, 0),
+                               OKV_TILE_FORM(32, 256, 0), OKV_TILE_FORM(16, 512, 0),
+                               OKV_TILE_FORM(32, 512, 0), OKV_TILE_FORM(4, 256, 0),
+                               OKV_TILE_FORM(16, 256, 1), OKV_TILE_FORM(16, 256, 2),
+                               OKV_TILE_FORM(32, 512, 1), OKV_TILE_FORM(32, 512, 2),
+                               OKV_TILE_FORM(16, 256, 3), OKV_TILE_FORM(16, 256, 4),
+                               OKV_TILE_FORM(16, 256, 5), OKV_TILE_FORM(16, 256, 6),
+                               OKV_TILE_FORM(8, 256, 6), OKV_TILE_FORM(4, 256, 6),
+                               OKV_TILE_FORM(32, 512, 6), OKV_TILE_FORM(16, 512, 6)};
+const TileForm* tile_form(uint32_t kib, uint32_t threads, uint32_t diag) {
   for (const TileForm& f : kTileForms)
-    if (f.kib == kib && f.threads == threads && f.seg == seg) return &f;
+    if (f.kib == kib && f.threads == threads && f.diag == diag) return &f;
   return nullptr;
 }
 void launch_tile(okv_ctx* ctx, const CopyParams& P, const TileGeo& g) {
-  const TileForm* f = tile_form(ctx->tile_kib, ctx->tile_threads, ctx->tile_seg);
+  const TileForm* f = tile_form(ctx->tile_kib, ctx->tile_threads, ctx->tile_diag);
   (ctx->tile_xcd ? f->x : f->plain)(ctx->stream, P, g.tpb, P.nblk * g.tpb);
 }
 
@@ -2053,7 +2150,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   prof_mark(ctx, 1);
   // small blocks: passes 1-3 in one launch (okv_decode_fused_kernel)
   const bool fused =
-      ctx->fused && nblk && nblk <= kFusedMaxBlocks && gather_threads(ctx, w, nblk) == 64;
+      ctx->fused && nblk && nblk <= ctx->fused_max && gather_threads(ctx, w, nblk) == 64;
   // large blocks: the source-tile pass (okv_tile_kernel); value_sweep 1-7 are
   // the round-2 forms (row pass + address-ordered value sweep)
   const bool large = nblk && !fused && gather_threads(ctx, w, nblk) == 256;
@@ -2139,8 +2236,18 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       F.epoch = ctx->f_epoch;
       F.tot = ctx->d_tot;
       hipLaunchKernelGGL(okv_decode_fused_kernel, dim3(nblk), dim3(64), 0, ctx->stream, P, F);
-      ctx->f_base += nblk;
+      const hipError_t le = hipGetLastError();
+      if (le != hipSuccess) {
+        // nothing ran: the counters keep their value, so f_base must too
+        return set_err(ctx, OKV_E_HIP, "okv_decode_fused_kernel launch", le);
+      }
+      ctx->f_base += nblk;  // both counters advanced by nblk once the grid completes
     } else if (tile) {
+      if (ctx->tile_diag >= 3) {  // phase probe: 8 timestamps per 256th workgroup
+        const size_t n = (size_t(nblk) * geo.tpb / 256 + 1) * 64;
+        if ((rc = grow(ctx, &ctx->d_vsrc, &ctx->cap_vsrc, n))) return rc;
+        P.vsrc = static_cast<uint64_t*>(ctx->d_vsrc);
+      }
       launch_tile(ctx, P, geo);
     } else if (sweep) {
       // per-block rows + keys (one wave per block), then the value sweep
@@ -2313,6 +2420,19 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   }
   if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
   if (const char* v = getenv("OKV_DECODE_FUSED")) ctx->fused = atoi(v) != 0;
+  // The fused kernel's blocks wait for the last-arriving block of their grid,
+  // so every block must be resident at once: cap the batch at a quarter of
+  // the device's resident capacity for it (room for other contexts' grids on
+  // the same device), and at kFusedMaxBlocks.
+  {
+    int ncu = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, okv_decode_fused_kernel, 64, 0) !=
+            hipSuccess)
+      ncu = per_cu = 0;
+    ctx->fused_max = std::min<uint32_t>(kFusedMaxBlocks, uint32_t(ncu) * uint32_t(per_cu) / 4);
+    if (ctx->fused_max == 0) ctx->fused = false;
+  }
   if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
   if (const char* v = getenv("OKV_VALUE_SWEEP")) {
     ctx->value_sweep = uint32_t(atoi(v));
@@ -2321,14 +2441,14 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
       return nullptr;
     }
   }
-  if (const char* v = getenv("OKV_TILE")) {  // <KiB>[x][w<threads>][s<chunks per lane run>]
+  if (const char* v = getenv("OKV_TILE")) {  // <KiB>[x][w<threads>]
     ctx->tile_kib = uint32_t(atoi(v));
     ctx->tile_xcd = strchr(v, 'x') != nullptr;
     const char* w = strchr(v, 'w');
     ctx->tile_threads = w ? uint32_t(atoi(w + 1)) : 256u;
-    const char* sg = strchr(v, 's');
-    ctx->tile_seg = sg ? uint32_t(atoi(sg + 1)) : 1u;
-    if (!tile_form(ctx->tile_kib, ctx->tile_threads, ctx->tile_seg)) {
+    const char* dg = strchr(v, 'd');
+    ctx->tile_diag = dg ? uint32_t(atoi(dg + 1)) : 0u;
+    if (!tile_form(ctx->tile_kib, ctx->tile_threads, ctx->tile_diag)) {
       delete ctx;
       return nullptr;
     }
@@ -2501,6 +2621,13 @@ int okv_hash_blocks(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes,
       OKV_HIP(hipMemcpyAsync(hashes, d_h, size_t(nblk) * 8, hipMemcpyDeviceToHost, ctx->stream));
   }
   if (!(flags & OKV_F_ASYNC)) OKV_HIP(hipStreamSynchronize(ctx->stream));
+  return OKV_OK;
+}
+
+// Diagnostic (tile-pass phase probe, OKV_TILE=...d3): copy the probe buffer to host.
+int okv_debug_probe(okv_ctx* ctx, void* host, size_t bytes) {
+  if (!ctx || !ctx->d_vsrc) return OKV_E_ARG;
+  OKV_HIP(hipMemcpy(host, ctx->d_vsrc, std::min(bytes, ctx->cap_vsrc), hipMemcpyDeviceToHost));
   return OKV_OK;
 }
 

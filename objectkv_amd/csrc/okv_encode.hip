@@ -953,7 +953,8 @@ __device__ __forceinline__ void lds_copy_field(uint32_t* img, uint32_t d, const 
 }
 
 template <uint32_t IMG, int V = 0>  // V: diagnostic ablation (OKV_ENC_VARIANT 4: no hash,
-                                   // 5: headers only, 6: loads without LDS writes)
+                                   // 5: headers only, 6: loads without LDS writes;
+                                   // 7: row positions by a workgroup scan, no pl reads)
 __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb,
                                                                     uint32_t G) {
   __shared__ uint4 img4[IMG / 16];
@@ -978,9 +979,40 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P
       bbase[t] = P.pbase[k0 + t];  // one trip with first[] and desc[]
     }
   }
+  __shared__ uint32_t s_wt[2][kThreads / 64];  // V == 7: per-wave record-size totals
   __syncthreads();
   const uint64_t R0 = bfirst[0], R1 = bfirst[g];
-  for (uint64_t r = R0 + threadIdx.x; r < R1; r += kThreads) {
+  uint32_t carry = 0;  // V == 7: image bytes of the rows before this pass
+  for (uint64_t base = R0; base < R1; base += kThreads) {  // uniform trip count (V == 7 barriers)
+    const uint64_t r = base + threadIdx.x;
+    const bool live = r < R1;
+    uint32_t kl = 0, vl = 0;
+    uint64_t ko = 0, vo = 0;
+    if (live) {
+      kl = P.key_len[r];
+      vl = P.val_len[r];
+      ko = P.key_off[r];
+      vo = P.val_off[r];
+    }
+    uint32_t srel = 0;  // V == 7: region-relative start of record r's row stream
+    if constexpr (V == 7) {
+      // exclusive scan of the record sizes in row order (< IMG bytes: u32)
+      const uint32_t sz = live ? 6 + kl + vl : 0u;
+      const uint32_t inc = wave_scan_dpp(sz);
+      const uint32_t wave = threadIdx.x >> 6, par = uint32_t((base - R0) / kThreads) & 1;
+      if ((threadIdx.x & 63) == 63) s_wt[par][wave] = inc;
+      __syncthreads();
+      uint32_t before = carry, tot = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kThreads / 64; ++w) {
+        const uint32_t t = s_wt[par][w];
+        before += w < wave ? t : 0u;
+        tot += t;
+      }
+      srel = before + inc - sz;
+      carry += tot;
+    }
+    if (!live) continue;
     uint32_t lo = 0, hi = g;  // block of row r
     while (hi - lo > 1) {
       const uint32_t m = (lo + hi) >> 1;
@@ -989,9 +1021,8 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P
       else
         hi = m;
     }
-    const uint32_t d = uint32_t(brel[lo] + Pg(P.pl, P.tp, int64_t(r) - 1) - bbase[lo]);
-    const uint32_t kl = P.key_len[r], vl = P.val_len[r];
-    const uint64_t ko = P.key_off[r], vo = P.val_off[r];
+    const uint32_t d = V == 7 ? uint32_t(brel[lo] + srel - (bbase[lo] - bbase[0]))
+                              : uint32_t(brel[lo] + Pg(P.pl, P.tp, int64_t(r) - 1) - bbase[lo]);
     if (V == 5) {
       lds_or16(img, d, make_uint4(kl | (vl << 16), vl >> 16, 0, 0));
     } else if (V == 6 && kl <= 64 && vl <= 64) {
@@ -1572,10 +1603,11 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
     else if (img == 12288)
       hipLaunchKernelGGL(okv_enc_pack_lds_kernel<12288>, dim3(ceil_div(pl.nb, GL)),
                          dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
-    else if (EV >= 4 && EV <= 6) {
+    else if (EV >= 4 && EV <= 7) {
       auto* kern = EV == 4   ? okv_enc_pack_lds_kernel<kImage, 4>
                    : EV == 5 ? okv_enc_pack_lds_kernel<kImage, 5>
-                             : okv_enc_pack_lds_kernel<kImage, 6>;
+                   : EV == 6 ? okv_enc_pack_lds_kernel<kImage, 6>
+                             : okv_enc_pack_lds_kernel<kImage, 7>;
       hipLaunchKernelGGL(kern, dim3(ceil_div(pl.nb, GL)), dim3(kThreads), 0, ctx->stream, pp,
                          pl.nb, uint32_t(GL));
     } else

@@ -218,6 +218,19 @@ __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x, int lane) {
   return x;
 }
 
+// Wave64 inclusive scan by DPP (no LDS round trips): Hillis-Steele inside
+// each 16-lane row, then row 0 -> 1, 2 -> 3 (row_bcast:15) and the first
+// half's total into the second (row_bcast:31).  All 64 lanes must be active.
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x) {
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, true);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, true);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, true);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, true);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+
 // Wave64 inclusive scan of a 64-bit value (DPP-free shuffle form).
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x, int lane) {
 #pragma unroll

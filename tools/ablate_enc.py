@@ -31,13 +31,21 @@ nb = -(-n // 42) + 1
 out = dict(seg=torch.empty(nb * 4096 + nb * 60 + 4096, dtype=torch.uint8, device=dev))
 variants = [(int(v), int(i)) for v in args.variants.split(",") for i in args.images.split(",")]
 res = {v: [] for v in variants}
+ref = None
 for rep in range(args.reps):
     for v in variants:
         os.environ["OKV_ENC_VARIANT"] = str(v[0])
         os.environ["OKV_ENC_IMAGE"] = str(v[1])
         enc.profile(True)
         enc.profile_reset_encode()
-        enc.encode_device(rows, n, out, strict_go=False, close=False)
+        eo = enc.encode_device(rows, n, out, strict_go=False, close=False)
+        if rep == 0 and v[0] in (0, 7):  # product-equivalent variants: the same file bytes
+            fb = int(eo.data_bytes + eo.meta_bytes)
+            if ref is None:
+                ref = out["seg"][:fb].clone()
+            else:
+                print(f"variant {v}: {'EQUAL' if torch.equal(ref, out['seg'][:fb]) else 'DIFFER'} "
+                      f"to variant {variants[0]}", flush=True)
         ph, _ = enc.profile_read_encode()
         if rep:
             res[v].append(ph)

@@ -31,7 +31,9 @@
 extern "C" {
 #endif
 
-#define OKV_ABI_VERSION 2 /* 2: okv_encode_opts.bloom / bloom_len */
+#define OKV_ABI_VERSION 3 /* 2: okv_encode_opts.bloom / bloom_len, and okv_profile_read writes
+                             4 doubles (ms[4]: the zstd stage slot was added);
+                             3: okv_open_ex / okv_open_opts */
 
 /* ---- return codes (int) -------------------------------------------------- */
 #define OKV_OK 0
@@ -123,6 +125,22 @@ typedef struct okv_ctx okv_ctx;
  * unless okv_open_on_stream is used (stream = a hipStream_t, opaque here). */
 okv_ctx *okv_open(int device);
 okv_ctx *okv_open_on_stream(int device, void *stream);
+
+/* Context options (okv_open_ex).  The library reads no environment variables:
+ * every choice a caller can make is here. */
+#define OKV_OPEN_NO_FUSED 1u      /* batches of <= 512 small blocks: three launches (count, scan,
+                                     gather) instead of the single-pass kernel, whose workgroups
+                                     wait for each other -- for devices whose compute slots other
+                                     work may hold; the outputs are identical */
+#define OKV_OPEN_ZSTD_ONE_PASS 2u /* zstd blocks: the one-wave-per-block decoder for every block
+                                     (one launch, no host synchronisation between stages: lower
+                                     latency for a few blocks); outputs identical */
+typedef struct okv_open_opts {
+  uint32_t size;  /* sizeof(okv_open_opts) */
+  uint32_t flags; /* OKV_OPEN_* */
+} okv_open_opts;
+/* stream may be NULL (the context creates its own); opts may be NULL (defaults). */
+okv_ctx *okv_open_ex(int device, void *stream, const okv_open_opts *opts);
 void okv_close(okv_ctx *ctx);
 const char *okv_last_error(const okv_ctx *ctx);
 void *okv_stream(const okv_ctx *ctx);
@@ -333,7 +351,8 @@ int okv_merge_rows(okv_ctx *ctx, const okv_merge_src *srcs, uint32_t nsrc,
  * okv_profile_read synchronises the stream and returns the summed
  * milliseconds per stage, ms[4] = {pass 1 count, pass 2 scan, pass 3 gather
  * (+ big-block copy / index), zstd decompression (0 for uncompressed)}, and
- * the number of decode calls timed. */
+ * the number of decode calls timed.  ms must hold 4 doubles (ABI 2 and later;
+ * ABI 1 wrote 3). */
 int okv_profile(okv_ctx *ctx, int enable);
 int okv_profile_read(okv_ctx *ctx, double *ms, uint64_t *calls);
 

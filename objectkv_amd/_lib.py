@@ -10,13 +10,17 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libokv_sst.so")
+# The product library; OKV_ABLATE=1 loads the ablation build instead (the
+# measured alternative kernel forms and their OKV_* knobs, tools/ablate*.py).
+LIB_PATH = os.path.join(_HERE, "libokv_sst_ablate.so" if os.environ.get("OKV_ABLATE") == "1"
+                        else "libokv_sst.so")
 
 # ---- constants (include/okv_sst.h) -------------------------------------------
 OKV_OK, OKV_E_ARG, OKV_E_HIP, OKV_E_CAPACITY, OKV_E_NOMEM, OKV_E_NODEV = 0, -1, -2, -3, -4, -5
 BLK_OK, BLK_EOF, BLK_SHORT, BLK_PANIC, BLK_UNSUPPORTED, BLK_CAPACITY = 0, 1, 2, 3, 4, 5
 COMP_NONE, COMP_ZSTD, COMP_LZ4 = 0, 1, 2
 F_DEVICE_PTRS, F_INDEX_ONLY, F_ASYNC, F_NO_CLOSE = 1, 2, 4, 8
+OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS = 1, 2
 # SegmentWriter sentinels (okv_sst.h OKV_W_*)
 W_KEY_TOO_LARGE, W_VALUE_TOO_LARGE, W_CLOSED, W_INVALID_KEY = -101, -102, -103, -104
 W_NIL_WRITER, W_UNSUPPORTED, W_NO_ROWS = -105, -106, -107
@@ -27,7 +31,7 @@ M_EOF = 1
 
 # exported symbols declared by include/*.h (checked by tests/test_abi.py)
 SYMBOLS = [
-    "okv_open", "okv_open_on_stream", "okv_close", "okv_last_error", "okv_stream", "okv_sync",
+    "okv_open", "okv_open_on_stream", "okv_open_ex", "okv_close", "okv_last_error", "okv_stream", "okv_sync",
     "okv_abi_version", "okv_decode_plan", "okv_decode_blocks", "okv_decode_totals",
     "okv_xxh64", "okv_hash_blocks", "okv_device_alloc", "okv_device_free", "okv_host_alloc",
     "okv_host_free", "okv_memcpy", "okv_profile", "okv_profile_read",
@@ -44,6 +48,10 @@ SYMBOLS = [
     "okv_reader_get_range", "okv_reader_close", "okv_reader_free", "okv_reader_row_iter",
     "okv_iter_next", "okv_iter_seek", "okv_iter_free",
 ]
+
+
+class OpenOpts(C.Structure):
+    _fields_ = [("size", C.c_uint32), ("flags", C.c_uint32)]
 
 
 class Row(C.Structure):
@@ -110,10 +118,11 @@ class MergeOut(C.Structure):
 _lib = None
 
 
-def build():
-    """Compile libokv_sst.so for gfx950 (hipcc) in-tree."""
+def build(ablate=True):
+    """Compile libokv_sst.so (and the ablation build) for gfx950 (hipcc) in-tree."""
     import subprocess
-    subprocess.run(["make", "-s", "-C", os.path.join(_HERE, "csrc")], check=True)
+    subprocess.run(["make", "-s", "-j4", "-C", os.path.join(_HERE, "csrc")] +
+                   (["ablate"] if ablate else []), check=True)
 
 
 def lib():
@@ -138,6 +147,7 @@ def lib():
     sig = {
         "okv_open": (p, [i32]),
         "okv_open_on_stream": (p, [i32, p]),
+        "okv_open_ex": (p, [i32, p, C.POINTER(OpenOpts)]),
         "okv_close": (None, [p]),
         "okv_last_error": (C.c_char_p, [p]),
         "okv_stream": (p, [p]),

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -45,6 +46,7 @@ struct okv_ctx {
   // single-pass small-block decode (okv_decode_fused_kernel)
   bool fused = true;               // OKV_DECODE_FUSED=0: passes 1-3 as separate launches
   uint32_t fused_max = 0;          // largest fused batch: resident-capacity bound (okv_open)
+  bool zstd_one_pass = false;      // OKV_OPEN_ZSTD_ONE_PASS: every zstd block by the general kernel
   uint32_t* f_flag = nullptr;      // [nblk] look-back flags, tagged with f_epoch
   okv::Prefix* f_agg = nullptr;
   okv::Prefix* f_incl = nullptr;
@@ -112,6 +114,18 @@ struct okv_ctx {
 };
 
 namespace okv {
+
+// A/B and diagnostic knobs: read from the environment in the ablation build
+// only (-DOKV_ABLATE, libokv_sst_ablate.so); the product library never reads
+// the environment, so its kernels do not change with a process's settings.
+inline const char* knob(const char* name) {
+#ifdef OKV_ABLATE
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 inline int set_err(okv_ctx* c, int code, const char* what, hipError_t e = hipSuccess) {
   if (c) {

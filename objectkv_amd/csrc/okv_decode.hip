@@ -1022,7 +1022,33 @@ struct TileRows {
   uint32_t pre[2][kRCap + 1];  // [key, value] exclusive prefix of lengths (pre[rows] = total)
   uint32_t sb[2][kRCap];       // block position of region byte x of row r = sb[r] + x
   uint32_t x[4];               // owned key range [x0, x1), value range [x2, x3)
+  // kDiag == 7 (value runs): whole value chunks in units of <= 64 inside one
+  // row piece {dest chunk, stage byte of its first chunk, count}, and the
+  // value chunks that mix rows, padding or a neighbouring tile's bytes
+  uint32_t unit[3][96];
+  uint32_t bnd[kRCap + 2];
+  uint32_t nunit, nbnd;
 };
+
+// 16 bytes at byte s (0..15, wave-uniform) of the 32-byte window (x, y): a
+// scalar branch picks the dwords, then 4 v_alignbyte.
+__device__ __forceinline__ uint4 funnel_u(const uint4& x, const uint4& y, uint32_t s) {
+  const uint32_t r = s & 3;
+  switch (s >> 2) {
+    case 0:
+      return make_uint4(funnel(x.y, x.x, r), funnel(x.z, x.y, r), funnel(x.w, x.z, r),
+                        funnel(y.x, x.w, r));
+    case 1:
+      return make_uint4(funnel(x.z, x.y, r), funnel(x.w, x.z, r), funnel(y.x, x.w, r),
+                        funnel(y.y, y.x, r));
+    case 2:
+      return make_uint4(funnel(x.w, x.z, r), funnel(y.x, x.w, r), funnel(y.y, y.x, r),
+                        funnel(y.z, y.y, r));
+    default:
+      return make_uint4(funnel(y.x, x.w, r), funnel(y.y, y.x, r), funnel(y.z, y.y, r),
+                        funnel(y.w, y.z, r));
+  }
+}
 
 // A destination chunk of a tile whose owned bytes [lo, hi) span rows or
 // padding: each row's piece from a global window (rare; kept out of line).
@@ -1183,6 +1209,36 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
           for (uint32_t g = gs; g <= ge; ++g) gt[reg][g - g0] = uint8_t(lane);
         }
       }
+      if constexpr (kDiag == 7) {
+        // row pieces of the owned value range: [a, e) = row r's bytes in [X2, X3)
+        const uint32_t X2 = X[2], X3 = X[3];
+        const uint32_t a = max(vp, X2), e = min(vp + v, X3);
+        const bool piece = live && v && a < e;
+        const uint32_t cs = piece ? (a + 15) >> 4 : 0u, ce = piece ? e >> 4 : 0u;
+        const uint32_t wc = ce > cs ? ce - cs : 0u;
+        const uint32_t nu = (wc + 63) >> 6;
+        const uint32_t ui = wave_scan_dpp(nu);
+        const uint32_t sbias0 = uint32_t(int64_t(off) - A);
+        for (uint32_t q = 0; q < nu; ++q) {
+          const uint32_t u = ui - nu + q;
+          R.unit[0][u] = cs + 64 * q;
+          R.unit[1][u] = vs - vp + 16 * (cs + 64 * q) + sbias0;
+          R.unit[2][u] = min(64u, wc - 64 * q);
+        }
+        // boundary chunks: where a piece ends inside a chunk, and the range's
+        // first chunk when it starts inside one (in order; equal neighbours skipped)
+        const bool eb = piece && (e & 15);
+        const uint64_t m = __ballot(eb);
+        const uint32_t head = (X2 < X3 && (X2 & 15)) ? 1u : 0u;
+        const uint32_t idx = head + uint32_t(__builtin_amdgcn_mbcnt_hi(
+                                        uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
+        if (eb) R.bnd[idx] = e >> 4;
+        if (lane == 0) {
+          if (head) R.bnd[0] = X2 >> 4;
+          R.nbnd = head + uint32_t(__builtin_popcountll(m));
+          R.nunit = __builtin_amdgcn_readlane(ui, 63);
+        }
+      }
     }
   }
   if constexpr (kDiag >= 3) T[3] = __builtin_amdgcn_s_memrealtime();
@@ -1195,7 +1251,48 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
   const uint32_t nv = vx1 > vx0 ? ((vx1 + 15) >> 4) - (vx0 >> 4) : 0u;
   const uint32_t sbias = uint32_t(int64_t(off) - A);  // stage byte of block position s: s + sbias
   if (kDiag == 1) return;  // diagnostic: metadata + DMA + row table only
-  if constexpr (kDirect) {
+  if constexpr (kDiag == 7) {
+    // value runs: one unit of <= 64 whole chunks of one row per wave iteration
+    const uint32_t nunit = R.nunit, nbnd = R.nbnd;
+    uint8_t* const varena = P.val_arena + vb0;
+    for (uint32_t u = tid >> 6; u < nunit; u += kNT / 64) {
+      const uint32_t c0 = __builtin_amdgcn_readfirstlane(R.unit[0][u]);
+      const uint32_t sbyte = __builtin_amdgcn_readfirstlane(R.unit[1][u]);
+      const uint32_t cnt = __builtin_amdgcn_readfirstlane(R.unit[2][u]);
+      if (lane < cnt) {
+        const uint32_t line = (sbyte >> 4) + lane;
+        const uint4 w = funnel_u(stage[line], stage[line + 1], sbyte & 15);
+        *reinterpret_cast<uint4*>(varena + (uint64_t(c0 + lane) << 4)) = w;
+      }
+    }
+    // keys and the boundary value chunks: per-lane lookup
+    for (uint32_t j = tid; j < nk + nbnd; j += kNT) {
+      const uint32_t reg = j >= nk;
+      if (reg && j > nk && R.bnd[j - nk] == R.bnd[j - nk - 1]) continue;
+      const uint32_t X0 = reg ? vx0 : kx0, X1 = reg ? vx1 : kx1;
+      const uint32_t x = reg ? R.bnd[j - nk] << 4 : ((kx0 >> 4) + j) << 4;
+      const uint32_t lo = max(x, X0), hi = min(x + 16, X1);
+      const uint32_t* pre = R.pre[reg];
+      const uint32_t* sb = R.sb[reg];
+      uint32_t r = gt[reg][(lo >> 6) - (X0 >> 6)];
+      while (r < lastr && pre[r + 1] <= lo) ++r;
+      uint8_t* dst = (reg ? P.val_arena + vb0 : P.key_arena + kb0) + x;
+      const uint32_t dend = min(hi, pre[rows]);
+      uint4 out = make_uint4(0, 0, 0, 0);
+      for (uint32_t d = lo; d < dend; ++r) {
+        const uint32_t e = min(dend, pre[r + 1]);
+        if (e > d) {
+          out = merge_bytes(out, load16_lds_b128(stage, sb[r] + x + sbias), int32_t(d - x),
+                            int32_t(e - x));
+          d = e;
+        }
+      }
+      if (lo == x && hi == x + 16)
+        *reinterpret_cast<uint4*>(dst) = out;
+      else
+        store_partial(dst, out, lo - x, hi - x);
+    }
+  } else if constexpr (kDirect) {
     constexpr uint32_t kU = (kT / 16 + 8 + kNT - 1) / kNT;  // chunk slots per lane
     uint4 v[kU];
     uint32_t xs[kU], los[kU], his[kU], regs[kU];
@@ -2093,7 +2190,10 @@ const TileForm kTileForms[] = {OKV_TILE_FORM(16, 256, 0), OKV_TILE_FORM(8, 256, 
                                OKV_TILE_FORM(16, 256, 3), OKV_TILE_FORM(16, 256, 4),
                                OKV_TILE_FORM(16, 256, 5), OKV_TILE_FORM(16, 256, 6),
                                OKV_TILE_FORM(8, 256, 6), OKV_TILE_FORM(4, 256, 6),
-                               OKV_TILE_FORM(32, 512, 6), OKV_TILE_FORM(16, 512, 6)};
+                               OKV_TILE_FORM(32, 512, 6), OKV_TILE_FORM(16, 512, 6),
+                               OKV_TILE_FORM(16, 256, 7), OKV_TILE_FORM(8, 256, 7),
+                               OKV_TILE_FORM(32, 512, 7), OKV_TILE_FORM(16, 512, 7),
+                               OKV_TILE_FORM(32, 256, 7)};
 const TileForm* tile_form(uint32_t kib, uint32_t threads, uint32_t diag) {
   for (const TileForm& f : kTileForms)
     if (f.kib == kib && f.threads == threads && f.diag == diag) return &f;
@@ -2403,23 +2503,22 @@ extern "C" {
 
 int okv_abi_version(void) { return OKV_ABI_VERSION; }
 
+okv_ctx* okv_open_ex(int device, void* stream, const okv_open_opts* opts) {
+  if (opts && opts->size < sizeof(okv_open_opts)) return nullptr;
+  okv_ctx* ctx = okv_open_on_stream(device, stream);
+  if (ctx && opts) {
+    if (opts->flags & OKV_OPEN_NO_FUSED) ctx->fused = false;
+    ctx->zstd_one_pass = (opts->flags & OKV_OPEN_ZSTD_ONE_PASS) != 0;
+  }
+  return ctx;
+}
+
 okv_ctx* okv_open_on_stream(int device, void* stream) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;
   if (hipSetDevice(device) != hipSuccess) return nullptr;
   okv_ctx* ctx = new okv_ctx();
   ctx->device = device;
-  // A/B knobs of the pass-3 launch (both bit-exact): OKV_GATHER_THREADS=64|256
-  // (workgroup width), OKV_GATHER_GRID=<workgroups> (persistent grid)
-  if (const char* v = getenv("OKV_GATHER_THREADS")) {
-    ctx->gather_threads = uint32_t(atoi(v));
-    if (ctx->gather_threads != 64 && ctx->gather_threads != 256) {
-      delete ctx;
-      return nullptr;
-    }
-  }
-  if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
-  if (const char* v = getenv("OKV_DECODE_FUSED")) ctx->fused = atoi(v) != 0;
   // The fused kernel's blocks wait for the last-arriving block of their grid,
   // so every block must be resident at once: cap the batch at a quarter of
   // the device's resident capacity for it (room for other contexts' grids on
@@ -2433,6 +2532,19 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
     ctx->fused_max = std::min<uint32_t>(kFusedMaxBlocks, uint32_t(ncu) * uint32_t(per_cu) / 4);
     if (ctx->fused_max == 0) ctx->fused = false;
   }
+#ifdef OKV_ABLATE
+  // ablation build only: the measured alternative forms (tools/ablate*.py)
+  // A/B knobs of the pass-3 launch (both bit-exact): OKV_GATHER_THREADS=64|256
+  // (workgroup width), OKV_GATHER_GRID=<workgroups> (persistent grid)
+  if (const char* v = getenv("OKV_GATHER_THREADS")) {
+    ctx->gather_threads = uint32_t(atoi(v));
+    if (ctx->gather_threads != 64 && ctx->gather_threads != 256) {
+      delete ctx;
+      return nullptr;
+    }
+  }
+  if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
+  if (const char* v = getenv("OKV_DECODE_FUSED")) ctx->fused = atoi(v) != 0;
   if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
   if (const char* v = getenv("OKV_VALUE_SWEEP")) {
     ctx->value_sweep = uint32_t(atoi(v));
@@ -2453,6 +2565,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
       return nullptr;
     }
   }
+#endif
   if (stream) {
     ctx->stream = static_cast<hipStream_t>(stream);
   } else {

@@ -1585,13 +1585,13 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
        uint64_t(kMaxChunks) * 16 / std::max<uint64_t>(pl.bmax, 1)});
   // record-major LDS assembly pays off for small records (most chunks would
   // mix fields); large records take the chunk-major kernels
-  const char* eimg = getenv("OKV_ENC_IMAGE");  // diagnostic: LDS image bytes (16384 / 32768)
+  const char* eimg = okv::knob("OKV_ENC_IMAGE");  // diagnostic: LDS image bytes (16384 / 32768)
   const int eimg_v = eimg ? atoi(eimg) : 0;
   const uint32_t img = (eimg_v == 32768 || eimg_v == 8192 || eimg_v == 12288) ? uint32_t(eimg_v)
                                                                               : kImage;
   const uint64_t GL = std::min<uint64_t>(kMaxRegion, img / std::max<uint64_t>(pl.bmax, 1));
   const bool aligned = o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0;
-  const char* evar = getenv("OKV_ENC_VARIANT");
+  const char* evar = okv::knob("OKV_ENC_VARIANT");
   const int EV = evar ? atoi(evar) : 0;
   if (aligned && GL >= 1 && pl.avg_rec <= 512 && EV != 3) {
     if (img == 32768)

@@ -636,7 +636,7 @@ int okv_merge_rows(okv_ctx* ctx, const okv_merge_src* srcs, uint32_t nsrc,
                        m->d_base, nsrc, n, m->kaddr, m->pfx, m->klen, m->split);
   }
   static const int stage = [] {
-    const char* e = getenv("OKV_MERGE_STAGE");  // A/B knob: 0 = windows searched in HBM / L2
+    const char* e = okv::knob("OKV_MERGE_STAGE");  // A/B knob: 0 = windows searched in HBM / L2
     return e ? atoi(e) : 1;
   }();
   hipLaunchKernelGGL(okv_merge_rank_kernel, gn, b256, 0, s, m->d_base, nsrc, n, m->kaddr, m->pfx,

@@ -1414,6 +1414,29 @@ __device__ __forceinline__ uint32_t wb_take(WinBits& w, uint32_t k) {
   const uint32_t v = __builtin_amdgcn_alignbit(c, a, pos & 31u);
   return v & ((1u << k) - 1u);
 }
+// Bits [pos, pos + 64) / [pos, pos + 32) of the window (window-relative pos,
+// 0 <= pos < 128; bits above the window read as 0): selects and funnel shifts,
+// no change to the read position (the sequence loop sets P itself).
+__device__ __forceinline__ uint64_t wb_get64(const WinBits& w, uint32_t pos) {
+  const uint32_t i = pos >> 5, s = pos & 31u;
+  const uint32_t w0 = uint32_t(w.lo), w1 = uint32_t(w.lo >> 32), w2 = uint32_t(w.hi),
+                 w3 = uint32_t(w.hi >> 32);
+  const uint32_t a = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
+  const uint32_t b = i == 0 ? w1 : i == 1 ? w2 : i == 2 ? w3 : 0u;
+  const uint32_t c = i == 0 ? w2 : i == 1 ? w3 : 0u;
+  return uint64_t(__builtin_amdgcn_alignbit(b, a, s)) |
+         (uint64_t(__builtin_amdgcn_alignbit(c, b, s)) << 32);
+}
+__device__ __forceinline__ uint32_t wb_get32(const WinBits& w, uint32_t pos) {
+  const uint32_t i = pos >> 5;
+  const uint32_t w0 = uint32_t(w.lo), w1 = uint32_t(w.lo >> 32), w2 = uint32_t(w.hi),
+                 w3 = uint32_t(w.hi >> 32);
+  const uint32_t a = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : w3;
+  const uint32_t c = i == 0 ? w1 : i == 1 ? w2 : i == 2 ? w3 : 0u;
+  return __builtin_amdgcn_alignbit(c, a, pos & 31u);
+}
+__device__ __forceinline__ uint32_t lowmask(uint32_t k) { return (1u << k) - 1u; }  // k <= 31
+
 // Slide the window down so its top dword holds bit P - 1; by 0..3 dwords.
 __device__ __forceinline__ void wb_slide(WinBits& w) {
   const int32_t dtop = ((w.f.P + 31) >> 5) - 1;
@@ -1459,6 +1482,11 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
   // 16 blocks per workgroup with LDS tables measured slower at C5 scale (half
   // the blocks in flight; the lane chain is instruction-bound, not table-bound).
   __shared__ uint32_t llb[36], mlb[53];
+  // packed sequences staged per lane and written out every kSeqStage: a global
+  // store in the loop would be waited for with the next table gathers (stores
+  // and loads retire in issue order)
+  constexpr uint32_t kSeqStage = 32;
+  __shared__ uint64_t sq[kSeqStage][64];
   const int lane = threadIdx.x & 63;
   if (lane < 36) llb[lane] = zst::LL_BASE[lane];
   if (lane < 53) mlb[lane] = zst::ML_BASE[lane];
@@ -1493,18 +1521,43 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
     zst::wb_slide(br);
     uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
     const int32_t P0 = 8 * br.f.s0;
+    // software-pipelined: sequence i + 1's three table gathers are issued as
+    // soon as its states are known, before sequence i's value work
+    uint32_t ell = T[sll], eof = T[512 + sof], eml = T[768 + sml];
     for (uint32_t i = 0; i < z.nseq; ++i) {
       if (br.f.P < P0) {  // libzstd: the stream overflowed before this sequence
         st = zst::kErr;
         break;
       }
-      const uint32_t ell = T[sll], eof = T[512 + sof], eml = T[768 + sml];
-      const uint32_t ofs = zst::fse_sym(eof);
-      const uint32_t ofv = (1u << ofs) + zst::wb_take(br, ofs);
-      const uint32_t mlx = zst::wb_take(br, zst::fse_xb(eml));
-      const uint32_t llx = zst::wb_take(br, zst::fse_xb(ell));
+      // Every field's position follows from the three entries: offset extra
+      // bits, then ML, then LL extra bits, then the LL / ML / OF state bits
+      // (read high to low).  The state bits and both length extras come out
+      // of ONE 64-bit window read (<= 26 + 16 + 16 bits), the offset extras of
+      // one 32-bit read, so the chain to the next table gathers is the entries,
+      // a few adds, one extraction and the slide.
+      const uint32_t ofs = zst::fse_sym(eof), xml = zst::fse_xb(eml), xll = zst::fse_xb(ell);
+      const uint32_t nl = zst::fse_nb(ell), nm = zst::fse_nb(eml), no = zst::fse_nb(eof);
+      const uint32_t nsb = i + 1 < z.nseq ? nl + nm + no : 0u;
+      const uint32_t p1 = uint32_t(br.f.P - 32 * br.wd) - ofs;  // offset extras at [p1, p1 + ofs)
+      const uint32_t p4 = p1 - xml - xll - nsb;                 // state bits at [p4, p4 + nsb)
+      const uint64_t e = zst::wb_get64(br, p4);
+      const uint32_t ofx = zst::wb_get32(br, p1) & zst::lowmask(ofs);
+      const uint32_t sbits = uint32_t(e) & zst::lowmask(nsb);
+      const uint32_t llx = uint32_t(e >> nsb) & zst::lowmask(xll);
+      const uint32_t mlx = uint32_t(e >> (nsb + xll)) & zst::lowmask(xml);
+      // next states (an unused last update reads nothing: nsb = 0) and their
+      // table entries, in flight during this sequence's value work
+      sll = zst::fse_base(ell) + (sbits >> (nm + no));
+      sml = zst::fse_base(eml) + ((sbits >> no) & zst::lowmask(nm));
+      sof = zst::fse_base(eof) + (sbits & zst::lowmask(no));
       const uint32_t ml = mlb[zst::fse_sym(eml)] + mlx;
       const uint32_t ll = llb[zst::fse_sym(ell)] + llx;
+      ell = T[sll];
+      eof = T[512 + sof];
+      eml = T[768 + sml];
+      br.f.P -= int32_t(ofs + xml + xll + nsb);
+      zst::wb_slide(br);
+      const uint32_t ofv = (1u << ofs) + ofx;
       // repeat offsets (RFC 8878 3.1.1.5), branch-free: ofv > 3 is a new
       // offset; else idx = ofv - 1 (+1 when ll == 0) picks rep0/rep1/rep2/rep0-1
       const bool fresh = ofv > 3;
@@ -1516,16 +1569,6 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
       rep2 = sh2 ? rep1 : rep2;
       rep1 = sh1 ? rep0 : rep1;
       rep0 = sh1 ? off : rep0;
-      if (i + 1 < z.nseq) {  // state updates: literals length, match length, offset --
-        // read in that order, so one take of all three (<= 9 + 9 + 8 bits) holds
-        // them high to low
-        const uint32_t nl = zst::fse_nb(ell), nm = zst::fse_nb(eml), no = zst::fse_nb(eof);
-        const uint32_t v = zst::wb_take(br, nl + nm + no);
-        sll = zst::fse_base(ell) + (v >> (nm + no));
-        sml = zst::fse_base(eml) + ((v >> no) & ((1u << nm) - 1u));
-        sof = zst::fse_base(eof) + (v & ((1u << no) - 1u));
-      }
-      zst::wb_slide(br);
       // execution checks (3.1.1.4), in the general kernel's order
       if (uint64_t(lsum) + ll > z.lit_total) {
         st = zst::kErr;
@@ -1540,9 +1583,17 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
         st = zst::kErr;
         break;
       }
-      S[i] = zst::seq_pack(ll, ml, off);
+      sq[i % kSeqStage][lane] = zst::seq_pack(ll, ml, off);
+      if (i % kSeqStage == kSeqStage - 1) {
+        const uint32_t i0 = i - (kSeqStage - 1);
+        for (uint32_t q = 0; q < kSeqStage; ++q) S[i0 + q] = sq[q][lane];
+      }
       lsum += ll;
       osum += ll + ml;
+    }
+    {  // the staged tail (sequences after the last full stage; a failed block's are moot)
+      const uint32_t done = st == zst::kOK ? z.nseq : 0u;
+      for (uint32_t i0 = done - done % kSeqStage, q = 0; i0 + q < done; ++q) S[i0 + q] = sq[q][lane];
     }
     if (st == zst::kOK && br.f.P > P0) st = zst::kErr;  // unread bits
     if (st == zst::kOK && uint64_t(osum) + (z.lit_total - lsum) > z.cap) st = zst::kCap;
@@ -1937,8 +1988,8 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
              uint32_t nblk, uint64_t total) {
   hipStream_t s = ctx->stream;
   int rc;
-  const bool general = getenv("OKV_ZSTD_GENERAL") != nullptr;
-  const bool prof = getenv("OKV_ZSTD_PROF") != nullptr;
+  const bool general = ctx->zstd_one_pass || okv::knob("OKV_ZSTD_GENERAL") != nullptr;
+  const bool prof = okv::knob("OKV_ZSTD_PROF") != nullptr;
   hipEvent_t ev[6] = {};
   if (prof)
     for (auto& e : ev) (void)hipEventCreate(&e);
@@ -1965,7 +2016,7 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
       return rc;
     zb = reinterpret_cast<zst::ZBlk*>(ctx->z_zb);
     // one workgroup per block (no per-workgroup scratch; OKV_ZSTD_PRO_GRID: A/B)
-    const uint32_t pgrid = getenv("OKV_ZSTD_PRO_GRID") ? uint32_t(atoi(getenv("OKV_ZSTD_PRO_GRID")))
+    const uint32_t pgrid = okv::knob("OKV_ZSTD_PRO_GRID") ? uint32_t(atoi(okv::knob("OKV_ZSTD_PRO_GRID")))
                                                        : nblk;
     hipLaunchKernelGGL(okv_zstd_pro_kernel, dim3(std::max(1u, std::min(nblk, pgrid))), dim3(64), 0, s,
                        seg, seg_bytes, descs, nblk, ctx->z_cap_off, ctx->z_dec, ctx->z_dec_len,
@@ -1985,7 +2036,7 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
     // one workgroup per block by default: the dispatcher balances blocks of
     // unequal work better than a grid-stride loop (16 384 x 64 KiB: 3.8 ms vs
     // 4.6 ms at 4096 workgroups, 5.6 at 2816); profiling caps it at its slots
-    uint32_t egrid = getenv("OKV_ZSTD_EXEC_GRID") ? uint32_t(atoi(getenv("OKV_ZSTD_EXEC_GRID")))
+    uint32_t egrid = okv::knob("OKV_ZSTD_EXEC_GRID") ? uint32_t(atoi(okv::knob("OKV_ZSTD_EXEC_GRID")))
                                                   : nblk;
     if (prof) egrid = std::min(egrid, kExecGridMax);
     egrid = std::max(egrid, 1u);

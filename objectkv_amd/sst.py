@@ -232,10 +232,15 @@ class Decoded:
 class Decoder:
     """One okv_ctx bound to a GPU (HIP device ordinal)."""
 
-    def __init__(self, device: int = 0, stream=None):
+    def __init__(self, device: int = 0, stream=None, flags: int = 0):
+        """flags: okv_open_opts.flags (OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS)."""
         L = lib()
-        self._ctx = (L.okv_open_on_stream(device, stream) if stream is not None
-                     else L.okv_open(device))
+        if flags:
+            opts = _lib.OpenOpts(C.sizeof(_lib.OpenOpts), flags)
+            self._ctx = L.okv_open_ex(device, stream, C.byref(opts))
+        else:
+            self._ctx = (L.okv_open_on_stream(device, stream) if stream is not None
+                         else L.okv_open(device))
         if not self._ctx:
             raise OkvError(_lib.OKV_E_NODEV, f"okv_open({device}) failed (no GPU?)")
         self.device = device

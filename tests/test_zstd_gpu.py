@@ -14,15 +14,22 @@ from tests import zstd_cases as ZC
 
 pytestmark = pytest.mark.gpu
 
-@pytest.fixture(params=["staged", "general"], autouse=True)
-def zmode(request, monkeypatch):
+@pytest.fixture(scope="module")
+def one_pass_decoder():
+    """A context opened with OKV_OPEN_ZSTD_ONE_PASS: every zstd block through
+    the one-wave-per-block kernel."""
+    dec = okv.Decoder(0, flags=okv._lib.OPEN_ZSTD_ONE_PASS)
+    yield dec
+    dec.close()
+
+
+@pytest.fixture(params=["staged", "one_pass"])
+def zdec(request, decoder, one_pass_decoder):
     """Every case through both device paths: the staged decoder (prologue ->
-    lane-per-block sequences -> parallel executor) and the general kernel."""
-    if request.param == "general":
-        monkeypatch.setenv("OKV_ZSTD_GENERAL", "1")
-    else:
-        monkeypatch.delenv("OKV_ZSTD_GENERAL", raising=False)
-    return request.param
+    lane-per-block sequences -> parallel executor, the default) and the
+    one-pass kernel (OKV_OPEN_ZSTD_ONE_PASS; also the staged path's fallback
+    for the blocks its prologue hands back)."""
+    return one_pass_decoder if request.param == "one_pass" else decoder
 
 
 SOA = ("row_start", "key_off", "key_len", "val_off", "val_len", "key_base", "val_base")
@@ -44,24 +51,24 @@ def _check(decoder, seg, descs, index_only=False):
 
 
 @pytest.mark.parametrize("case", ZC.cases(), ids=lambda c: c[0])
-def test_zstd_cases(decoder, case):
+def test_zstd_cases(zdec, case):
     name, seg, descs, _note = case
-    got = _check(decoder, seg, descs)
+    got = _check(zdec, seg, descs)
     assert int(got.status.max()) == 0, name
-    _check(decoder, seg, descs, index_only=True)  # every block OKV_BLK_UNSUPPORTED
+    _check(zdec, seg, descs, index_only=True)  # every block OKV_BLK_UNSUPPORTED
 
 
 @pytest.mark.parametrize("case", ZC.corrupt_cases(), ids=lambda c: c[0])
-def test_zstd_corrupt(decoder, case):
+def test_zstd_corrupt(zdec, case):
     name, seg, descs = case
-    _check(decoder, seg, descs)
+    _check(zdec, seg, descs)
 
 
-def test_zstd_segment_through_product_reader(decoder):
+def test_zstd_segment_through_product_reader(zdec):
     """RowIter / GetRow / GetRange over a zstd segment (C++ reader mirror)."""
     rows = ZC._rows(21, 2500)
     seg, flen, _meta = ZC.Z.zstd_segment(rows, 3584, 4096, level=7)
-    pr = R.SegmentReader(seg, flen, decoder)
+    pr = R.SegmentReader(seg, flen, zdec)
     orr = P.SegmentReader(seg, flen)
     it, oit = pr.RowIter(R.DirectionAscending), orr.RowIter(0)
     n = 0
@@ -82,15 +89,15 @@ def test_zstd_segment_through_product_reader(decoder):
     assert [(r.Key, r.Value) for r in got] == [(r.Key, r.Value) for r in want]
 
 
-def test_zstd_bench_shape_blocks(decoder):
+def test_zstd_bench_shape_blocks(zdec):
     """64 KiB text blocks as bench.py --config cz builds them (libzstd level 3)."""
     from tools.zstd_gen import text_zstd_segment
     seg, descs, _ = text_zstd_segment(24, 9, 3)
-    got = _check(decoder, seg.tobytes(), [tuple(int(x) for x in d) for d in descs])
+    got = _check(zdec, seg.tobytes(), [tuple(int(x) for x in d) for d in descs])
     assert int(got.status.max()) == 0
 
 
-def test_zstd_long_runs_and_rle_literals(decoder):
+def test_zstd_long_runs_and_rle_literals(zdec):
     """Matches far longer than the executor's 4 KiB byte map, offset-1 runs,
     and blocks whose literals are RLE."""
     rows = []
@@ -100,11 +107,11 @@ def test_zstd_long_runs_and_rle_literals(decoder):
     seg, _, _ = ZC.Z.zstd_segment(rows, 57344, 65536, level=3)
     from oracle import pyoracle as P2
     md = P2.bytes_to_metadata(ZC._meta_of(seg))
-    got = _check(decoder, seg, [st.desc() for st in md.entries])
+    got = _check(zdec, seg, [st.desc() for st in md.entries])
     assert int(got.status.max()) == 0
 
 
-def test_zstd_staged_equals_general_under_corruption(decoder, zmode, monkeypatch):
+def test_zstd_staged_equals_general_under_corruption(decoder, one_pass_decoder):
     """Byte flips in the sequence sections of 48 blocks.  Two-sided against the
     oracle (libzstd as the decoder checker): every block's status must equal
     the oracle's -- a corrupt frame the checker rejects must fail on the
@@ -123,8 +130,7 @@ def test_zstd_staged_equals_general_under_corruption(decoder, zmode, monkeypatch
             b[off + csz - 1 - rng.randrange(min(csz - 20, 3000))] ^= 1 << rng.randrange(8)
     dl = [tuple(int(x) for x in d) for d in descs]
     staged = _check(decoder, bytes(b), dl)
-    monkeypatch.setenv("OKV_ZSTD_GENERAL", "1")
-    general = _check(decoder, bytes(b), dl)
+    general = _check(one_pass_decoder, bytes(b), dl)
     assert np.array_equal(staged.status, general.status)
     assert staged.val_arena.tobytes() == general.val_arena.tobytes()
     # the flips must actually exercise both outcomes

@@ -8,6 +8,9 @@ usage: python tools/ablate.py [arm ...]     arm = <threads>[:<grid>[:<staged>]] 
 env:   ABL_NBLK (65536), ABL_ROUNDS (5), ABL_KIND (1 = Zipf C3, 0 = fixed C2),
        ABL_BS (65536), ABL_TH (57344)
 """
+import os as _os
+_os.environ.setdefault("OKV_ABLATE", "1")  # the ablation build (its OKV_* knobs)
+
 import os
 import sys
 

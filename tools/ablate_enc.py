@@ -2,6 +2,9 @@
 
     python tools/ablate_enc.py [--rows N] [--reps R] [--variants 0,1,2]
 """
+import os as _os
+_os.environ.setdefault("OKV_ABLATE", "1")  # the ablation build (its OKV_* knobs)
+
 import argparse
 import os
 import sys

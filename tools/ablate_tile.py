@@ -11,6 +11,9 @@ env:   ABL_NBLK (65536), ABL_ROUNDS (5), ABL_KIND (1 = Zipf C3), ABL_BS (65536),
 Prints per arm: pass-3 ms (HIP events), count + scan ms, and the whole
 one-at-a-time decode step (host clock, no events) with its roofline fraction.
 """
+import os as _os
+_os.environ.setdefault("OKV_ABLATE", "1")  # the ablation build (its OKV_* knobs)
+
 import os
 import re
 import sys

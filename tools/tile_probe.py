@@ -6,6 +6,9 @@ after its stores drain.  Prints per-phase medians / p90 in microseconds.
 
 usage: python tools/tile_probe.py [tile form, default 16x]
 """
+import os as _os
+_os.environ.setdefault("OKV_ABLATE", "1")  # the ablation build (its OKV_* knobs)
+
 import ctypes as C
 import os
 import sys

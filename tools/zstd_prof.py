@@ -1,5 +1,8 @@
 """zstd decode diagnostics on the CZ workload: phase cycle counters
 (OKV_ZSTD_PROF) and an A/B of LDS staging (OKV_ZSTD_STAGE)."""
+import os as _os
+_os.environ.setdefault("OKV_ABLATE", "1")  # the ablation build (its OKV_* knobs)
+
 import os
 import sys
 

@@ -37,6 +37,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s device-resident SST block decode + M rows/s, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+PMC_ROUND = "r3"  # profiles/<round>/pmc_<config>_<mode>.json (FETCH/WRITE_SIZE passes)
 
 CONFIGS = {
     # name: (synth kind, seed, nblocks, threshold, block size, description)
@@ -139,10 +140,10 @@ def source_sha(paths=DECODE_SOURCES):
 
 
 def pmc_traffic(config, mode, kernel, sources=DECODE_SOURCES):
-    """HBM bytes per launch of `kernel` from profiles/r2/pmc_<config>_<mode>.json
+    """HBM bytes per launch of `kernel` from profiles/<PMC_ROUND>/pmc_<config>_<mode>.json
     -- used only if it was collected from the kernel sources being timed
     (same source_sha); else None."""
-    path = os.path.join(ROOT, "profiles", "r2", f"pmc_{config}_{mode}.json")
+    path = os.path.join(ROOT, "profiles", PMC_ROUND, f"pmc_{config}_{mode}.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
@@ -458,15 +459,7 @@ def run_decode(args, torch, okv, D):
         # read OriginalSize per block; write payload (padded arenas) + 22 B/row
         # SoA (u64 key_off, u16 key_len, u64 val_off, u32 val_len) + 28 B/block
         alg = orig_bytes + payload + rows * 22 + nblk * 28
-        sweep = os.environ.get("OKV_VALUE_SWEEP", "7") not in ("0", "") and \
-            os.environ.get("OKV_GATHER_STAGED", "1") != "0"
-        roof_kernel = ("okv_decode_fused_kernel (passes 1-3) + okv_copy_kernel"
-                       if nblk <= 512 and in_bytes / max(nblk, 1) <= 16384 else
-                       "okv_gather_small_kernel + okv_copy_kernel"
-                       if in_bytes / max(nblk, 1) <= 16384 else
-                       "okv_rows_kernel + okv_value_sweep_kernel + okv_gather_staged_kernel "
-                       "(exits: the sweep was safe) + okv_copy_kernel" if sweep else
-                       "okv_gather_staged_kernel + okv_copy_kernel")
+        roof_kernel = path_kernels(okv, dec.last_path())
         roof_ms = ms["copy"]
     achieved = alg / (roof_ms * 1e-3) / 1e9
     pass3 = tuple(w for w in roof_kernel.replace("(", " ").split() if w.startswith("okv_"))
@@ -529,6 +522,17 @@ def run_decode(args, torch, okv, D):
     emit(D, line)
     if not e2e:
         dec.close()
+
+
+def path_kernels(okv, lp):
+    """The pass-3 kernels the last decode launched (okv_last_path bits)."""
+    L = okv._lib
+    names = [(L.PATH_FUSED, "okv_decode_fused_kernel (passes 1-3)"),
+             (L.PATH_SMALL, "okv_gather_small_kernel"), (L.PATH_TILE, "okv_tile_kernel"),
+             (L.PATH_SWEEP, "okv_rows_kernel + okv_value_sweep_kernel"),
+             (L.PATH_STAGED, "okv_gather_staged_kernel"), (L.PATH_GATHER, "okv_gather_kernel"),
+             (L.PATH_BIG, "okv_copy_kernel")]
+    return " + ".join(n for bit, n in names if lp & bit) or "none"
 
 
 def cpu_decode_baseline(args, seg, descs, nblk, comp):
@@ -605,8 +609,7 @@ def run_encode(args, torch, okv, D):
     enc._check(okv._lib.lib().okv_hash_blocks(enc._ctx, out["seg"].data_ptr(), eo.data_bytes,
                                                out["desc"].data_ptr(), nb, hv.data_ptr(),
                                                okv._lib.F_DEVICE_PTRS), "hash")
-    ablation = os.environ.get("OKV_ENC_VARIANT", "0") not in ("", "0", "3")
-    assert ablation or torch.equal(hv, out["hash"][:nb])  # diagnostic arms skip hash / bytes
+    assert torch.equal(hv, out["hash"][:nb])  # the fused block hashes == a separate rehash
     ver = None
     if rank == 0 and not args.no_verify:
         from oracle import coracle

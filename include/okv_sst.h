@@ -356,6 +356,20 @@ int okv_merge_rows(okv_ctx *ctx, const okv_merge_src *srcs, uint32_t nsrc,
 int okv_profile(okv_ctx *ctx, int enable);
 int okv_profile_read(okv_ctx *ctx, double *ms, uint64_t *calls);
 
+/* The pass-3 kernels the context's last okv_decode_blocks call launched (a
+ * bitmask of OKV_PATH_*), for tests and benchmarks that must show which
+ * shipping kernel ran.  Set before the call returns, async or not. */
+#define OKV_PATH_FUSED 1u  /* okv_decode_fused_kernel: passes 1-3 in one launch */
+#define OKV_PATH_SMALL 2u  /* okv_gather_small_kernel: one wave per small block */
+#define OKV_PATH_TILE 4u   /* okv_tile_kernel: large blocks, source tiles */
+#define OKV_PATH_SWEEP 8u  /* okv_rows_kernel + okv_value_sweep_kernel */
+#define OKV_PATH_STAGED 16u /* okv_gather_staged_kernel as the pass */
+#define OKV_PATH_GATHER 32u /* okv_gather_kernel (unstaged) */
+#define OKV_PATH_BIG 64u    /* okv_copy_kernel / okv_index_kernel for big blocks (always
+                               launched after a non-fused pass; exits when none) */
+#define OKV_PATH_ZSTD 128u  /* the zstd stage ran first */
+uint32_t okv_last_path(const okv_ctx *ctx);
+
 /* Device / pinned-host memory helpers for callers without another allocator. */
 void *okv_device_alloc(okv_ctx *ctx, size_t bytes);
 void okv_device_free(okv_ctx *ctx, void *p);

@@ -21,6 +21,9 @@ BLK_OK, BLK_EOF, BLK_SHORT, BLK_PANIC, BLK_UNSUPPORTED, BLK_CAPACITY = 0, 1, 2, 
 COMP_NONE, COMP_ZSTD, COMP_LZ4 = 0, 1, 2
 F_DEVICE_PTRS, F_INDEX_ONLY, F_ASYNC, F_NO_CLOSE = 1, 2, 4, 8
 OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS = 1, 2
+# okv_last_path bits (include/okv_sst.h OKV_PATH_*)
+PATH_FUSED, PATH_SMALL, PATH_TILE, PATH_SWEEP = 1, 2, 4, 8
+PATH_STAGED, PATH_GATHER, PATH_BIG, PATH_ZSTD = 16, 32, 64, 128
 # SegmentWriter sentinels (okv_sst.h OKV_W_*)
 W_KEY_TOO_LARGE, W_VALUE_TOO_LARGE, W_CLOSED, W_INVALID_KEY = -101, -102, -103, -104
 W_NIL_WRITER, W_UNSUPPORTED, W_NO_ROWS = -105, -106, -107
@@ -34,7 +37,7 @@ SYMBOLS = [
     "okv_open", "okv_open_on_stream", "okv_open_ex", "okv_close", "okv_last_error", "okv_stream", "okv_sync",
     "okv_abi_version", "okv_decode_plan", "okv_decode_blocks", "okv_decode_totals",
     "okv_xxh64", "okv_hash_blocks", "okv_device_alloc", "okv_device_free", "okv_host_alloc",
-    "okv_host_free", "okv_memcpy", "okv_profile", "okv_profile_read",
+    "okv_host_free", "okv_memcpy", "okv_profile", "okv_profile_read", "okv_last_path",
     "okv_encode_rows", "okv_encode_close", "okv_encode_profile_read", "okv_encode_profile_reset",
     "okv_synth_rows_fixed", "okv_merge_rows",
     "okv_writer_new", "okv_writer_write_row", "okv_writer_close", "okv_writer_data",
@@ -166,6 +169,7 @@ def lib():
         "okv_memcpy": (i32, [p, p, p, C.c_size_t, i32]),
         "okv_profile": (i32, [p, i32]),
         "okv_profile_read": (i32, [p, C.POINTER(C.c_double), C.POINTER(u64)]),
+        "okv_last_path": (C.c_uint32, [p]),
         "okv_encode_rows": (i32, [p, C.POINTER(Rows), C.POINTER(EncodeOpts),
                                   C.POINTER(EncodeOut), u32]),
         "okv_encode_close": (i32, [p, C.POINTER(EncodeOut), u32]),

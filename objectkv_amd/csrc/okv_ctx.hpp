@@ -53,6 +53,7 @@ struct okv_ctx {
   unsigned long long* f_ctr = nullptr;  // block-index counter, f_base at the next call
   unsigned long long f_base = 0;
   uint32_t f_epoch = 0;
+  uint32_t last_path = 0;          // OKV_PATH_* of the last decode (okv_last_path)
   size_t f_cap = 0;
   okv::Totals* d_tot = nullptr;
   okv::Totals* h_tot = nullptr;  // pinned

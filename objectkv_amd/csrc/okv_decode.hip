@@ -630,6 +630,7 @@ __global__ __launch_bounds__(NT) void okv_gather_kernel(CopyParams P) {
 // chain (metadata -> record positions -> headers -> keys), so it is sized for
 // occupancy: one window per lane in flight.  When the sweep is unsafe (big
 // blocks, capacity) it gathers the values itself.
+#ifdef OKV_ABLATE  // the round-2 row pass of the value sweep (ablation build only)
 __global__ __launch_bounds__(64) void okv_rows_kernel(CopyParams P) {
   __shared__ GatherSmem sm;
   // unsafe for the sweep (big blocks, capacity): okv_gather_staged_kernel,
@@ -665,6 +666,7 @@ __global__ __launch_bounds__(64) void okv_rows_kernel(CopyParams P) {
     if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
   }
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // Pass 3, wave-staged form (experimental, OKV_GATHER_STAGED=1): the value
@@ -673,7 +675,6 @@ __global__ __launch_bounds__(64) void okv_rows_kernel(CopyParams P) {
 // the loads in flight no longer cost registers, and a chunk's spill windows
 // come from the same image (no second trip).  Keys keep the global windows.
 // ---------------------------------------------------------------------------
-#define OKV_LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 constexpr uint32_t kStU = 5;                        // value tiles (1 KiB) per iteration
 template <uint32_t U> struct StCfg { static constexpr uint32_t cap = U * 1024 + 1024; };
 
@@ -1022,7 +1023,7 @@ struct TileRows {
   uint32_t pre[2][kRCap + 1];  // [key, value] exclusive prefix of lengths (pre[rows] = total)
   uint32_t sb[2][kRCap];       // block position of region byte x of row r = sb[r] + x
   uint32_t x[4];               // owned key range [x0, x1), value range [x2, x3)
-  // kDiag == 7 (value runs): whole value chunks in units of <= 64 inside one
+  // value runs (kRuns): whole value chunks in units of <= 64 inside one
   // row piece {dest chunk, stage byte of its first chunk, count}, and the
   // value chunks that mix rows, padding or a neighbouring tile's bytes
   uint32_t unit[3][96];
@@ -1071,7 +1072,14 @@ __device__ __noinline__ uint4 tile_chunk_pieces(const uint8_t* seg, uint64_t seg
 
 template <uint32_t kT, uint32_t kNT, bool kXcd, int kDiag = 0>
 __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tpb, uint32_t ntile) {
+  // kDiag: 0 the product form (value runs); ablation arms: 1 no chunk pass,
+  // 2 no DMA, 3 phase probe of the per-chunk form, 4 (+ no stores), 5 (+ no
+  // data reads), 6 direct unaligned global loads, 7 phase probe of the product
+  // form, 8 the per-chunk form (every chunk looked up per lane)
   constexpr bool kDirect = kDiag == 6;  // no LDS stage: one unaligned global load per chunk
+  constexpr bool kChunk = (kDiag >= 3 && kDiag <= 5) || kDiag == 8;
+  constexpr bool kRuns = !kChunk && !kDirect;
+  constexpr bool kProbe = (kDiag >= 3 && kDiag <= 5) || kDiag == 7;
   constexpr uint32_t kG = kT / 64 + 8;  // 64-byte destination granules per region table
   __shared__ TileRows R;
   __shared__ uint8_t gt[2][kG];         // row holding byte max(64 g, range start)
@@ -1079,8 +1087,8 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
   uint32_t L = blockIdx.x;
   if constexpr (kXcd) L = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
   if (L >= ntile) return;
-  uint64_t T[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // kDiag == 3: phase timestamps (sampled workgroups)
-  if constexpr (kDiag >= 3) T[0] = __builtin_amdgcn_s_memrealtime();
+  uint64_t T[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // kProbe: phase timestamps (sampled workgroups)
+  if constexpr (kProbe) T[0] = __builtin_amdgcn_s_memrealtime();
   // uniform block index (an SGPR: the loads below are scalar, all in one trip)
   const uint32_t b = __builtin_amdgcn_readfirstlane(L / tpb);
   const uint32_t t = L - b * tpb;
@@ -1099,7 +1107,7 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
   asm volatile("" ::"s"(off), "s"(c.rows), "s"(c.kbytes), "s"(c.vbytes), "s"(c.pend),
                "s"(c.status), "s"(lpre.rows), "s"(lpre.kb), "s"(lpre.vb), "s"(tpre.rows),
                "s"(tpre.kb), "s"(tpre.vb));
-  if constexpr (kDiag >= 3) T[1] = __builtin_amdgcn_s_memrealtime();
+  if constexpr (kProbe) T[1] = __builtin_amdgcn_s_memrealtime();
   const uint64_t row0 = tpre.rows + lpre.rows, kb0 = tpre.kb + lpre.kb, vb0 = tpre.vb + lpre.vb;
   const bool fits = row0 + c.rows <= P.row_cap &&
                     (P.index_only ||
@@ -1138,7 +1146,7 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
       }
     }
   }
-  if constexpr (kDiag >= 3) T[2] = __builtin_amdgcn_s_memrealtime();
+  if constexpr (kProbe) T[2] = __builtin_amdgcn_s_memrealtime();
   // row table (wave 0, lane r = row r) while the tile is in flight
   if (tid < 64) {
     const bool live = lane < rows;
@@ -1209,7 +1217,7 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
           for (uint32_t g = gs; g <= ge; ++g) gt[reg][g - g0] = uint8_t(lane);
         }
       }
-      if constexpr (kDiag == 7) {
+      if constexpr (kRuns) {
         // row pieces of the owned value range: [a, e) = row r's bytes in [X2, X3)
         const uint32_t X2 = X[2], X3 = X[3];
         const uint32_t a = max(vp, X2), e = min(vp + v, X3);
@@ -1233,25 +1241,28 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
         const uint32_t idx = head + uint32_t(__builtin_amdgcn_mbcnt_hi(
                                         uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
         if (eb) R.bnd[idx] = e >> 4;
+        // read lane 63 with the whole wave active (inside the lane-0 branch the
+        // compiler may compute ui for lane 0 only)
+        const uint32_t nunit = __builtin_amdgcn_readlane(ui, 63);
         if (lane == 0) {
           if (head) R.bnd[0] = X2 >> 4;
           R.nbnd = head + uint32_t(__builtin_popcountll(m));
-          R.nunit = __builtin_amdgcn_readlane(ui, 63);
+          R.nunit = nunit;
         }
       }
     }
   }
-  if constexpr (kDiag >= 3) T[3] = __builtin_amdgcn_s_memrealtime();
+  if constexpr (kProbe) T[3] = __builtin_amdgcn_s_memrealtime();
   if (P.index_only) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (kDiag >= 3) T[4] = __builtin_amdgcn_s_memrealtime();
+  if constexpr (kProbe) T[4] = __builtin_amdgcn_s_memrealtime();
   const uint32_t kx0 = R.x[0], kx1 = R.x[1], vx0 = R.x[2], vx1 = R.x[3];
   const uint32_t nk = kx1 > kx0 ? ((kx1 + 15) >> 4) - (kx0 >> 4) : 0u;
   const uint32_t nv = vx1 > vx0 ? ((vx1 + 15) >> 4) - (vx0 >> 4) : 0u;
   const uint32_t sbias = uint32_t(int64_t(off) - A);  // stage byte of block position s: s + sbias
   if (kDiag == 1) return;  // diagnostic: metadata + DMA + row table only
-  if constexpr (kDiag == 7) {
+  if constexpr (kRuns) {
     // value runs: one unit of <= 64 whole chunks of one row per wave iteration
     const uint32_t nunit = R.nunit, nbnd = R.nbnd;
     uint8_t* const varena = P.val_arena + vb0;
@@ -1374,7 +1385,7 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
     else
       store_partial(dst, out, lo - x, hi - x);
   }
-  if constexpr (kDiag >= 3) {
+  if constexpr (kProbe) {
     T[5] = __builtin_amdgcn_s_memrealtime();
     __syncthreads();
     T[6] = __builtin_amdgcn_s_memrealtime();
@@ -2182,26 +2193,29 @@ struct TileForm {
   TileForm {                                                                                \
     K, N, D, launch_tile_t<K * 1024, N, true, D>, launch_tile_t<K * 1024, N, false, D>      \
   }
+#ifdef OKV_ABLATE
 const TileForm kTileForms[] = {OKV_TILE_FORM(16, 256, 0), OKV_TILE_FORM(8, 256, 0),
                                OKV_TILE_FORM(32, 256, 0), OKV_TILE_FORM(16, 512, 0),
                                OKV_TILE_FORM(32, 512, 0), OKV_TILE_FORM(4, 256, 0),
                                OKV_TILE_FORM(16, 256, 1), OKV_TILE_FORM(16, 256, 2),
-                               OKV_TILE_FORM(32, 512, 1), OKV_TILE_FORM(32, 512, 2),
                                OKV_TILE_FORM(16, 256, 3), OKV_TILE_FORM(16, 256, 4),
                                OKV_TILE_FORM(16, 256, 5), OKV_TILE_FORM(16, 256, 6),
-                               OKV_TILE_FORM(8, 256, 6), OKV_TILE_FORM(4, 256, 6),
-                               OKV_TILE_FORM(32, 512, 6), OKV_TILE_FORM(16, 512, 6),
-                               OKV_TILE_FORM(16, 256, 7), OKV_TILE_FORM(8, 256, 7),
-                               OKV_TILE_FORM(32, 512, 7), OKV_TILE_FORM(16, 512, 7),
-                               OKV_TILE_FORM(32, 256, 7)};
+                               OKV_TILE_FORM(16, 256, 7), OKV_TILE_FORM(16, 256, 8),
+                               OKV_TILE_FORM(8, 256, 8), OKV_TILE_FORM(32, 512, 8)};
 const TileForm* tile_form(uint32_t kib, uint32_t threads, uint32_t diag) {
   for (const TileForm& f : kTileForms)
     if (f.kib == kib && f.threads == threads && f.diag == diag) return &f;
   return nullptr;
 }
+#endif
 void launch_tile(okv_ctx* ctx, const CopyParams& P, const TileGeo& g) {
+#ifdef OKV_ABLATE
   const TileForm* f = tile_form(ctx->tile_kib, ctx->tile_threads, ctx->tile_diag);
   (ctx->tile_xcd ? f->x : f->plain)(ctx->stream, P, g.tpb, P.nblk * g.tpb);
+#else
+  // the product form: 16 KiB source tiles, 256 threads, XCD-grouped, value runs
+  launch_tile_t<16384, 256, true, 0>(ctx->stream, P, g.tpb, P.nblk * g.tpb);
+#endif
 }
 
 int read_totals(okv_ctx* ctx, Totals* out) {
@@ -2254,9 +2268,14 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   // large blocks: the source-tile pass (okv_tile_kernel); value_sweep 1-7 are
   // the round-2 forms (row pass + address-ordered value sweep)
   const bool large = nblk && !fused && gather_threads(ctx, w, nblk) == 256;
+#ifdef OKV_ABLATE
   const bool tile = large && ctx->value_sweep == 8;
   const bool sweep = large && !tile && ctx->value_sweep && !index_only && ctx->gather_staged &&
                      o->row_cap < (uint64_t(1) << 32);
+#else
+  const bool tile = large;  // the product: okv_tile_kernel for every large-block decode
+  constexpr bool sweep = false;
+#endif
   const TileGeo geo = tile ? tile_geo(ctx, w.seg_bytes, nblk, index_only) : TileGeo{1, ~0ull};
   uint16_t* rt_kl = nullptr;
   if (tile || sweep) {
@@ -2318,6 +2337,16 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
                                         ((std::max<uint64_t>(o->row_cap, 1) * 8 + 255) & ~255ull));
     P.vtile = static_cast<uint32_t*>(ctx->d_vtile);
   }
+  const uint32_t gt = nblk ? gather_threads(ctx, w, nblk) : 0;
+  ctx->last_path = (comp ? OKV_PATH_ZSTD : 0u) |
+                   (!nblk ? 0u
+                    : fused ? OKV_PATH_FUSED
+                    : OKV_PATH_BIG | (tile ? OKV_PATH_TILE
+                                      : sweep ? OKV_PATH_SWEEP | OKV_PATH_STAGED
+                                      : gt == 256 && ctx->gather_staged && !index_only
+                                          ? OKV_PATH_STAGED
+                                      : gt == 64 && ctx->gather_staged ? OKV_PATH_SMALL
+                                                                       : OKV_PATH_GATHER));
   if (nblk) {
     const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
     if (fused) {
@@ -2343,13 +2372,16 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       }
       ctx->f_base += nblk;  // both counters advanced by nblk once the grid completes
     } else if (tile) {
-      if (ctx->tile_diag >= 3) {  // phase probe: 8 timestamps per 256th workgroup
+      if ((ctx->tile_diag >= 3 && ctx->tile_diag <= 5) || ctx->tile_diag == 7) {
+        // phase probe: 8 timestamps per 256th workgroup
         const size_t n = (size_t(nblk) * geo.tpb / 256 + 1) * 64;
         if ((rc = grow(ctx, &ctx->d_vsrc, &ctx->cap_vsrc, n))) return rc;
         P.vsrc = static_cast<uint64_t*>(ctx->d_vsrc);
       }
       launch_tile(ctx, P, geo);
-    } else if (sweep) {
+    }
+#ifdef OKV_ABLATE
+    else if (sweep) {
       // per-block rows + keys (one wave per block), then the value sweep
       hipLaunchKernelGGL(okv_rows_kernel, g, dim3(64), 0, ctx->stream, P);
       if (sw_tiles) {
@@ -2387,6 +2419,13 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       hipLaunchKernelGGL(okv_gather_kernel<64>, g, dim3(64), 0, ctx->stream, P);
     else
       hipLaunchKernelGGL(okv_gather_kernel<kThreads>, g, dim3(kThreads), 0, ctx->stream, P);
+#else
+    else if (gather_threads(ctx, w, nblk) == 64) {
+      hipLaunchKernelGGL(okv_gather_small_kernel, g, dim3(64), 0, ctx->stream, P);
+    } else {
+      return set_err(ctx, OKV_E_ARG, "decode path");  // unreachable: large => tile
+    }
+#endif
     const uint32_t nbig_grid = std::min<uint32_t>(nblk, 512);
     if (index_only)
       hipLaunchKernelGGL(okv_index_kernel, dim3((nbig_grid + kThreads - 1) / kThreads),
@@ -2737,12 +2776,16 @@ int okv_hash_blocks(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes,
   return OKV_OK;
 }
 
-// Diagnostic (tile-pass phase probe, OKV_TILE=...d3): copy the probe buffer to host.
+#ifdef OKV_ABLATE
+// Diagnostic (tile-pass phase probe, OKV_TILE=...d3 / d7): copy the probe buffer to host.
 int okv_debug_probe(okv_ctx* ctx, void* host, size_t bytes) {
   if (!ctx || !ctx->d_vsrc) return OKV_E_ARG;
   OKV_HIP(hipMemcpy(host, ctx->d_vsrc, std::min(bytes, ctx->cap_vsrc), hipMemcpyDeviceToHost));
   return OKV_OK;
 }
+#endif
+
+uint32_t okv_last_path(const okv_ctx* ctx) { return ctx ? ctx->last_path : 0u; }
 
 int okv_profile(okv_ctx* ctx, int enable) {
   if (!ctx) return OKV_E_ARG;

@@ -1585,37 +1585,38 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
        uint64_t(kMaxChunks) * 16 / std::max<uint64_t>(pl.bmax, 1)});
   // record-major LDS assembly pays off for small records (most chunks would
   // mix fields); large records take the chunk-major kernels
+  const bool aligned = o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0;
+#ifdef OKV_ABLATE
   const char* eimg = okv::knob("OKV_ENC_IMAGE");  // diagnostic: LDS image bytes (16384 / 32768)
   const int eimg_v = eimg ? atoi(eimg) : 0;
   const uint32_t img = (eimg_v == 32768 || eimg_v == 8192 || eimg_v == 12288) ? uint32_t(eimg_v)
                                                                               : kImage;
-  const uint64_t GL = std::min<uint64_t>(kMaxRegion, img / std::max<uint64_t>(pl.bmax, 1));
-  const bool aligned = o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0;
+  const uint64_t GLa = std::min<uint64_t>(kMaxRegion, img / std::max<uint64_t>(pl.bmax, 1));
   const char* evar = okv::knob("OKV_ENC_VARIANT");
-  const int EV = evar ? atoi(evar) : 0;
-  if (aligned && GL >= 1 && pl.avg_rec <= 512 && EV != 3) {
+  const int EV = evar ? atoi(evar) : 7;
+  if (aligned && GLa >= 1 && pl.avg_rec <= 512 && EV != 3) {
     if (img == 32768)
-      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<32768>, dim3(ceil_div(pl.nb, GL)),
-                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
+      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<32768>, dim3(ceil_div(pl.nb, GLa)),
+                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GLa));
     else if (img == 8192)
-      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<8192>, dim3(ceil_div(pl.nb, GL)),
-                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
+      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<8192>, dim3(ceil_div(pl.nb, GLa)),
+                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GLa));
     else if (img == 12288)
-      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<12288>, dim3(ceil_div(pl.nb, GL)),
-                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
+      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<12288>, dim3(ceil_div(pl.nb, GLa)),
+                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GLa));
     else if (EV >= 4 && EV <= 7) {
       auto* kern = EV == 4   ? okv_enc_pack_lds_kernel<kImage, 4>
                    : EV == 5 ? okv_enc_pack_lds_kernel<kImage, 5>
                    : EV == 6 ? okv_enc_pack_lds_kernel<kImage, 6>
                              : okv_enc_pack_lds_kernel<kImage, 7>;
-      hipLaunchKernelGGL(kern, dim3(ceil_div(pl.nb, GL)), dim3(kThreads), 0, ctx->stream, pp,
-                         pl.nb, uint32_t(GL));
+      hipLaunchKernelGGL(kern, dim3(ceil_div(pl.nb, GLa)), dim3(kThreads), 0, ctx->stream, pp,
+                         pl.nb, uint32_t(GLa));
     } else
-      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<kImage>, dim3(ceil_div(pl.nb, GL)),
-                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
+      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<kImage>, dim3(ceil_div(pl.nb, GLa)),
+                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GLa));
     hashed = true;
   } else if (aligned && G >= 1) {
-    const int V = EV;
+    const int V = EV == 7 ? 0 : EV;
     const dim3 grid(ceil_div(pl.nb, G)), blk(kThreads);
     if (V == 1)
       hipLaunchKernelGGL(okv_enc_pack_region_kernel<1>, grid, blk, 0, ctx->stream, pp, pl.nb,
@@ -1626,6 +1627,18 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
     else
       hipLaunchKernelGGL(okv_enc_pack_region_kernel<0>, grid, blk, 0, ctx->stream, pp, pl.nb,
                          uint32_t(G));
+#else
+  const uint64_t GL = std::min<uint64_t>(kMaxRegion, kImage / std::max<uint64_t>(pl.bmax, 1));
+  if (aligned && GL >= 1 && pl.avg_rec <= 512) {
+    // small records: record-major LDS assembly, hashes fused (the DPP-scan form)
+    hipLaunchKernelGGL((okv_enc_pack_lds_kernel<kImage, 7>), dim3(ceil_div(pl.nb, GL)),
+                       dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
+    hashed = true;
+  } else if (aligned && G >= 1) {
+    // large records: chunk-major regions
+    hipLaunchKernelGGL(okv_enc_pack_region_kernel<0>, dim3(ceil_div(pl.nb, G)), dim3(kThreads), 0,
+                       ctx->stream, pp, pl.nb, uint32_t(G));
+#endif
   } else if (o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0) {
     hipLaunchKernelGGL(okv_enc_pack_kernel, dim3(uint32_t(pl.nb)), dim3(kThreads), 0,
                        ctx->stream, pp);

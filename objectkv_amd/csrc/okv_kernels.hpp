@@ -44,6 +44,9 @@ struct Desc {         // == okv_block_desc
 __device__ __forceinline__ uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
 // Bytes [pos, pos+4) from two consecutive aligned dwords.
+// An LDS pointer for __builtin_amdgcn_global_load_lds (LDS DMA destination).
+#define OKV_LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
   return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }

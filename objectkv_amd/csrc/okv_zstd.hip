@@ -461,7 +461,15 @@ struct Out {
 // sequence stage and the executor.
 enum : int32_t { kKindDone = 0, kKindSeq = 1, kKindSlow = 2 };
 enum : uint32_t { kFlagFcs = 1, kFlagCsum = 2, kFlagRle = 4 };
-constexpr uint32_t kTabWords = 1280;  // LL [0, 512), OF [512, 768), ML [768, 1280)
+// Sequence-stage tables, 16 bits per state: symbol (6 bits) | the state's
+// FSE "next state" value x (10 bits; x in [count, 2 count), so < 2^(AL+1)).
+// nbBits = AL - floor(log2 x) and baseline = (x << nbBits) - 2^AL follow, so
+// 64 blocks' tables (160 KiB) fit one CU's LDS.
+constexpr uint32_t kTabEnt = 1280;  // LL [0, 512), OF [512, 768), ML [768, 1280)
+__device__ __forceinline__ uint16_t fse_pack16(uint32_t e, uint32_t al) {
+  const uint32_t x = (fse_base(e) + (1u << al)) >> fse_nb(e);
+  return uint16_t(fse_sym(e) | (x << 6));
+}
 struct ZBlk {
   const uint8_t* stream;  // sequence bitstream
   const uint8_t* lits;    // literal bytes (unused with kFlagRle)
@@ -480,7 +488,7 @@ struct ZBlk {
 struct Pro {
   uint8_t* lit_blk;   // literal scratch of this segment block (lit_cap bytes)
   uint64_t lit_cap;
-  uint32_t* tabs;     // kTabWords table words of this block
+  uint16_t* tabs;     // kTabEnt packed states of this block (fse_pack16)
   ZBlk* zb;
   bool deferrable;    // the compressed block being decoded may be deferred
   uint64_t fcs;
@@ -807,9 +815,11 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
   if constexpr (PRO) {
     // hand the sequences to the lane-per-block stage: tables to HBM, setup to zb
     const int lane = threadIdx.x & 63;
-    for (uint32_t u = lane; u < (1u << fs.ll_al); u += 64) pro->tabs[u] = sm.ll[u];
-    for (uint32_t u = lane; u < (1u << fs.of_al); u += 64) pro->tabs[512 + u] = sm.of[u];
-    for (uint32_t u = lane; u < (1u << fs.ml_al); u += 64) pro->tabs[768 + u] = sm.ml[u];
+    for (uint32_t u = lane; u < (1u << fs.ll_al); u += 64) pro->tabs[u] = fse_pack16(sm.ll[u], fs.ll_al);
+    for (uint32_t u = lane; u < (1u << fs.of_al); u += 64)
+      pro->tabs[512 + u] = fse_pack16(sm.of[u], fs.of_al);
+    for (uint32_t u = lane; u < (1u << fs.ml_al); u += 64)
+      pro->tabs[768 + u] = fse_pack16(sm.ml[u], fs.ml_al);
     if (lane == 0) {
       ZBlk& z = *pro->zb;
       z.stream = p + at;
@@ -1260,7 +1270,7 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
     const uint8_t* __restrict__ seg, uint64_t seg_bytes, const Desc* __restrict__ descs,
     uint32_t nblk, const uint64_t* __restrict__ cap_off, uint8_t* __restrict__ dec,
     uint64_t* __restrict__ dec_len, int32_t* __restrict__ zstatus, uint8_t* __restrict__ lits,
-    uint32_t* __restrict__ tabs, zst::ZBlk* __restrict__ zb) {
+    uint16_t* __restrict__ tabs, zst::ZBlk* __restrict__ zb) {
   __shared__ zst::SmemCore sm;
   const int lane = threadIdx.x & 63;
   for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
@@ -1282,7 +1292,7 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
       zst::Pro pro;
       pro.lit_blk = lits + cap_off[b];
       pro.lit_cap = o.cap;
-      pro.tabs = tabs + uint64_t(b) * zst::kTabWords;
+      pro.tabs = tabs + uint64_t(b) * zst::kTabEnt;
       pro.zb = zb + b;
       pro.deferrable = false;
       pro.fcs = 0;
@@ -1449,6 +1459,10 @@ __device__ __forceinline__ void wb_slide(WinBits& w) {
     return cut >= 4 ? 0u : (v & (0xffffffffu << (8 * cut)));
   };
   const uint32_t c0 = low(w.l2, w.wd - 3), c1 = low(w.l1, w.wd - 2), c2 = low(w.l0, w.wd - 1);
+  // the last reads of the dwords in flight before the next loads: those then
+  // reuse their registers (a load hoisted above these reads needs other
+  // registers and a loop-carried copy, which waits for it)
+  asm volatile("" ::"v"(c0), "v"(c1), "v"(c2) : "memory");
   const uint32_t w0 = uint32_t(w.lo), w1 = uint32_t(w.lo >> 32), w2 = uint32_t(w.hi),
                  w3 = uint32_t(w.hi >> 32);
   // C = [c0 c1 c2 w0 w1 w2 w3]; new window k = C[k + 3 - sft]
@@ -1471,30 +1485,76 @@ __device__ __forceinline__ uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t 
 
 // ---- stage 2: sequences, one lane per segment block --------------------------------
 // RFC 8878 3.1.1.3.2 / libzstd ZSTD_decodeSequence for every deferred block at
-// once: each lane owns a block's FSE states and bitstream (tables gathered from
-// HBM), checks each sequence exactly as the general kernel does and writes it
-// packed.  64 blocks advance per wave instruction.
+// once: each lane owns a block's FSE states and bitstream, checks each
+// sequence exactly as the general kernel does and writes it packed.  64 blocks
+// advance per wave instruction.  The lane chain is one table lookup per state
+// per sequence: the 64 blocks' tables live in LDS (16-bit states, 160 KiB: one
+// workgroup per CU), so a step costs its instructions plus an LDS trip, not an
+// HBM / L2 trip (the round-2/3 form gathered 32-bit states from HBM:
+// ~1900 cycles per sequence, most of it the gather's latency).
+namespace zst {
+// Extra-bits count and baseline of literal-length / match-length codes (RFC
+// 8878 3.1.1.3.2.1.1, the LL_BITS / LL_BASE / ML_BITS / ML_BASE tables above)
+// without a memory lookup.
+// All branch-free (bsel masks): the lanes are different blocks, and these
+// feed the state chain.
+__device__ __forceinline__ uint32_t msk(bool c) { return 0u - uint32_t(c); }
+__device__ __forceinline__ uint32_t ll_xbits(uint32_t c) {
+  const uint32_t mid = max(1u, (c - min(c, 16u)) >> 1);
+  return bsel(msk(c < 16), 0u, bsel(msk(c < 25), mid, c - 19));
+}
+__device__ __forceinline__ uint32_t ml_xbits(uint32_t c) {
+  const uint32_t mid = max(1u, (c - min(c, 32u)) >> 1);
+  return bsel(msk(c < 32), 0u, bsel(msk(c < 43), mid, c - 36));
+}
+// LL_BASE[16..24] - 16 and ML_BASE[32..40] - 35, 6 bits each (the same list)
+constexpr uint64_t kLLB = 0ull | (2ull << 6) | (4ull << 12) | (6ull << 18) | (8ull << 24) |
+                          (12ull << 30) | (16ull << 36) | (24ull << 42) | (32ull << 48);
+__device__ __forceinline__ uint32_t ll_base(uint32_t c) {
+  const uint32_t j = min(c - min(c, 16u), 8u), k = (c - min(c, 25u)) & 31u;
+  const uint32_t mid = 16u + uint32_t(kLLB >> (6 * j)) % 64u;
+  return bsel(msk(c < 16), c, bsel(msk(c < 25), mid, 64u << k));
+}
+__device__ __forceinline__ uint32_t ml_base(uint32_t c) {
+  const uint32_t j = min(c - min(c, 32u), 8u), k = (c - min(c, 43u)) & 31u;
+  const uint32_t mid = 35u + uint32_t(kLLB >> (6 * j)) % 64u;
+  const uint32_t hi = bsel(msk(c < 41), mid, bsel(msk(c < 42), 83u, 99u));
+  return bsel(msk(c < 32), c + 3, bsel(msk(c < 43), hi, (128u << k) + 3u));
+}
+// One packed state: symbol, nbBits and baseline (al = the table's accuracy log).
+struct St16 {
+  uint32_t sym, nb, base;
+};
+__device__ __forceinline__ St16 st16(uint32_t e, uint32_t al) {
+  const uint32_t x = e >> 6;  // >= 1 in every built table (x | 1: clz defined on garbage)
+  const uint32_t nb = al + __builtin_clz(x | 1u) - 31u;
+  return St16{e & 63u, nb, (x << nb) - (1u << al)};
+}
+}  // namespace zst
+
 __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict__ zb, uint32_t nblk,
-                                                          const uint32_t* __restrict__ tabs,
+                                                          const uint16_t* __restrict__ tabs,
                                                           const uint64_t* __restrict__ seq_off,
                                                           uint64_t* __restrict__ seqs) {
-  // Tables stay in HBM / L2: 64 blocks' tables (320 KiB) do not fit LDS, and
-  // 16 blocks per workgroup with LDS tables measured slower at C5 scale (half
-  // the blocks in flight; the lane chain is instruction-bound, not table-bound).
-  __shared__ uint32_t llb[36], mlb[53];
-  // packed sequences staged per lane and written out every kSeqStage: a global
-  // store in the loop would be waited for with the next table gathers (stores
-  // and loads retire in issue order)
-  constexpr uint32_t kSeqStage = 32;
-  __shared__ uint64_t sq[kSeqStage][64];
+  __shared__ uint16_t tl[64 * zst::kTabEnt];  // 163 840 B: this workgroup's 64 blocks' tables
   const int lane = threadIdx.x & 63;
-  if (lane < 36) llb[lane] = zst::LL_BASE[lane];
-  if (lane < 53) mlb[lane] = zst::ML_BASE[lane];
-  __syncthreads();
-  const uint32_t b = blockIdx.x * 64 + lane;
+  const uint32_t b0 = blockIdx.x * 64;
+  const uint32_t nb_wg = min(64u, nblk - b0);
+  {  // the tables of blocks [b0, b0 + nb_wg): LDS DMA, 1 KiB per wave instruction
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(tabs + uint64_t(b0) * zst::kTabEnt);
+    const uint32_t n16 = nb_wg * zst::kTabEnt * 2 / 16;  // 160 pieces of 16 B per block
+    for (uint32_t k0 = 0; k0 < n16; k0 += 64) {
+      const uint32_t k = min(k0 + uint32_t(lane), n16 - 1);  // a tail lane reloads the last piece
+      __builtin_amdgcn_global_load_lds(src + 16ull * k, OKV_LDS_PTR(reinterpret_cast<uint4*>(tl) + k0),
+                                       16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const uint32_t b = b0 + lane;
   if (b >= nblk || zb[b].kind != zst::kKindSeq) return;
   const zst::ZBlk z = zb[b];
-  const uint32_t* T = tabs + uint64_t(b) * zst::kTabWords;
+  const uint16_t* T = tl + lane * zst::kTabEnt;
   uint64_t* S = seqs + seq_off[b];
   int32_t st = zst::kOK;
   uint32_t lsum = 0, osum = 0;
@@ -1515,29 +1575,36 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
     br.lo = uint64_t(zst::lb_dw(br.f, dtop - 3)) | (uint64_t(zst::lb_dw(br.f, dtop - 2)) << 32);
     br.hi = uint64_t(zst::lb_dw(br.f, dtop - 1)) | (uint64_t(zst::lb_dw(br.f, dtop)) << 32);
     zst::wb_issue(br);
-    uint32_t sll = zst::wb_take(br, z.ll_al);
-    uint32_t sof = zst::wb_take(br, z.of_al);
-    uint32_t sml = zst::wb_take(br, z.ml_al);
+    const uint32_t lla = z.ll_al, ofa = z.of_al, mla = z.ml_al;
+    uint32_t sll = zst::wb_take(br, lla);
+    uint32_t sof = zst::wb_take(br, ofa);
+    uint32_t sml = zst::wb_take(br, mla);
     zst::wb_slide(br);
     uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
     const int32_t P0 = 8 * br.f.s0;
-    // software-pipelined: sequence i + 1's three table gathers are issued as
+    // software-pipelined: sequence i + 1's three state lookups are issued as
     // soon as its states are known, before sequence i's value work
-    uint32_t ell = T[sll], eof = T[512 + sof], eml = T[768 + sml];
-    for (uint32_t i = 0; i < z.nseq; ++i) {
-      if (br.f.P < P0) {  // libzstd: the stream overflowed before this sequence
-        st = zst::kErr;
-        break;
-      }
-      // Every field's position follows from the three entries: offset extra
+    uint32_t ell = T[sll & 511], eof = T[512 + (sof & 255)], eml = T[768 + (sml & 511)];
+    // No breaks: a failed check sets st and the loop ends at its head.  An
+    // early exit would make the window loads in flight at the latch
+    // loop-carried copies, i.e. a full wait for them (and the store) every
+    // sequence.
+    // The previous sequence's packed form is stored at the top of the next
+    // iteration: every wait for the window loads also waits for older stores
+    // (vmcnt), so the store is issued a whole sequence before that wait.
+    uint64_t pend_seq = 0;
+    for (uint32_t i = 0; i < z.nseq && st == zst::kOK; ++i) {
+      if (i) S[i - 1] = pend_seq;
+      // libzstd: the stream overflowed before this sequence
+      const bool over = br.f.P < P0;
+      // Every field's position follows from the three states: offset extra
       // bits, then ML, then LL extra bits, then the LL / ML / OF state bits
       // (read high to low).  The state bits and both length extras come out
       // of ONE 64-bit window read (<= 26 + 16 + 16 bits), the offset extras of
-      // one 32-bit read, so the chain to the next table gathers is the entries,
-      // a few adds, one extraction and the slide.
-      const uint32_t ofs = zst::fse_sym(eof), xml = zst::fse_xb(eml), xll = zst::fse_xb(ell);
-      const uint32_t nl = zst::fse_nb(ell), nm = zst::fse_nb(eml), no = zst::fse_nb(eof);
-      const uint32_t nsb = i + 1 < z.nseq ? nl + nm + no : 0u;
+      // one 32-bit read.
+      const zst::St16 L = zst::st16(ell, lla), O = zst::st16(eof, ofa), M = zst::st16(eml, mla);
+      const uint32_t ofs = O.sym, xml = zst::ml_xbits(M.sym), xll = zst::ll_xbits(L.sym);
+      const uint32_t nsb = i + 1 < z.nseq ? L.nb + M.nb + O.nb : 0u;
       const uint32_t p1 = uint32_t(br.f.P - 32 * br.wd) - ofs;  // offset extras at [p1, p1 + ofs)
       const uint32_t p4 = p1 - xml - xll - nsb;                 // state bits at [p4, p4 + nsb)
       const uint64_t e = zst::wb_get64(br, p4);
@@ -1546,17 +1613,17 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
       const uint32_t llx = uint32_t(e >> nsb) & zst::lowmask(xll);
       const uint32_t mlx = uint32_t(e >> (nsb + xll)) & zst::lowmask(xml);
       // next states (an unused last update reads nothing: nsb = 0) and their
-      // table entries, in flight during this sequence's value work
-      sll = zst::fse_base(ell) + (sbits >> (nm + no));
-      sml = zst::fse_base(eml) + ((sbits >> no) & zst::lowmask(nm));
-      sof = zst::fse_base(eof) + (sbits & zst::lowmask(no));
-      const uint32_t ml = mlb[zst::fse_sym(eml)] + mlx;
-      const uint32_t ll = llb[zst::fse_sym(ell)] + llx;
-      ell = T[sll];
-      eof = T[512 + sof];
-      eml = T[768 + sml];
+      // entries, in flight during this sequence's value work
+      sll = L.base + (sbits >> (M.nb + O.nb));
+      sml = M.base + ((sbits >> O.nb) & zst::lowmask(M.nb));
+      sof = O.base + (sbits & zst::lowmask(O.nb));
+      ell = T[sll & 511];
+      eof = T[512 + (sof & 255)];
+      eml = T[768 + (sml & 511)];
       br.f.P -= int32_t(ofs + xml + xll + nsb);
       zst::wb_slide(br);
+      const uint32_t ml = zst::ml_base(M.sym) + mlx;
+      const uint32_t ll = zst::ll_base(L.sym) + llx;
       const uint32_t ofv = (1u << ofs) + ofx;
       // repeat offsets (RFC 8878 3.1.1.5), branch-free: ofv > 3 is a new
       // offset; else idx = ofv - 1 (+1 when ll == 0) picks rep0/rep1/rep2/rep0-1
@@ -1569,32 +1636,22 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
       rep2 = sh2 ? rep1 : rep2;
       rep1 = sh1 ? rep0 : rep1;
       rep0 = sh1 ? off : rep0;
-      // execution checks (3.1.1.4), in the general kernel's order
-      if (uint64_t(lsum) + ll > z.lit_total) {
-        st = zst::kErr;
-        break;
-      }
-      const uint64_t mstart = uint64_t(osum) + ll;
-      if (mstart + ml > z.cap) {
-        st = zst::kCap;
-        break;
-      }
-      if (off > mstart) {  // before the frame start (no dictionary)
-        st = zst::kErr;
-        break;
-      }
-      sq[i % kSeqStage][lane] = zst::seq_pack(ll, ml, off);
-      if (i % kSeqStage == kSeqStage - 1) {
-        const uint32_t i0 = i - (kSeqStage - 1);
-        for (uint32_t q = 0; q < kSeqStage; ++q) S[i0 + q] = sq[q][lane];
-      }
-      lsum += ll;
-      osum += ll + ml;
+      // execution checks (3.1.1.4), in the general kernel's order; totals stay
+      // those of the sequences before a failing one
+      // (32-bit: ll, ml < 2^17 and osum <= cap, lsum <= lit_total < 2^31 while
+      // the block is live)
+      const uint32_t mstart = osum + ll;
+      st = over || lsum + ll > z.lit_total ? zst::kErr
+           : mstart + ml > z.cap          ? zst::kCap
+           : off > mstart                 ? zst::kErr
+                                          : zst::kOK;
+      // kept unconditionally (a failed block's sequences are never read)
+      pend_seq = zst::seq_pack(ll, ml, off);
+      const bool ok = st == zst::kOK;
+      lsum += ok ? ll : 0u;
+      osum += ok ? ll + ml : 0u;
     }
-    {  // the staged tail (sequences after the last full stage; a failed block's are moot)
-      const uint32_t done = st == zst::kOK ? z.nseq : 0u;
-      for (uint32_t i0 = done - done % kSeqStage, q = 0; i0 + q < done; ++q) S[i0 + q] = sq[q][lane];
-    }
+    if (st == zst::kOK && z.nseq) S[z.nseq - 1] = pend_seq;
     if (st == zst::kOK && br.f.P > P0) st = zst::kErr;  // unread bits
     if (st == zst::kOK && uint64_t(osum) + (z.lit_total - lsum) > z.cap) st = zst::kCap;
     if (st == zst::kOK && (z.flags & zst::kFlagFcs) && uint64_t(osum) + (z.lit_total - lsum) != z.fcs)
@@ -2007,7 +2064,7 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
                    size_t(nblk) * sizeof(zst::ZBlk))))
       return rc;
     if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_tabs), &ctx->z_cap_tabs,
-                   size_t(nblk) * zst::kTabWords * 4)))
+                   size_t(nblk) * zst::kTabEnt * 2 + 16)))
       return rc;
     if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_blit), &ctx->z_cap_blit, total + 64)))
       return rc;
@@ -2020,7 +2077,7 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
                                                        : nblk;
     hipLaunchKernelGGL(okv_zstd_pro_kernel, dim3(std::max(1u, std::min(nblk, pgrid))), dim3(64), 0, s,
                        seg, seg_bytes, descs, nblk, ctx->z_cap_off, ctx->z_dec, ctx->z_dec_len,
-                       ctx->z_status, ctx->z_blit, ctx->z_tabs, zb);
+                       ctx->z_status, ctx->z_blit, reinterpret_cast<uint16_t*>(ctx->z_tabs), zb);
     hipLaunchKernelGGL(okv_zstd_seqoff_kernel, dim3(1), dim3(1024), 0, s, zb, nblk,
                        ctx->z_seq_off);
     uint64_t nseq_total = 0;
@@ -2031,7 +2088,7 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
                    nseq_total * 8 + 64)))
       return rc;
     hipLaunchKernelGGL(okv_zstd_seq_kernel, dim3((nblk + 63) / 64), dim3(64), 0, s, zb, nblk,
-                       ctx->z_tabs, ctx->z_seq_off, ctx->z_seqs);
+                       reinterpret_cast<const uint16_t*>(ctx->z_tabs), ctx->z_seq_off, ctx->z_seqs);
     if (prof) (void)hipEventRecord(ev[2], s);
     // one workgroup per block by default: the dispatcher balances blocks of
     // unequal work better than a grid-stride loop (16 384 x 64 KiB: 3.8 ms vs

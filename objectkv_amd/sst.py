@@ -279,6 +279,10 @@ class Decoder:
         self._check(lib().okv_profile_read(self._ctx, ms, C.byref(n)), "okv_profile_read")
         return {"count": ms[0], "scan": ms[1], "copy": ms[2], "zstd": ms[3]}, n.value
 
+    def last_path(self) -> int:
+        """OKV_PATH_* bits: the pass-3 kernels the last decode call launched."""
+        return int(lib().okv_last_path(self._ctx))
+
     # -- host-pointer API ------------------------------------------------------
     def plan(self, seg, descs: np.ndarray, compression=COMP_NONE, index_only=False):
         s = _bytes_array(seg)

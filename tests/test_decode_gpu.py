@@ -250,32 +250,43 @@ def _mixed_segment(kinds, seed):
 
 
 @pytest.fixture(scope="module")
-def decoders_by_width():
-    """One decoder per pass-3 form, so every gather runs on the same inputs
-    whatever the average block size: OKV_GATHER_THREADS=64 (one wave per
-    block, whole block staged in LDS; batches of <= 512 blocks in the
-    single-pass fused kernel), 64u (the same with OKV_DECODE_FUSED=0: three
-    launches), 256 (LDS-staged value spans, the default for large blocks),
-    64 / 256 with OKV_GATHER_STAGED=0 and no fusion (global windows): 64g, 256g,
-    and 256 with the values produced by the address-ordered value sweep
-    (OKV_VALUE_SWEEP=1 / 2 tiles per workgroup, 5: aligned loads + lane shuffles):
-    256s, 256s2, 256a."""
-    import os
-    decs = {}
-    try:
-        for w in ("64", "64u", "64g", "256", "256g", "256s", "256s2", "256a"):
-            os.environ["OKV_GATHER_THREADS"] = w[:3].rstrip("gus")
-            os.environ["OKV_GATHER_STAGED"] = "0" if w.endswith("g") else "1"
-            os.environ["OKV_DECODE_FUSED"] = "1" if w == "64" else "0"
-            os.environ["OKV_VALUE_SWEEP"] = {"256s": "1", "256s2": "2", "256a": "5"}.get(w, "0")
-            decs[w] = okv.Decoder(0)
-    finally:
-        for k in ("OKV_GATHER_THREADS", "OKV_GATHER_STAGED", "OKV_DECODE_FUSED",
-                  "OKV_VALUE_SWEEP"):
-            os.environ.pop(k, None)
-    yield decs
-    for d in decs.values():
-        d.close()
+def nofused_decoder():
+    """A context opened with OKV_OPEN_NO_FUSED: small batches of small blocks
+    take the three-launch path (count, scan, okv_gather_small_kernel)."""
+    dec = okv.Decoder(0, flags=_lib.OPEN_NO_FUSED)
+    yield dec
+    dec.close()
+
+
+# The shipping decode paths.  Which kernels run follows from the call: the
+# average block span (segment bytes / blocks) picks the small-block kernels
+# (<= 16 KiB) or the large-block tile pass; <= 512 small blocks run the
+# single-pass fused kernel unless the context was opened with NO_FUSED; big
+# blocks (> 64 rows, or past the tile span) go to okv_copy_kernel on either.
+PATHS = ["as_given", "nofused", "large"]
+
+
+def decode_path(path, decoder, nofused, seg, d, **kw):
+    """Decode (seg, d) through one shipping path; returns (decoded, seg used).
+    "large": the segment buffer padded with zeros so the blocks average more
+    than 16 KiB (a caller decoding some blocks of a larger segment) -- every
+    block goes through the large-block pass."""
+    seg = bytes(seg)
+    if path == "large":
+        n = max(1, d.shape[0])
+        seg = seg + bytes(max(0, 16385 * n - len(seg)) + 4096)
+    dec = nofused if path == "nofused" else decoder
+    got = dec.decode(seg, d, **kw)
+    lp = dec.last_path()
+    if d.shape[0]:
+        if path == "nofused":
+            assert not lp & _lib.PATH_FUSED, lp
+        if path == "large":
+            # the large-block pass ran (not the small-block kernels)
+            assert not lp & (_lib.PATH_FUSED | _lib.PATH_SMALL), lp
+            if not kw.get("index_only"):
+                assert lp & (_lib.PATH_TILE | _lib.PATH_SWEEP), lp
+    return got, seg
 
 
 def _wide_segment(seed, nblk=120):
@@ -310,40 +321,46 @@ def _wide_segment(seed, nblk=120):
     return bytes(seg), np.array(descs, np.uint64).reshape(-1, 4)
 
 
-@pytest.mark.parametrize("width", ["256", "256g", "256s", "256s2", "256a", "64", "64u", "64g"])
-def test_wide_spans_all_gathers(decoders_by_width, width):
-    """Stage overflow (one-tile retry and global fallback), the segment's
-    first and last bytes, odd block offsets: every gather vs the oracle."""
+@pytest.mark.parametrize("path", PATHS)
+def test_wide_spans_all_paths(decoder, nofused_decoder, path):
+    """Long keys with tiny values (a value tile spans many records), stage
+    overflow, the segment's first and last bytes, odd block offsets: every
+    shipping path vs the oracle."""
     for seed in (1, 2):
         seg, d = _wide_segment(seed)
-        got = decoders_by_width[width].decode(seg, d)
-        _assert_same_as_oracle(got, seg, d, 0, False)
+        got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d)
+        _assert_same_as_oracle(got, seg2, d, 0, False)
 
 
-@pytest.mark.parametrize("width", ["64", "64u", "64g", "256", "256g", "256s", "256s2", "256a"])
-def test_mixed_blocks_both_gather_widths(decoders_by_width, width):
+@pytest.mark.parametrize("path", PATHS)
+def test_mixed_blocks_all_paths(decoder, nofused_decoder, path):
     """A segment mixing 4 KiB blocks, 64 KiB blocks with few rows and blocks
-    over kRCap rows, through the 64- and the 256-thread gather."""
+    over kRCap rows, full and index-only, through every shipping path."""
     rng = np.random.default_rng(11)
     kinds = list(rng.choice(["s", "s", "L", "M"], size=300))
     seg, d = _mixed_segment(kinds, 5)
     for index_only in (False, True):
-        got = decoders_by_width[width].decode(seg, d, index_only=index_only)
-        _assert_same_as_oracle(got, seg, d, 0, index_only)
+        got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d, index_only=index_only)
+        _assert_same_as_oracle(got, seg2, d, 0, index_only)
 
 
 @pytest.mark.parametrize("nblk", [255, 256, 257, 513])
-def test_single_tile_and_scan_paths(decoder, decoders_by_width, nblk):
+def test_single_tile_and_scan_paths(decoder, nofused_decoder, nblk):
     """<= 256 blocks: pass 1 writes the totals itself (one tile, no scan
     launch, in-kernel big-block counter reset); more: okv_scan_kernel.  Both
-    with a block over kRCap rows, against the oracle and each other."""
+    with a block over kRCap rows, through every shipping path, against the
+    oracle and each other."""
     kinds = ["s"] * nblk
     kinds[nblk // 2] = "M"
     kinds[-1] = "M"
     seg, d = _mixed_segment(kinds, nblk)
-    outs = [dec.decode(seg, d) for dec in (decoder, *decoders_by_width.values())]
-    for got in outs:
-        _assert_same_as_oracle(got, seg, d, 0, False)
+    outs = []
+    for path in PATHS:
+        got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d)
+        _assert_same_as_oracle(got, seg2, d, 0, False)
+        outs.append(got)
+    for got in outs[1:]:
+        assert got.val_arena.tobytes() == outs[0].val_arena.tobytes()
     # the same decoder again after a larger call (scratch reuse, counter reset)
     again = decoder.decode(seg, d)
     assert again.val_arena.tobytes() == outs[0].val_arena.tobytes()
@@ -367,19 +384,21 @@ def _tiny_value_segment(seed, nblk=300):
     return bytes(seg), np.array(descs, np.uint64).reshape(-1, 4)
 
 
-@pytest.mark.parametrize("width", ["256s", "256s2", "256a"])
-def test_value_sweep(decoders_by_width, width):
-    """The value sweep vs the oracle: C3 blocks, wide spans, tiny values (row
-    window overflow), a fuzz of corrupt/truncated blocks (statuses with rows
-    of other blocks around them), and an undersized value arena (capacity:
-    the kernels fall back to the per-block gather on device)."""
-    dec = decoders_by_width[width]
+@pytest.mark.parametrize("path", PATHS)
+def test_tiny_values_fuzz_and_capacity(decoder, nofused_decoder, path):
+    """C3 blocks; tiny values (thousands of rows per 4 KiB of values, many
+    rows per destination chunk); a fuzz of corrupt / truncated blocks
+    (statuses with other blocks' rows around them) -- every shipping path vs
+    the oracle.  Then an undersized value arena on the device: the blocks past
+    it report OKV_BLK_CAPACITY, the blocks before it match the oracle."""
     w = okv.synth_segment(okv.sst.SYNTH_ZIPF, 7, nblocks=96, threshold=57344, block_size=65536)
     seg, d = w.data(), w.descs()
-    _assert_same_as_oracle(dec.decode(seg, d), seg, d, 0, False)
+    got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d)
+    _assert_same_as_oracle(got, seg2, d, 0, False)
     for seed in (3, 4):
         seg, d = _tiny_value_segment(seed)
-        _assert_same_as_oracle(dec.decode(seg, d), seg, d, 0, False)
+        got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d)
+        _assert_same_as_oracle(got, seg2, d, 0, False)
     rng = np.random.default_rng(77)
     for trial in range(12):
         seg = bytearray()
@@ -402,13 +421,13 @@ def test_value_sweep(decoders_by_width, width):
             seg += body + bytes(bsize - len(body))
             descs.append((off, bsize, orig, 0))
         d = np.array(descs, np.uint64).reshape(-1, 4)
-        _assert_same_as_oracle(dec.decode(bytes(seg), d), bytes(seg), d, 0, False)
-    # device path with an undersized value arena: the blocks past it report
-    # OKV_BLK_CAPACITY (sweep unsafe: the per-block gather runs), the blocks
-    # before it match the oracle
+        got, seg2 = decode_path(path, decoder, nofused_decoder, bytes(seg), d)
+        _assert_same_as_oracle(got, seg2, d, 0, False)
+    # device path with an undersized value arena
     import torch
     w = okv.synth_segment(okv.sst.SYNTH_ZIPF, 8, nblocks=64, threshold=57344, block_size=65536)
     seg, d = w.data(), w.descs()[:64]
+    dec = nofused_decoder if path == "nofused" else decoder
     ref = dec.decode(seg, d)
     dev = torch.device("cuda", 0)
     seg_t = torch.from_numpy(seg).to(dev)

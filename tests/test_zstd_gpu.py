@@ -117,8 +117,6 @@ def test_zstd_staged_equals_general_under_corruption(decoder, one_pass_decoder):
     the oracle's -- a corrupt frame the checker rejects must fail on the
     device too, and vice versa -- and the decoded rows of the blocks that
     succeed must equal its bytes.  Both device paths, and they agree."""
-    if zmode == "general":
-        pytest.skip("compares the two paths itself")
     import random
     from tools.zstd_gen import text_zstd_segment
     seg, descs, _ = text_zstd_segment(48, 13, 3)

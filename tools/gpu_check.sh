@@ -10,7 +10,7 @@ ok() {  # continue on 0 (pass) or 1 (test failures); stop on crash/timeout
   echo "[$name] exit $rc"
   if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $name"; exit "$rc"; fi
 }
-timeout -k 10 500 python -m pytest tests -m gpu -x -q > gpurun_out/${TAG}_pytest_gpu.log 2>&1; ok $? pytest
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1; ok $? pytest
 tail -5 gpurun_out/${TAG}_pytest_gpu.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1; ok $? smoke
 tail -3 gpurun_out/${TAG}_smoke.log

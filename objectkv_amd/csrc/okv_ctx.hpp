@@ -41,7 +41,9 @@ struct okv_ctx {
   okv::Prefix* d_tile_tot = nullptr;
   okv::Prefix* d_tile_pre = nullptr;
   uint32_t* d_rec = nullptr;       // nblk x kRCap record positions (pass 1, rec_index)
-  uint32_t* d_big = nullptr;       // big-block list + its counter (d_big[nblk])
+  uint32_t* d_big = nullptr;       // big-block list [nblk]
+  uint32_t* d_ctr = nullptr;       // [0] count-kernel arrivals, [1..2] big-block counter slots
+  uint32_t big_slot = 0;           // slot the next launch counts big blocks in
   size_t cap_blocks = 0;
   // single-pass small-block decode (okv_decode_fused_kernel)
   bool fused = true;               // OKV_DECODE_FUSED=0: passes 1-3 as separate launches

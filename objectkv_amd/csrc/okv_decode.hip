@@ -5,28 +5,27 @@
 // Launches per call:
 //   1. okv_count_kernel  -- one lane per block walks the record headers in
 //      HBM, validating exactly what the Go loop validates; per block it emits
-//      (status, rows, key bytes, value bytes, end position), the positions of
-//      its first kRCap records (rec_index layout: 64-byte segments of 16
-//      records, filled by a wave's lockstep stores) and a 256-block exclusive
-//      scan.  Blocks with more rows go on the "big block" list.  Segments of
-//      <= 64 MiB with small blocks first touch every line of their blocks
-//      (prefetch), so the dependent chase hits the caches.  A one-tile launch
-//      (<= 256 blocks) zeroes the big-block counter and writes the totals
-//      itself: no memset, no scan launch.
-//   2. okv_scan_kernel   -- one workgroup scans the tile totals (> 256 blocks).
-//   3. okv_gather_kernel -- one workgroup per block: one wave rebuilds the row
-//      table in parallel (recorded positions + header reads + wave scans),
-//      writes the SoA row index, then every lane gathers 16-byte destination
-//      chunks of the packed key/value arenas straight from HBM (two aligned
-//      16-byte loads + byte funnel) and stores them whole (dwordx4); chunks
-//      spanning a row boundary are completed in registers.  Tiny LDS, so
-//      occupancy is set by registers (5 waves/SIMD).  256 threads for large
-//      blocks, 64 (one wave per block) when blocks average <= 16 KiB.
-//   4. okv_copy_kernel   -- persistent, over the big-block list only: stages
+//      (status, rows, key bytes, value bytes, end position), the positions and
+//      key lengths of its first kRCap records (block-major table, written
+//      through LDS in whole 16-byte pieces) and a 256-block exclusive scan.
+//      Blocks with more rows go on the "big block" list.  Pass 2 runs in the
+//      same launch: the workgroup that arrives last scans the tile totals
+//      (sc1 hand-off), so a decode needs no memset and no scan launch.
+//   2. pass 3, by the call's average block span:
+//      okv_tile_kernel (> 16 KiB, the C3/C5 kernel) -- one workgroup per
+//        16 KiB source tile of a block: the tile's bytes are DMA'd into LDS
+//        while wave 0 rebuilds the row table from pass 1's record table; whole
+//        value chunks go out as wave-uniform runs, keys and the chunks that
+//        mix rows by a per-lane lookup; tile 0 writes the SoA row index.
+//      okv_gather_small_kernel (<= 16 KiB blocks) -- one wave per block, the
+//        whole block staged in LDS.
+//      okv_decode_fused_kernel (<= 512 small blocks) -- passes 1-3 in one
+//        launch (replaces 1 and 2 as well).
+//   3. okv_copy_kernel   -- persistent, over the big-block list only: stages
 //      the block in LDS and chases its headers there (rare: > kRCap rows).
-// OKV_F_INDEX_ONLY writes spans into seg instead of arenas (3 + okv_index_kernel).
-// Measured alternatives to pass 3 (LDS-DMA staging, pipelined loader/gatherer,
-// persistent streaming, tile-major, ...) are in DESIGN.md §4; all slower.
+// OKV_F_INDEX_ONLY writes spans into seg instead of arenas (+ okv_index_kernel).
+// Measured alternatives to pass 3 are in DESIGN.md §4 and the ablation build
+// (-DOKV_ABLATE).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -77,8 +76,8 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     Prefix* __restrict__ tile_tot, uint32_t* __restrict__ rt_pos, uint16_t* __restrict__ rt_kl,
     uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count,
     const int32_t* __restrict__ pre_status, int prefetch, uint64_t span_cap,
-    Prefix* __restrict__ single_pre, Totals* __restrict__ single_tot,
-    uint64_t* __restrict__ single_row_start) {
+    Prefix* __restrict__ tile_pre, Totals* __restrict__ tot, uint64_t* __restrict__ row_start,
+    uint32_t* __restrict__ arrive, uint32_t* __restrict__ big_zero) {
   // slots of the current chunk: positions [lane][kRecChunk + 1] (odd stride:
   // the walking lanes' stores hit distinct banks), key lengths [lane][kRecChunk]
   __shared__ uint32_t s_pos[kThreads * (kRecChunk + 1)];
@@ -88,10 +87,9 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
   const uint32_t b = blockIdx.x * kTile + tid;
   uint64_t rows = 0, kb = 0, vb = 0, p = 0;
   int32_t st = OKV_BLK_OK;
-  if (single_pre) {
-    if (tid == 0) *big_count = 0;
-    __syncthreads();
-  }
+  // the other big-block counter slot, for the next launch (its readers, the
+  // previous decode's kernels, have completed: stream order)
+  if (blockIdx.x == 0 && tid == 0) *big_zero = 0;
   uint64_t len = 0, orig = 0, off = 0;
   bool walking = false;
   if (b < nblk) {
@@ -228,76 +226,70 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     e.bad = inc[3];
     lp[b] = e;
   }
+  // Pass 2 in the same launch: the workgroup whose arrival is counted last
+  // scans the tile totals.  Hand-off (MI355X_MICROARCH.md, inter-workgroup
+  // visibility, row 1): one lane per workgroup stores its totals with sc1
+  // stores, drains them, then adds to one counter; the last adder (told by
+  // the value its add returns) reads every total with sc1 loads.
+  __shared__ uint32_t s_last;
   if (tid == kThreads - 1) {
-    Prefix t;
-    t.rows = inc[0] + v[0];
-    t.kb = inc[1] + v[1];
-    t.vb = inc[2] + v[2];
-    t.bad = inc[3] + v[3];
-    tile_tot[blockIdx.x] = t;
-    if (single_pre) {  // what okv_scan_kernel writes for one tile
-      *single_pre = Prefix{0, 0, 0, 0};
-      *single_tot = Totals{t.rows, t.kb, t.vb, t.bad};
-      if (single_row_start) single_row_start[nblk] = t.rows;
+    const Prefix t{inc[0] + v[0], inc[1] + v[1], inc[2] + v[2], inc[3] + v[3]};
+    if (gridDim.x == 1) {
+      *tile_pre = Prefix{0, 0, 0, 0};
+      *tot = Totals{t.rows, t.kb, t.vb, t.bad};
+      if (row_start) row_start[nblk] = t.rows;
+      s_last = 0;
+    } else {
+      Prefix* q = tile_tot + blockIdx.x;
+      __hip_atomic_store(&q->rows, t.rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&q->kb, t.kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&q->vb, t.vb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&q->bad, t.bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t a =
+          __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = a == gridDim.x - 1;
     }
   }
-}
-
-// ---------------------------------------------------------------------------
-// Pass 2: exclusive scan of the tile totals (single workgroup, carried loop).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void okv_scan_kernel(const Prefix* __restrict__ tile_tot,
-                                                        uint32_t ntiles,
-                                                        Prefix* __restrict__ tile_pre,
-                                                        Totals* __restrict__ tot,
-                                                        uint64_t* __restrict__ row_start,
-                                                        uint32_t nblk) {
-  __shared__ uint64_t s_w[4][16];
-  __shared__ uint64_t s_carry[4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid < 4) s_carry[tid] = 0;
   __syncthreads();
-  for (uint32_t base = 0; base < ntiles; base += 1024) {
+  if (!s_last) return;
+  // the last workgroup: exclusive scan of gridDim.x tile totals, 256 at a time
+  uint64_t carry[4] = {0, 0, 0, 0};
+  for (uint32_t base = 0; base < gridDim.x; base += kThreads) {
     const uint32_t i = base + tid;
-    Prefix t = {0, 0, 0, 0};
-    if (i < ntiles) t = tile_tot[i];
-    uint64_t v[4] = {t.rows, t.kb, t.vb, t.bad};
-    uint64_t inc[4];
+    uint64_t x[4] = {0, 0, 0, 0};
+    if (i < gridDim.x) {
+      const Prefix* q = tile_tot + i;
+      x[0] = __hip_atomic_load(&q->rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      x[1] = __hip_atomic_load(&q->kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      x[2] = __hip_atomic_load(&q->vb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      x[3] = __hip_atomic_load(&q->bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    uint64_t in[4];
+    __syncthreads();  // s_w reuse
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      inc[k] = wave_incl_scan(v[k], lane);
-      if (lane == 63) s_w[k][wave] = inc[k];
+      in[k] = wave_incl_scan(x[k], lane);
+      if (lane == 63) s_w[k][wave] = in[k];
     }
     __syncthreads();
+    uint64_t sum[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      uint64_t off = s_carry[k];
-      for (int w = 0; w < wave; ++w) off += s_w[k][w];
-      inc[k] += off - v[k];
+      uint64_t o = carry[k];
+      for (int w = 0; w < wave; ++w) o += s_w[k][w];
+      in[k] += o - x[k];  // exclusive
+      sum[k] = s_w[k][0] + s_w[k][1] + s_w[k][2] + s_w[k][3];
     }
-    if (i < ntiles) {
-      Prefix e;
-      e.rows = inc[0];
-      e.kb = inc[1];
-      e.vb = inc[2];
-      e.bad = inc[3];
-      tile_pre[i] = e;
-    }
-    __syncthreads();
-    if (tid == 1023) {
+    if (i < gridDim.x) tile_pre[i] = Prefix{in[0], in[1], in[2], in[3]};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) s_carry[k] = inc[k] + v[k];
-    }
-    __syncthreads();
+    for (int k = 0; k < 4; ++k) carry[k] += sum[k];
   }
   if (tid == 0) {
-    Totals T;
-    T.rows = s_carry[0];
-    T.kb = s_carry[1];
-    T.vb = s_carry[2];
-    T.bad = s_carry[3];
-    *tot = T;
-    if (row_start) row_start[nblk] = T.rows;
+    *tot = Totals{carry[0], carry[1], carry[2], carry[3]};
+    if (row_start) row_start[nblk] = carry[0];
+    // every workgroup has added: reset the counter for the next launch
+    __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1070,12 +1062,13 @@ __device__ __noinline__ uint4 tile_chunk_pieces(const uint8_t* seg, uint64_t seg
   return out;
 }
 
-template <uint32_t kT, uint32_t kNT, bool kXcd, int kDiag = 0>
-__global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tpb, uint32_t ntile) {
+template <uint32_t kT, uint32_t kNT, bool kXcd, int kDiag>
+__device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uint32_t ntile) {
   // kDiag: 0 the product form (value runs); ablation arms: 1 no chunk pass,
   // 2 no DMA, 3 phase probe of the per-chunk form, 4 (+ no stores), 5 (+ no
   // data reads), 6 direct unaligned global loads, 7 phase probe of the product
-  // form, 8 the per-chunk form (every chunk looked up per lane)
+  // form, 8 the per-chunk form (every chunk looked up per lane); 9 (a launch
+  // choice) the product form without the 8-waves register cap
   constexpr bool kDirect = kDiag == 6;  // no LDS stage: one unaligned global load per chunk
   constexpr bool kChunk = (kDiag >= 3 && kDiag <= 5) || kDiag == 8;
   constexpr bool kRuns = !kChunk && !kDirect;
@@ -1113,18 +1106,26 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
                     (P.index_only ||
                      (kb0 + round16(c.kbytes) <= P.key_cap && vb0 + round16(c.vbytes) <= P.val_cap));
   const int32_t st = (c.status == OKV_BLK_OK && !fits) ? int32_t(OKV_BLK_CAPACITY) : c.status;
-  if (t == 0 && tid == 0) {
-    P.row_start[b] = row0;
-    if (P.key_base) P.key_base[b] = kb0;
-    if (P.val_base) P.val_base[b] = vb0;
-    P.blk_status[b] = st;
-  }
+  // Tile 0 writes the block outputs and the SoA row index.  Stores wait
+  // until the LDS tables are built: the compiler makes wave 0's LDS writes
+  // wait for the wave's outstanding memory operations (it cannot tell them
+  // from the DMA's LDS target).
+  auto block_outputs = [&]() {
+    if (t == 0 && tid == 0) {
+      P.row_start[b] = row0;
+      if (P.key_base) P.key_base[b] = kb0;
+      if (P.val_base) P.val_base[b] = vb0;
+      P.blk_status[b] = st;
+    }
+  };
   const uint64_t pend = c.pend;
   const uint32_t P0 = t * kT;
   // big blocks are okv_copy_kernel's (the same test as okv_count_kernel's)
   if (st != OKV_BLK_OK || c.rows == 0 || c.rows > uint64_t(kRCap) || pend > P.span_cap ||
-      pend >= (uint64_t(1) << 32) || P0 >= pend)
+      pend >= (uint64_t(1) << 32) || P0 >= pend) {
+    block_outputs();
     return;
+  }
   const uint32_t rows = uint32_t(c.rows), lastr = rows - 1;
   const uint32_t P1 = uint32_t(min<uint64_t>(uint64_t(P0) + kT, pend));
   const bool last_tile = P1 == pend;
@@ -1134,14 +1135,18 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
   const int64_t A = int64_t((off + P0) & ~uint64_t(15)) - 16;
   const int64_t E = int64_t((off + P1 + 15) & ~uint64_t(15)) + 16;
   const uint32_t np = uint32_t((E - A) >> 4);
-  if (!P.index_only && kDiag != 2 && !kDirect) {
+  // Waves 1.. issue the DMA; wave 0 builds the row table meanwhile.  (With a
+  // share of the DMA in flight, wave 0's LDS row-table writes would wait for
+  // it: the compiler cannot tell them apart from the DMA's LDS target.)
+  if (!P.index_only && kDiag != 2 && !kDirect && tid >= 64) {
     const int64_t lim = int64_t(round16(P.seg_bytes));
-    for (uint32_t k0 = 0; k0 < np; k0 += kNT) {
-      const uint32_t i = k0 + tid;
+    const uint32_t u = tid - 64;
+    for (uint32_t k0 = 0; k0 < np; k0 += kNT - 64) {
+      const uint32_t i = k0 + u;
       if (i < np) {
         int64_t a = A + (int64_t(i) << 4);
         if (a < 0 || a + 16 > lim) a = int64_t(off) & ~int64_t(15);  // bytes never used
-        __builtin_amdgcn_global_load_lds(P.seg + a, OKV_LDS_PTR(stage + k0 + (tid & ~63u)), 16,
+        __builtin_amdgcn_global_load_lds(P.seg + a, OKV_LDS_PTR(stage + k0 + (u & ~63u)), 16,
                                          0, 0);
       }
     }
@@ -1166,35 +1171,27 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
         R.pre[1][rows] = vi;
       }
     }
-    if (t == 0 && live) {  // the block's SoA row index
-      const uint64_t g = row0 + lane;
-      P.key_len[g] = uint16_t(k);
-      P.val_len[g] = v;
-      if (P.index_only) {
-        P.key_off[g] = off + ks;
-        P.val_off[g] = off + vs;
-      } else {
-        P.key_off[g] = kb0 + kp;
-        P.val_off[g] = vb0 + vp;
-      }
-    }
     if (!P.index_only) {
       // the owned ranges: [first byte whose source is >= P0, same for P1); the
       // last tile also owns the 16-byte padding after the region
       const uint32_t KT = __builtin_amdgcn_readlane(ki, lastr);
       const uint32_t VT = __builtin_amdgcn_readlane(vi, lastr);
-      auto first_at = [&](uint32_t len, uint32_t src, uint32_t pr, uint32_t tot, uint32_t Q) {
+      // (row: the lane holding that byte; lastr when none does)
+      auto first_at = [&](uint32_t len, uint32_t src, uint32_t pr, uint32_t tot, uint32_t Q,
+                          uint32_t& row) {
         const uint64_t mk = __ballot(live && len && src + len > Q);
+        row = lastr;
         if (!mk) return tot;
         const uint32_t j = uint32_t(__ffsll(static_cast<unsigned long long>(mk)) - 1);
+        row = j;
         const uint32_t s0 = __builtin_amdgcn_readlane(src, j), p0 = __builtin_amdgcn_readlane(pr, j);
         return Q > s0 ? p0 + (Q - s0) : p0;
       };
-      uint32_t X[4];
-      X[0] = first_at(k, ks, kp, KT, P0);
-      X[1] = last_tile ? uint32_t(round16(KT)) : first_at(k, ks, kp, KT, P1);
-      X[2] = first_at(v, vs, vp, VT, P0);
-      X[3] = last_tile ? uint32_t(round16(VT)) : first_at(v, vs, vp, VT, P1);
+      uint32_t X[4], jx, jv;
+      X[0] = first_at(k, ks, kp, KT, P0, jx);
+      X[1] = last_tile ? uint32_t(round16(KT)) : first_at(k, ks, kp, KT, P1, jx);
+      X[2] = first_at(v, vs, vp, VT, P0, jv);
+      X[3] = last_tile ? uint32_t(round16(VT)) : first_at(v, vs, vp, VT, P1, jx);
       if (lane == 0) {
         R.x[0] = X[0];
         R.x[1] = X[1];
@@ -1202,9 +1199,11 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
         R.x[3] = X[3];
       }
       // granule tables: gt[reg][g - (X0 >> 6)] = row holding byte max(64 g, X0);
-      // granules past the last row's bytes (padding) keep the preset lastr
+      // granules past the last row's bytes (padding) keep the preset lastr.
+      // The value-run form needs the key table only (its boundary chunks carry
+      // their row): a 4 KiB value is 64 granules, a serial per-lane loop.
 #pragma unroll
-      for (uint32_t reg = 0; reg < 2; ++reg) {
+      for (uint32_t reg = 0; reg < (kRuns ? 1u : 2u); ++reg) {
         const uint32_t X0 = X[2 * reg], X1 = X[2 * reg + 1];
         if (X1 <= X0) continue;
         const uint32_t g0 = X0 >> 6, gl = (X1 - 1) >> 6;
@@ -1234,29 +1233,56 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
           R.unit[2][u] = min(64u, wc - 64 * q);
         }
         // boundary chunks: where a piece ends inside a chunk, and the range's
-        // first chunk when it starts inside one (in order; equal neighbours skipped)
+        // first chunk when it starts inside one (in order; equal neighbours
+        // skipped), as chunk << 8 | the row holding the chunk's first owned
+        // byte: the lowest row whose piece ends in the chunk (a row before it
+        // holding that byte would end in the chunk too), or for the head chunk
+        // the row holding X2
         const bool eb = piece && (e & 15);
         const uint64_t m = __ballot(eb);
         const uint32_t head = (X2 < X3 && (X2 & 15)) ? 1u : 0u;
         const uint32_t idx = head + uint32_t(__builtin_amdgcn_mbcnt_hi(
                                         uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
-        if (eb) R.bnd[idx] = e >> 4;
+        if (eb) R.bnd[idx] = ((e >> 4) << 8) | lane;
         // read lane 63 with the whole wave active (inside the lane-0 branch the
         // compiler may compute ui for lane 0 only)
         const uint32_t nunit = __builtin_amdgcn_readlane(ui, 63);
         if (lane == 0) {
-          if (head) R.bnd[0] = X2 >> 4;
+          if (head) R.bnd[0] = ((X2 >> 4) << 8) | jv;
           R.nbnd = head + uint32_t(__builtin_popcountll(m));
           R.nunit = nunit;
         }
       }
     }
+    if (P.index_only && t == 0 && live) {  // the SoA row index (spans into seg)
+      const uint64_t g = row0 + lane;
+      P.key_len[g] = uint16_t(k);
+      P.val_len[g] = v;
+      P.key_off[g] = off + ks;
+      P.val_off[g] = off + vs;
+    }
   }
   if constexpr (kProbe) T[3] = __builtin_amdgcn_s_memrealtime();
-  if (P.index_only) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (P.index_only) {
+    block_outputs();
+    return;
+  }
+  // the DMA waves wait for their loads (wave 0 has none: its SoA stores drain
+  // on their own)
+  if (tid >= 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if constexpr (kProbe) T[4] = __builtin_amdgcn_s_memrealtime();
+  if (t == 0 && tid < 64) {  // the block outputs and SoA row index (from the LDS tables)
+    block_outputs();
+    if (lane < rows) {
+      const uint64_t g = row0 + lane;
+      const uint32_t kp = R.pre[0][lane], vp = R.pre[1][lane];
+      P.key_len[g] = uint16_t(R.pre[0][lane + 1] - kp);
+      P.val_len[g] = R.pre[1][lane + 1] - vp;
+      P.key_off[g] = kb0 + kp;
+      P.val_off[g] = vb0 + vp;
+    }
+  }
   const uint32_t kx0 = R.x[0], kx1 = R.x[1], vx0 = R.x[2], vx1 = R.x[3];
   const uint32_t nk = kx1 > kx0 ? ((kx1 + 15) >> 4) - (kx0 >> 4) : 0u;
   const uint32_t nv = vx1 > vx0 ? ((vx1 + 15) >> 4) - (vx0 >> 4) : 0u;
@@ -1279,13 +1305,14 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
     // keys and the boundary value chunks: per-lane lookup
     for (uint32_t j = tid; j < nk + nbnd; j += kNT) {
       const uint32_t reg = j >= nk;
-      if (reg && j > nk && R.bnd[j - nk] == R.bnd[j - nk - 1]) continue;
+      const uint32_t bv = reg ? R.bnd[j - nk] : 0u;
+      if (reg && j > nk && (bv >> 8) == (R.bnd[j - nk - 1] >> 8)) continue;
       const uint32_t X0 = reg ? vx0 : kx0, X1 = reg ? vx1 : kx1;
-      const uint32_t x = reg ? R.bnd[j - nk] << 4 : ((kx0 >> 4) + j) << 4;
+      const uint32_t x = reg ? (bv >> 8) << 4 : ((kx0 >> 4) + j) << 4;
       const uint32_t lo = max(x, X0), hi = min(x + 16, X1);
       const uint32_t* pre = R.pre[reg];
       const uint32_t* sb = R.sb[reg];
-      uint32_t r = gt[reg][(lo >> 6) - (X0 >> 6)];
+      uint32_t r = reg ? (bv & 255u) : uint32_t(gt[0][(lo >> 6) - (X0 >> 6)]);
       while (r < lastr && pre[r + 1] <= lo) ++r;
       uint8_t* dst = (reg ? P.val_arena + vb0 : P.key_arena + kb0) + x;
       const uint32_t dend = min(hi, pre[rows]);
@@ -1396,6 +1423,22 @@ __global__ __launch_bounds__(kNT) void okv_tile_kernel(CopyParams P, uint32_t tp
   }
 }
 
+// The product form runs 8 waves per SIMD (8 workgroups per CU: the LDS
+// bound; registers capped at 64 per lane, no spills); the ablation build also
+// has the uncapped form (70 registers, 7 waves per SIMD) as arm d9.
+template <uint32_t kT, uint32_t kNT, bool kXcd, int kDiag = 0>
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kT <= 16384 ? 8 : 4))) void okv_tile_kernel(
+    CopyParams P, uint32_t tpb, uint32_t ntile) {
+  tile_pass<kT, kNT, kXcd, kDiag>(P, tpb, ntile);
+}
+#ifdef OKV_ABLATE
+template <uint32_t kT, uint32_t kNT, bool kXcd>
+__global__ __launch_bounds__(kNT) void okv_tile_kernel_w7(CopyParams P, uint32_t tpb,
+                                                          uint32_t ntile) {
+  tile_pass<kT, kNT, kXcd, 0>(P, tpb, ntile);
+}
+#endif
+
 // Pass 3, small-block staged form (blocks averaging <= 16 KiB, e.g. 4 KiB
 // blocks): one wave per block DMAs the whole block into its LDS stage right
 // after the metadata arrives, then reads the record headers and assembles
@@ -1487,6 +1530,7 @@ struct FusedParams {
   unsigned long long base;  // its value at this call's start
   uint32_t epoch;
   Totals* tot;
+  uint32_t* big_zero;  // the other big-block counter slot: zeroed for the next launch
 };
 
 // Hand-off without release/acquire fences (an agent-scope release writes back
@@ -1529,6 +1573,7 @@ __global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, Fuse
   const uint32_t b = s_b;
   if (b >= P.nblk) return;
   const uint32_t tag = F.epoch << 2;
+  if (b == 0 && lane == 0) *F.big_zero = 0;
   // ---- pass 1 for this block (okv_count_kernel's rules) ----
   const Desc d = P.descs[b];
   const uint64_t len = (P.comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
@@ -2048,6 +2093,11 @@ int ensure_blocks(okv_ctx* ctx, uint32_t nblk) {
     (void)hipFree(ctx->d_rec);
     (void)hipFree(ctx->d_big);
   }
+  if (!ctx->d_ctr) {
+    OKV_HIP(hipMalloc(&ctx->d_ctr, 64));
+    OKV_HIP(hipMemsetAsync(ctx->d_ctr, 0, 64, ctx->stream));
+    ctx->big_slot = 0;
+  }
   OKV_HIP(hipMalloc(&ctx->d_rec, n * kRCap * sizeof(uint32_t)));
   OKV_HIP(hipMalloc(&ctx->d_big, (n + 1) * sizeof(uint32_t)));
   OKV_HIP(hipMalloc(&ctx->d_cnt, n * sizeof(BlockCount)));
@@ -2056,6 +2106,16 @@ int ensure_blocks(okv_ctx* ctx, uint32_t nblk) {
   OKV_HIP(hipMalloc(&ctx->d_tile_pre, (ntiles + 1) * sizeof(Prefix)));
   ctx->cap_blocks = n;
   return OKV_OK;
+}
+
+// Counters kept across calls (zeroed once): the count kernel's arrival
+// counter (reset by its last workgroup) and two big-block counter slots.  A
+// launch uses slot big_slot and zeroes the other one, which the next launch
+// uses: its previous readers (the kernels of the decode before) have completed
+// by then, so no memset launch is needed per decode.
+constexpr uint32_t kCtrArrive = 0, kCtrBig = 1;
+uint32_t* big_counter(okv_ctx* ctx, uint32_t other = 0) {
+  return ctx->d_ctr + kCtrBig + (ctx->big_slot ^ other);
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -2138,24 +2198,23 @@ int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_star
                 bool timed = false, uint16_t* rt_kl = nullptr, uint64_t span_cap = ~0ull) {
   int rc = ensure_blocks(ctx, nblk);
   if (rc) return rc;
-  const uint32_t ntiles = (nblk + kTile - 1) / kTile;
-  const bool single = ntiles == 1;
+  // one launch: the count walk, and the tile-total scan by its last workgroup
+  // (an empty batch still runs one workgroup: it writes the zero totals)
+  const uint32_t ntiles = std::max<uint32_t>(1, (nblk + kTile - 1) / kTile);
   // prefetch block lines before the chase when the segment fits in the caches
   // and blocks are small (dense headers); 64 KiB blocks touch ~5 % of their lines
   const int prefetch = nblk && w.seg_bytes <= (64ull << 20) && w.seg_bytes / nblk <= 16384;
-  if (!single) OKV_HIP(hipMemsetAsync(ctx->d_big + nblk, 0, sizeof(uint32_t), ctx->stream));
-  if (ntiles)
-    hipLaunchKernelGGL(okv_count_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, w.seg,
-                       w.seg_bytes, w.descs, nblk, w.comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
-                       ctx->d_rec, rt_kl, ctx->d_big, ctx->d_big + nblk, w.pre, prefetch, span_cap,
-                       single ? ctx->d_tile_pre : nullptr, single ? ctx->d_tot : nullptr,
-                       single ? d_row_start : nullptr);
-  if (timed) prof_mark(ctx, 2);
-  if (!single)
-    hipLaunchKernelGGL(okv_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, ctx->d_tile_tot,
-                       ntiles, ctx->d_tile_pre, ctx->d_tot, d_row_start, nblk);
-  if (timed) prof_mark(ctx, 3);
+  hipLaunchKernelGGL(okv_count_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, w.seg,
+                     w.seg_bytes, w.descs, nblk, w.comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
+                     ctx->d_rec, rt_kl, ctx->d_big, big_counter(ctx), w.pre, prefetch, span_cap,
+                     ctx->d_tile_pre, ctx->d_tot, d_row_start, ctx->d_ctr + kCtrArrive,
+                     big_counter(ctx, 1));
   OKV_HIP(hipGetLastError());
+  ctx->big_slot ^= 1u;  // the launch zeroes the other slot: the next launch's counter
+  if (timed) {
+    prof_mark(ctx, 2);
+    prof_mark(ctx, 3);
+  }
   return OKV_OK;
 }
 
@@ -2181,6 +2240,13 @@ TileGeo tile_geo(const okv_ctx* ctx, uint64_t seg_bytes, uint32_t nblk, bool ind
 template <uint32_t kT, uint32_t kNT, bool kXcd, int kDiag>
 void launch_tile_t(hipStream_t s, const CopyParams& P, uint32_t tpb, uint32_t ntile) {
   const uint32_t grid = kXcd ? ((ntile + 7u) & ~7u) : ntile;
+#ifdef OKV_ABLATE
+  if constexpr (kDiag == 9) {
+    hipLaunchKernelGGL((okv_tile_kernel_w7<kT, kNT, kXcd>), dim3(grid), dim3(kNT), 0, s, P, tpb,
+                       ntile);
+    return;
+  }
+#endif
   hipLaunchKernelGGL((okv_tile_kernel<kT, kNT, kXcd, kDiag>), dim3(grid), dim3(kNT), 0, s, P, tpb,
                      ntile);
 }
@@ -2201,7 +2267,8 @@ const TileForm kTileForms[] = {OKV_TILE_FORM(16, 256, 0), OKV_TILE_FORM(8, 256, 
                                OKV_TILE_FORM(16, 256, 3), OKV_TILE_FORM(16, 256, 4),
                                OKV_TILE_FORM(16, 256, 5), OKV_TILE_FORM(16, 256, 6),
                                OKV_TILE_FORM(16, 256, 7), OKV_TILE_FORM(16, 256, 8),
-                               OKV_TILE_FORM(8, 256, 8), OKV_TILE_FORM(32, 512, 8)};
+                               OKV_TILE_FORM(8, 256, 8), OKV_TILE_FORM(32, 512, 8),
+                               OKV_TILE_FORM(16, 256, 9)};
 const TileForm* tile_form(uint32_t kib, uint32_t threads, uint32_t diag) {
   for (const TileForm& f : kTileForms)
     if (f.kib == kib && f.threads == threads && f.diag == diag) return &f;
@@ -2284,9 +2351,10 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       return rc;
     rt_kl = static_cast<uint16_t*>(ctx->d_hdr);
   }
+  if ((rc = ensure_blocks(ctx, nblk))) return rc;
+  uint32_t* const big_count = big_counter(ctx);  // this decode's slot (launch_plan flips it)
   if (fused) {
-    if ((rc = ensure_blocks(ctx, nblk)) || (rc = ensure_fused(ctx, nblk))) return rc;
-    OKV_HIP(hipMemsetAsync(ctx->d_big + nblk, 0, sizeof(uint32_t), ctx->stream));
+    if ((rc = ensure_fused(ctx, nblk))) return rc;
     prof_mark(ctx, 2);
     prof_mark(ctx, 3);
   } else {
@@ -2304,7 +2372,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   P.rt_kl = rt_kl;
   P.span_cap = geo.span_cap;
   P.big_list = ctx->d_big;
-  P.big_count = ctx->d_big + nblk;
+  P.big_count = big_count;
   P.cnt = ctx->d_cnt;
   P.lp = ctx->d_lp;
   P.tile_pre = ctx->d_tile_pre;
@@ -2364,6 +2432,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       ctx->f_epoch = (ctx->f_epoch + 1) & 0x3fffffffu;
       F.epoch = ctx->f_epoch;
       F.tot = ctx->d_tot;
+      F.big_zero = big_counter(ctx, 1);
       hipLaunchKernelGGL(okv_decode_fused_kernel, dim3(nblk), dim3(64), 0, ctx->stream, P, F);
       const hipError_t le = hipGetLastError();
       if (le != hipSuccess) {
@@ -2371,6 +2440,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
         return set_err(ctx, OKV_E_HIP, "okv_decode_fused_kernel launch", le);
       }
       ctx->f_base += nblk;  // both counters advanced by nblk once the grid completes
+      ctx->big_slot ^= 1u;  // the kernel zeroed the other slot (see big_counter)
     } else if (tile) {
       if ((ctx->tile_diag >= 3 && ctx->tile_diag <= 5) || ctx->tile_diag == 7) {
         // phase probe: 8 timestamps per 256th workgroup
@@ -2634,6 +2704,7 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->d_tile_pre);
   (void)hipFree(ctx->d_rec);
   (void)hipFree(ctx->d_big);
+  (void)hipFree(ctx->d_ctr);
   (void)hipFree(ctx->f_flag);
   (void)hipFree(ctx->f_agg);
   (void)hipFree(ctx->f_incl);

@@ -408,13 +408,17 @@ def run_decode(args, torch, okv, D):
     # latency-bound pass 1 overlaps another's bandwidth-bound pass 3.  Every
     # step is still one whole-segment decode; the one-at-a-time latency is
     # reported beside it.
+    # Each in-flight decode reads its own copy of the segment (consecutive
+    # segments of a reader are different bytes: two decodes of one buffer
+    # could share its lines in the caches).
     inflight = max(1, args.decode_inflight)
-    decs, outs, streams = [dec], [out], []
+    decs, outs, streams, segs = [dec], [out], [], [seg_t]
     for i in range(1, inflight):
         streams.append(torch.cuda.Stream(dev))
         decs.append(okv.Decoder(D.local, stream=streams[-1].cuda_stream))
         outs.append(new_out())
-        decs[i].decode_device(seg_t, seg.nbytes, d_t, nblk, outs[i], compression=comp,
+        segs.append(seg_t.clone())
+        decs[i].decode_device(segs[i], seg.nbytes, d_t, nblk, outs[i], compression=comp,
                               index_only=index_only, sync=True)
         for k, v in out.items():  # each context's outputs == the verified ones
             if index_only and k in ("key_arena", "val_arena", "key_base", "val_base"):
@@ -425,7 +429,7 @@ def run_decode(args, torch, okv, D):
     def step_inflight(sync=False):
         i = turn[0] % inflight
         turn[0] += 1
-        return decs[i].decode_device(seg_t, seg.nbytes, d_t, nblk, outs[i], compression=comp,
+        return decs[i].decode_device(segs[i], seg.nbytes, d_t, nblk, outs[i], compression=comp,
                                      index_only=index_only, sync=sync)
 
     for _ in range(max(args.warmup, inflight)):

@@ -418,12 +418,23 @@ def run_decode(args, torch, okv, D):
         decs.append(okv.Decoder(D.local, stream=streams[-1].cuda_stream))
         outs.append(new_out())
         segs.append(seg_t.clone())
+        torch.cuda.synchronize(dev)  # the copy (current stream) before the decode (its stream)
         decs[i].decode_device(segs[i], seg.nbytes, d_t, nblk, outs[i], compression=comp,
                               index_only=index_only, sync=True)
         for k, v in out.items():  # each context's outputs == the verified ones
             if index_only and k in ("key_arena", "val_arena", "key_base", "val_base"):
                 continue
             assert torch.equal(outs[i][k], v), k
+    # pass 3 of each decode waits for the previous decode's pass 3 (ring of
+    # contexts, okv_decode_chain): one decode's header walk (pass 1) runs under
+    # the previous decode's pass 3, while the bandwidth-bound pass-3 kernels of
+    # two segments never share the HBM (measured: sharing it is slower).  Only
+    # for large blocks: small-block and zstd decodes are latency-bound and gain
+    # from running side by side.
+    chained = inflight > 1 and bs >= 32768 and kind != "zstd"
+    if chained:
+        for i in range(inflight):
+            decs[i].chain(decs[i - 1])
     turn = [0]
 
     def step_inflight(sync=False):
@@ -440,6 +451,9 @@ def run_decode(args, torch, okv, D):
     # the stream, 40 % of a C2 step) -----------------------------------------------
     t_max, per = D.timed(step_inflight, args.steps)
     ms_per_step = 1e3 * t_max / args.steps
+    if chained:
+        for d in decs:
+            d.chain(None)
     t_one, _ = D.timed(step, args.steps) if inflight > 1 else (t_max, per)
     for d in decs[1:]:
         d.close()
@@ -501,6 +515,7 @@ def run_decode(args, torch, okv, D):
         "original_GiB_s": round(orig_bytes * world / (t_max / args.steps) / 2**30, 3),
         "per_rank_ms_per_step": [round(1e3 * p / args.steps, 4) for p in per],
         "decodes_in_flight": inflight,
+        "pass3_chained": chained,
         "latency_ms_per_step": round(1e3 * t_one / args.steps, 4),
         "kernel_ms": {k: round(v, 4) for k, v in ms.items()},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

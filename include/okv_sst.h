@@ -170,6 +170,18 @@ int okv_decode_blocks(okv_ctx *ctx, const uint8_t *seg, uint64_t seg_bytes,
                       const okv_block_desc *descs, uint32_t nblk, int compression,
                       okv_decode_out *out, uint32_t flags);
 
+/*
+ * Consecutive-segment pipelining (a reader decoding segment after segment: a
+ * compaction feed, a scan over a level).  After okv_decode_chain(ctx, after),
+ * every decode on ctx starts its pass 3 (the bandwidth-bound kernels) only
+ * once the pass 3 last enqueued on `after` has finished.  Two contexts chained
+ * to each other, decoding alternate segments on their own streams, run each
+ * decode's header walk (pass 1, latency-bound) under the other's pass 3,
+ * while their pass-3 kernels never run concurrently.  after = NULL unchains.
+ * Both contexts must be on the same device and stay open while chained.
+ */
+int okv_decode_chain(okv_ctx *ctx, okv_ctx *after);
+
 /* After an OKV_F_ASYNC decode and okv_sync(): copy the device totals into out. */
 int okv_decode_totals(okv_ctx *ctx, okv_decode_out *out);
 

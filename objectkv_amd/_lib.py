@@ -38,6 +38,7 @@ SYMBOLS = [
     "okv_abi_version", "okv_decode_plan", "okv_decode_blocks", "okv_decode_totals",
     "okv_xxh64", "okv_hash_blocks", "okv_device_alloc", "okv_device_free", "okv_host_alloc",
     "okv_host_free", "okv_memcpy", "okv_profile", "okv_profile_read", "okv_last_path",
+    "okv_decode_chain",
     "okv_encode_rows", "okv_encode_close", "okv_encode_profile_read", "okv_encode_profile_reset",
     "okv_synth_rows_fixed", "okv_merge_rows",
     "okv_writer_new", "okv_writer_write_row", "okv_writer_close", "okv_writer_data",
@@ -170,6 +171,7 @@ def lib():
         "okv_profile": (i32, [p, i32]),
         "okv_profile_read": (i32, [p, C.POINTER(C.c_double), C.POINTER(u64)]),
         "okv_last_path": (C.c_uint32, [p]),
+        "okv_decode_chain": (i32, [p, p]),
         "okv_encode_rows": (i32, [p, C.POINTER(Rows), C.POINTER(EncodeOpts),
                                   C.POINTER(EncodeOut), u32]),
         "okv_encode_close": (i32, [p, C.POINTER(EncodeOut), u32]),

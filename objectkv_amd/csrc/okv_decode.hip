@@ -1801,7 +1801,7 @@ template <int V, class Src>
 __device__ __forceinline__ void materialise(const Src& src, const CopyParams& P,
                                            CopySmem& sm, uint64_t rows, uint64_t kbytes,
                                            uint64_t vbytes, uint64_t row0, uint64_t kb0,
-                                           uint64_t vb0) {
+                                           uint64_t vb0, uint64_t pend) {
   const uint32_t tid = threadIdx.x;
   const uint32_t Gk = group_size(kbytes / rows), Gv = group_size(vbytes / rows);
   uint64_t p = 0, kacc = 0, vacc = 0;  // chase state (lane 0)
@@ -1809,9 +1809,14 @@ __device__ __forceinline__ void materialise(const Src& src, const CopyParams& P,
     const int nb = int(rows - r0 < kRowBatch ? rows - r0 : kRowBatch);
     if (tid == 0) {
       // serial header chase: record i+1 starts at rec_i + 6 + klen_i + vlen_i
+      // (lengths and positions clamped to pass 1's totals and walk end: if the
+      // segment changed under the decode, reads stay inside the block's walk
+      // and writes inside its regions)
       for (int i = 0; i < nb; ++i) {
         uint32_t kl, vl;
         src.header(p, kl, vl);
+        kl = uint32_t(min<uint64_t>(kl, kbytes - kacc));
+        vl = uint32_t(min<uint64_t>(vl, vbytes - vacc));
         sm.s.rec[i] = p;
         sm.s.klen[i] = kl;
         sm.s.vlen[i] = vl;
@@ -1819,7 +1824,7 @@ __device__ __forceinline__ void materialise(const Src& src, const CopyParams& P,
         sm.s.vpre[i] = vacc;
         kacc += kl;
         vacc += vl;
-        p += 6 + uint64_t(kl) + uint64_t(vl);
+        p = min<uint64_t>(p + 6 + uint64_t(kl) + uint64_t(vl), pend - 6);
       }
       sm.s.kpre[nb] = kacc;
       sm.s.vpre[nb] = vacc;
@@ -1899,17 +1904,21 @@ __device__ __forceinline__ void materialise_fast(const CopyParams& P, CopySmem& 
   FastRows& t = sm.f;
   if (tid == 0) {
     // serial header chase in LDS: record i+1 starts at rec_i + 6 + klen_i + vlen_i
+    // (lengths clamped to pass 1's totals: if the segment changed under the
+    // decode, the walk still writes only inside this block's regions)
     const uint32_t* sw = reinterpret_cast<const uint32_t*>(sm.stage);
     uint32_t p = 0, ka = 0, va = 0;
     for (int i = 0; i < rows; ++i) {
       uint32_t kl, vl;
       header_lds(sw, bias + p, kl, vl);
+      kl = min(kl, uint32_t(kbytes) - ka);
+      vl = min(vl, uint32_t(vbytes) - va);
       t.rec[i] = p;
       t.kpre[i] = ka;
       t.vpre[i] = va;
       ka += kl;
       va += vl;
-      p += 6 + kl + vl;
+      p = min(p + 6 + kl + vl, uint32_t(kStage));
     }
     t.rec[rows] = p;
     t.kpre[rows] = ka;
@@ -1952,11 +1961,11 @@ __global__ __launch_bounds__(kThreads) void okv_copy_kernel(CopyParams P) {
                             B.vb0);
       } else {
         LdsSrc src{reinterpret_cast<const uint32_t*>(sm.stage), 16u + shift};
-        materialise<3>(src, P, sm, c.rows, c.kbytes, c.vbytes, B.row0, B.kb0, B.vb0);
+        materialise<3>(src, P, sm, c.rows, c.kbytes, c.vbytes, B.row0, B.kb0, B.vb0, c.pend);
       }
     } else {
       GlobalSrc src{P.seg, P.seg_bytes, d.offset};
-      materialise<3>(src, P, sm, c.rows, c.kbytes, c.vbytes, B.row0, B.kb0, B.vb0);
+      materialise<3>(src, P, sm, c.rows, c.kbytes, c.vbytes, B.row0, B.kb0, B.vb0, c.pend);
     }
     __syncthreads();  // LDS is reused by the next big block
   }
@@ -1982,7 +1991,9 @@ __global__ __launch_bounds__(kThreads) void okv_index_kernel(CopyParams P) {
       P.key_len[g] = uint16_t(kl);
       P.val_off[g] = off + p + 6 + kl;
       P.val_len[g] = vl;
-      p += 6 + uint64_t(kl) + uint64_t(vl);
+      // (clamped to pass 1's walk end: reads stay in the block if the segment
+      // changed under the decode)
+      p = min<uint64_t>(p + 6 + uint64_t(kl) + uint64_t(vl), c.pend - 6);
     }
   }
 }
@@ -2415,6 +2426,9 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
                                           ? OKV_PATH_STAGED
                                       : gt == 64 && ctx->gather_staged ? OKV_PATH_SMALL
                                                                        : OKV_PATH_GATHER));
+  // okv_decode_chain: pass 3 after the chained context's last pass 3
+  if (ctx->chain && ctx->chain->p3_rec)
+    OKV_HIP(hipStreamWaitEvent(ctx->stream, ctx->chain->p3_done, 0));
   if (nblk) {
     const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
     if (fused) {
@@ -2503,6 +2517,10 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
     else
       hipLaunchKernelGGL(okv_copy_kernel, dim3(nbig_grid), dim3(kThreads), 0, ctx->stream, P);
     OKV_HIP(hipGetLastError());
+  }
+  if (ctx->p3_done) {
+    OKV_HIP(hipEventRecord(ctx->p3_done, ctx->stream));
+    ctx->p3_rec = true;
   }
   prof_mark(ctx, 4);
   if (flags & OKV_F_ASYNC) return OKV_OK;
@@ -2705,6 +2723,7 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->d_rec);
   (void)hipFree(ctx->d_big);
   (void)hipFree(ctx->d_ctr);
+  if (ctx->p3_done) (void)hipEventDestroy(ctx->p3_done);
   (void)hipFree(ctx->f_flag);
   (void)hipFree(ctx->f_agg);
   (void)hipFree(ctx->f_incl);
@@ -2737,6 +2756,19 @@ void okv_close(okv_ctx* ctx) {
 
 const char* okv_last_error(const okv_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
 void* okv_stream(const okv_ctx* ctx) { return ctx ? ctx->stream : nullptr; }
+
+int okv_decode_chain(okv_ctx* ctx, okv_ctx* after) {
+  if (!ctx || after == ctx || (after && after->device != ctx->device))
+    return set_err(ctx, OKV_E_ARG, "okv_decode_chain: contexts");
+  for (okv_ctx* c : {ctx, after}) {
+    if (c && !c->p3_done) {
+      OKV_HIP(hipSetDevice(c->device));
+      OKV_HIP(hipEventCreateWithFlags(&c->p3_done, hipEventDisableTiming));
+    }
+  }
+  ctx->chain = after;
+  return OKV_OK;
+}
 
 int okv_sync(okv_ctx* ctx) {
   if (!ctx) return OKV_E_ARG;

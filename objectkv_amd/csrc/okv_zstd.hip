@@ -718,7 +718,9 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
     int64_t qn = csize;
     if (ltype == 2) {
       uint32_t mb;
+      const long long th = o.prof ? clock64() : 0;
       const int32_t used = read_huf_tree(sm, q, qn, mb);
+      if (o.prof) prof_add(o, 12, clock64() - th);
       if (used < 0) return kErr;
       fs.huf_ok = true;
       fs.huf_bits = mb;
@@ -812,6 +814,7 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
   if (used < 0) return kErr;
   at += used;
   if (((modes >> 2) & 3) != 3) seq_xbits(sm.ml, fs.ml_al, 2);
+  if (o.prof) prof_add(o, 10, clock64() - t1);
   if constexpr (PRO) {
     // hand the sequences to the lane-per-block stage: tables to HBM, setup to zb
     const int lane = threadIdx.x & 63;
@@ -1270,15 +1273,16 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
     const uint8_t* __restrict__ seg, uint64_t seg_bytes, const Desc* __restrict__ descs,
     uint32_t nblk, const uint64_t* __restrict__ cap_off, uint8_t* __restrict__ dec,
     uint64_t* __restrict__ dec_len, int32_t* __restrict__ zstatus, uint8_t* __restrict__ lits,
-    uint16_t* __restrict__ tabs, zst::ZBlk* __restrict__ zb) {
+    uint16_t* __restrict__ tabs, zst::ZBlk* __restrict__ zb, unsigned long long* __restrict__ prof) {
   __shared__ zst::SmemCore sm;
   const int lane = threadIdx.x & 63;
   for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const long long tw = prof ? clock64() : 0;
     const Desc d = descs[b];
     int32_t st = OKV_BLK_OK;
     int32_t kind = zst::kKindDone;
     zst::Out o;
-    o.prof = nullptr;
+    o.prof = prof;  // diagnostics (ablation build, OKV_ZSTD_PROF); null in the product
     o.base = dec + cap_off[b];
     o.cap = cap_off[b + 1] - cap_off[b];
     o.pos = o.committed = o.frame0 = 0;
@@ -1317,6 +1321,10 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
       }
     }
     __builtin_amdgcn_s_waitcnt(0);
+    if (prof && lane == 0) {
+      atomicAdd(prof + 11, (unsigned long long)(clock64() - tw));
+      atomicAdd(prof + 13, 1ull);
+    }
   }
 }
 
@@ -2059,6 +2067,13 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
     eprof = eprof_buf;
     (void)hipMemsetAsync(eprof, 0, 16 * 8 * kExecGridMax, s);
   }
+  static unsigned long long* pprof_buf = nullptr;  // prologue phase cycles (diagnostics)
+  unsigned long long* pprof = nullptr;
+  if (prof) {
+    if (!pprof_buf) (void)hipMalloc(&pprof_buf, 16 * 8);
+    pprof = pprof_buf;
+    (void)hipMemsetAsync(pprof, 0, 16 * 8, s);
+  }
   if (!general) {
     if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_zb), &ctx->z_cap_zb,
                    size_t(nblk) * sizeof(zst::ZBlk))))
@@ -2077,7 +2092,8 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
                                                        : nblk;
     hipLaunchKernelGGL(okv_zstd_pro_kernel, dim3(std::max(1u, std::min(nblk, pgrid))), dim3(64), 0, s,
                        seg, seg_bytes, descs, nblk, ctx->z_cap_off, ctx->z_dec, ctx->z_dec_len,
-                       ctx->z_status, ctx->z_blit, reinterpret_cast<uint16_t*>(ctx->z_tabs), zb);
+                       ctx->z_status, ctx->z_blit, reinterpret_cast<uint16_t*>(ctx->z_tabs), zb,
+                       pprof);
     hipLaunchKernelGGL(okv_zstd_seqoff_kernel, dim3(1), dim3(1024), 0, s, zb, nblk,
                        ctx->z_seq_off);
     uint64_t nseq_total = 0;
@@ -2131,6 +2147,13 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
             "[zstd exec] chunks %llu, cycles/chunk: load+scan %.0f map %.0f init %.0f jump %.0f "
             "(rounds %.2f) gather %.0f commit %.0f\n",
             h[9], h[0] / c, h[1] / c, h[2] / c, h[3] / c, h[8] / c, h[4] / c, h[5] / c);
+    unsigned long long pp[16] = {};
+    (void)hipMemcpy(pp, pprof, sizeof(pp), hipMemcpyDeviceToHost);
+    const double nb = pp[13] ? double(pp[13]) : 1.0;
+    fprintf(stderr,
+            "[zstd pro] blocks %llu, cycles/block: whole %.0f literals %.0f (huffman tree %.0f) "
+            "sequence tables %.0f\n",
+            pp[13], pp[11] / nb, pp[0] / nb, pp[12] / nb, pp[10] / nb);
   }
   return OKV_OK;
 }

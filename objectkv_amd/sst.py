@@ -279,6 +279,12 @@ class Decoder:
         self._check(lib().okv_profile_read(self._ctx, ms, C.byref(n)), "okv_profile_read")
         return {"count": ms[0], "scan": ms[1], "copy": ms[2], "zstd": ms[3]}, n.value
 
+    def chain(self, after: "Decoder | None") -> None:
+        """okv_decode_chain: this decoder's pass 3 waits for `after`'s last
+        pass 3 (consecutive-segment pipelining on two decoders); None unchains."""
+        self._check(lib().okv_decode_chain(self._ctx, after._ctx if after else None),
+                    "okv_decode_chain")
+
     def last_path(self) -> int:
         """OKV_PATH_* bits: the pass-3 kernels the last decode call launched."""
         return int(lib().okv_last_path(self._ctx))

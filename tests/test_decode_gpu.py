@@ -455,3 +455,60 @@ def test_tiny_values_fuzz_and_capacity(decoder, nofused_decoder, path):
         lo = int(vbase[b])
         hi = int(vbase[b + 1]) if b + 1 < 64 else vb
         assert arena[lo:hi].tobytes() == ref.val_arena[lo:hi].tobytes()
+
+
+def test_decode_chain_ring():
+    """okv_decode_chain: two decoders chained to each other (each one's pass 3
+    after the other's last pass 3) decoding alternate segments on their own
+    streams, async; every result == the oracle.  A context cannot chain to
+    itself."""
+    import torch
+    a, b = okv.Decoder(0), okv.Decoder(0)
+    try:
+        with pytest.raises(Exception):
+            a.chain(a)
+        a.chain(b)
+        b.chain(a)
+        dev = torch.device("cuda", 0)
+        cases = []
+        for seed in (5, 6):
+            w = okv.synth_segment(okv.sst.SYNTH_ZIPF, seed, nblocks=384, threshold=57344,
+                                  block_size=65536)
+            seg, d = w.data(), w.descs()[:384]
+            seg_t = torch.from_numpy(seg).to(dev)
+            d_t = torch.from_numpy(d.view(np.int64).copy()).to(dev)
+            rows, kb, vb = a.plan_device(seg_t, seg.size, d_t, 384)
+            cases.append((seg, d, seg_t, d_t, rows, kb, vb))
+        outs = []
+        for i in range(6):
+            dec = (a, b)[i % 2]
+            seg, d, seg_t, d_t, rows, kb, vb = cases[i % 2]
+            out = dict(row_start=torch.zeros(385, dtype=torch.int64, device=dev),
+                       key_base=torch.zeros(384, dtype=torch.int64, device=dev),
+                       val_base=torch.zeros(384, dtype=torch.int64, device=dev),
+                       status=torch.zeros(384, dtype=torch.int32, device=dev),
+                       key_off=torch.zeros(rows, dtype=torch.int64, device=dev),
+                       key_len=torch.zeros(rows, dtype=torch.int16, device=dev),
+                       val_off=torch.zeros(rows, dtype=torch.int64, device=dev),
+                       val_len=torch.zeros(rows, dtype=torch.int32, device=dev),
+                       key_arena=torch.zeros(kb, dtype=torch.uint8, device=dev),
+                       val_arena=torch.zeros(vb, dtype=torch.uint8, device=dev))
+            dec.decode_device(seg_t, seg.size, d_t, 384, out, sync=False)
+            outs.append((i % 2, out))
+        torch.cuda.synchronize()
+        for k, out in outs:
+            seg, d = cases[k][0], cases[k][1]
+            ref = CO.decode_soa(seg, CO.descs_array([tuple(int(x) for x in r)
+                                                     for r in d]))
+            for f, rk in (("status", "status"), ("row_start", "row_start"),
+                          ("key_len", "key_len"), ("val_len", "val_len")):
+                got = out[f].cpu().numpy()
+                assert np.array_equal(got.view(ref[rk].dtype) if got.dtype != ref[rk].dtype
+                                      else got, ref[rk]), f
+            assert out["key_arena"].cpu().numpy().tobytes() == ref["key_arena"].tobytes()
+            assert out["val_arena"].cpu().numpy().tobytes() == ref["val_arena"].tobytes()
+        a.chain(None)
+        b.chain(None)
+    finally:
+        a.close()
+        b.close()

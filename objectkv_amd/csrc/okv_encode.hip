@@ -954,9 +954,13 @@ __device__ __forceinline__ void lds_copy_field(uint32_t* img, uint32_t d, const 
 
 template <uint32_t IMG, int V = 0>  // V: diagnostic ablation (OKV_ENC_VARIANT 4: no hash,
                                    // 5: headers only, 6: loads without LDS writes;
-                                   // 7: row positions by a workgroup scan, no pl reads)
-__global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb,
-                                                                    uint32_t G) {
+                                   // 7: row positions by a workgroup scan, no pl reads (the product);
+                                   // 8: 7 without the register cap)
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(V == 7 ? 8 : 1)))
+void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
+  // V == 7, the product form: registers capped for 8 waves per SIMD (7 at 70
+  // registers uncapped); V == 8 (ablation) is the same code uncapped
+  constexpr int VL = V == 8 ? 7 : V;
   __shared__ uint4 img4[IMG / 16];
   __shared__ uint64_t bfirst[kMaxRegion + 1], brel[kMaxRegion], bbase[kMaxRegion];
   __shared__ uint32_t slim[kMaxRegion], blen[kMaxRegion];  // end of whole stripes, BlockSize
@@ -979,11 +983,11 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P
       bbase[t] = P.pbase[k0 + t];  // one trip with first[] and desc[]
     }
   }
-  __shared__ uint32_t s_wt[2][kThreads / 64];  // V == 7: per-wave record-size totals
+  __shared__ uint32_t s_wt[2][kThreads / 64];  // VL == 7: per-wave record-size totals
   __syncthreads();
   const uint64_t R0 = bfirst[0], R1 = bfirst[g];
-  uint32_t carry = 0;  // V == 7: image bytes of the rows before this pass
-  for (uint64_t base = R0; base < R1; base += kThreads) {  // uniform trip count (V == 7 barriers)
+  uint32_t carry = 0;  // VL == 7: image bytes of the rows before this pass
+  for (uint64_t base = R0; base < R1; base += kThreads) {  // uniform trip count (VL == 7 barriers)
     const uint64_t r = base + threadIdx.x;
     const bool live = r < R1;
     uint32_t kl = 0, vl = 0;
@@ -994,8 +998,8 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P
       ko = P.key_off[r];
       vo = P.val_off[r];
     }
-    uint32_t srel = 0;  // V == 7: region-relative start of record r's row stream
-    if constexpr (V == 7) {
+    uint32_t srel = 0;  // VL == 7: region-relative start of record r's row stream
+    if constexpr (VL == 7) {
       // exclusive scan of the record sizes in row order (< IMG bytes: u32)
       const uint32_t sz = live ? 6 + kl + vl : 0u;
       const uint32_t inc = wave_scan_dpp(sz);
@@ -1021,11 +1025,11 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P
       else
         hi = m;
     }
-    const uint32_t d = V == 7 ? uint32_t(brel[lo] + srel - (bbase[lo] - bbase[0]))
+    const uint32_t d = VL == 7 ? uint32_t(brel[lo] + srel - (bbase[lo] - bbase[0]))
                               : uint32_t(brel[lo] + Pg(P.pl, P.tp, int64_t(r) - 1) - bbase[lo]);
-    if (V == 5) {
+    if (VL == 5) {
       lds_or16(img, d, make_uint4(kl | (vl << 16), vl >> 16, 0, 0));
-    } else if (V == 6 && kl <= 64 && vl <= 64) {
+    } else if (VL == 6 && kl <= 64 && vl <= 64) {
       const Lines5 K = load_lines5(P.key_arena + ko, kl);
       const Lines5 Vl = load_lines5(P.val_arena + vo, vl);
       uint32_t x = 0;
@@ -1053,7 +1057,7 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P
   for (uint32_t q = threadIdx.x; q < nq; q += kThreads) {
     const uint4 v = img4[q];
     dst[q] = v;
-    if (V == 4) continue;
+    if (VL == 4) continue;
     const uint32_t p = q << 4;
     uint32_t lo = 0, hi = g;  // block holding byte p
     while (hi - lo > 1) {
@@ -1069,7 +1073,7 @@ __global__ __launch_bounds__(kThreads) void okv_enc_pack_lds_kernel(PackParams P
       img4[q] = make_uint4(uint32_t(a), uint32_t(a >> 32), uint32_t(c), uint32_t(c >> 32));
     }
   }
-  if (V == 4) return;
+  if (VL == 4) return;
   // only LDS has to be ordered here (a __syncthreads would also wait for the
   // image's global stores)
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -1604,10 +1608,11 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
     else if (img == 12288)
       hipLaunchKernelGGL(okv_enc_pack_lds_kernel<12288>, dim3(ceil_div(pl.nb, GLa)),
                          dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GLa));
-    else if (EV >= 4 && EV <= 7) {
+    else if (EV >= 4 && EV <= 8) {
       auto* kern = EV == 4   ? okv_enc_pack_lds_kernel<kImage, 4>
                    : EV == 5 ? okv_enc_pack_lds_kernel<kImage, 5>
                    : EV == 6 ? okv_enc_pack_lds_kernel<kImage, 6>
+                   : EV == 8 ? okv_enc_pack_lds_kernel<kImage, 8>
                              : okv_enc_pack_lds_kernel<kImage, 7>;
       hipLaunchKernelGGL(kern, dim3(ceil_div(pl.nb, GLa)), dim3(kThreads), 0, ctx->stream, pp,
                          pl.nb, uint32_t(GLa));

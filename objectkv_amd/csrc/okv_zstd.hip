@@ -242,43 +242,83 @@ __device__ int32_t read_ncount(const uint8_t* p, int64_t n, int16_t* norm, uint3
   return int32_t((bit + 7) >> 3);
 }
 
-// Build an FSE decoding table from normalized counts (RFC 8878 4.1.1).
-// Wave-uniform: every lane runs it, lane 0 writes.
+// Build an FSE decoding table from normalized counts (RFC 8878 4.1.1), with
+// the whole wave (called wave-uniformly by the 64 lanes of a one-wave
+// workgroup; every alphabet here has <= 64 symbols: LL 36, ML 53, OF 32,
+// Huffman weights 16).  The reference procedure is three serial loops; each is
+// restated in parallel:
+//  * low-probability symbols (count -1) take the top cells in symbol order:
+//    cell size - 1 - (their rank among the low symbols);
+//  * the spread visits positions (j * step) & mask for j = 0, 1, ..., skipping
+//    positions above the low cells; the k-th visited valid position holds the
+//    symbol s with cum[s] <= k < cum[s + 1] (counts in symbol order), so every
+//    j is placed independently (a ballot counts the valid positions before it);
+//  * cell u of symbol s gets state x = next[s] + (cells of s before u): the
+//    cells of s in a 64-cell chunk are found by six ballots over the symbol's
+//    bits, and each symbol's last cell in the chunk advances next[s].
+// The serial walk returns to position 0 exactly when the positive counts fill
+// the cells below the low ones; that is the check here.
 __device__ bool build_fse(uint32_t* table, const int16_t* norm, uint32_t nsym, uint32_t al,
                           uint16_t* next) {
-  const uint32_t size = 1u << al;
-  const bool w = (threadIdx.x & 63) == 0;
-  int32_t high = int32_t(size) - 1;
-  for (uint32_t s = 0; s < nsym; ++s) {
-    if (norm[s] == -1) {
-      if (w) table[high] = s;
-      --high;
-      if (w) next[s] = 1;
-    } else {
-      if (w) next[s] = uint16_t(norm[s]);
+  __shared__ uint16_t s_cum[64];  // first placement of each symbol
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t size = 1u << al, mask = size - 1;
+  const uint64_t below = (uint64_t(1) << lane) - 1;
+  auto mbcnt = [](uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+  };
+  const bool has = lane < nsym;
+  const int32_t nv = has ? int32_t(norm[lane]) : 0;
+  const bool low = nv == -1;
+  const uint64_t lowm = __ballot(low);
+  const int32_t high = int32_t(size) - 1 - int32_t(__builtin_popcountll(lowm));
+  if (low) table[size - 1 - mbcnt(lowm)] = lane;
+  if (has) next[lane] = low ? uint16_t(1) : uint16_t(nv);
+  const uint32_t c = nv > 0 ? uint32_t(nv) : 0u;
+  const uint32_t inc = wave_scan_dpp(c);
+  const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+  s_cum[lane] = uint16_t(inc - c);
+  __syncthreads();
+  if (int32_t(total) != high + 1) return false;
+  const uint32_t step = (size >> 1) + (size >> 3) + 3;
+  uint32_t carry = 0;
+  for (uint32_t j0 = 0; j0 < size; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    const uint32_t pos = (j * step) & mask;
+    const bool valid = j < size && int32_t(pos) <= high;
+    const uint64_t vm = __ballot(valid);
+    if (valid) {
+      const uint32_t k = carry + mbcnt(vm);
+      uint32_t lo = 0, hi = nsym;  // cum[lo] <= k < cum[hi] (cum[nsym] = total)
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_cum[mid] <= k)
+          lo = mid;
+        else
+          hi = mid;
+      }
+      table[pos] = lo;
     }
+    carry += uint32_t(__builtin_popcountll(vm));
   }
   __syncthreads();
-  const uint32_t step = (size >> 1) + (size >> 3) + 3, mask = size - 1;
-  uint32_t pos = 0;
-  for (uint32_t s = 0; s < nsym; ++s) {
-    for (int32_t i = 0; i < norm[s]; ++i) {
-      if (w) table[pos] = s;
-      do {
-        pos = (pos + step) & mask;
-      } while (int32_t(pos) > high);
+  for (uint32_t u0 = 0; u0 < size; u0 += 64) {
+    const uint32_t u = u0 + lane;
+    const bool in = u < size;
+    const uint32_t s = in ? (table[u] & 0xffu) : 0u;
+    uint64_t same = __ballot(in);
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const bool bit = (s >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      same &= bit ? bb : ~bb;
     }
-  }
-  if (pos != 0) return false;
-  __syncthreads();
-  // nbBits / baseline per state: lanes share the states (next[] updated in order by lane 0)
-  if (w) {
-    for (uint32_t u = 0; u < size; ++u) {
-      const uint32_t s = table[u] & 0xff;
-      const uint32_t x = next[s]++;
+    const uint32_t x = (in ? uint32_t(next[s]) : 0u) + mbcnt(same);
+    if (in) {
       const uint32_t nb = al - (31 - __builtin_clz(x));
       const uint32_t base = (x << nb) - size;
       table[u] = s | (nb << 8) | (base << 16);
+      if ((same & ~below & ~(uint64_t(1) << lane)) == 0) next[s] = uint16_t(x + 1);
     }
   }
   __syncthreads();
@@ -344,13 +384,21 @@ __device__ int32_t read_huf_tree(SmemCore& sm, const uint8_t* p, int64_t n, uint
     used = 1 + int32_t(csz);
   }
   __syncthreads();
+  // From here on the whole wave works in parallel (64 symbols per chunk; the
+  // reference's loops are serial over the symbols, HUF_readStats /
+  // HUF_readDTableX1 in libzstd).
+  const uint32_t lane = threadIdx.x & 63;
   // implied last weight: the weights' 2^(w-1) must sum to a power of two
-  uint32_t sum = 0;
-  for (uint32_t i = 0; i < nw; ++i) {
+  uint32_t part = 0;
+  bool wbad = false;
+  for (uint32_t i = lane; i < nw; i += 64) {
     const uint32_t w = sm.wgt[i];
-    if (w > kHufMaxBits) return -1;
-    if (w) sum += 1u << (w - 1);
+    wbad |= w > uint32_t(kHufMaxBits);
+    part += w ? (1u << (w - 1)) : 0u;
   }
+  if (__any(wbad)) return -1;
+  for (int d = 32; d; d >>= 1) part += __shfl_xor(part, d, 64);
+  const uint32_t sum = part;
   if (sum == 0) return -1;
   const uint32_t mb = 32 - __builtin_clz(sum);  // highbit(sum) + 1
   if (mb > kHufMaxBits) return -1;
@@ -360,37 +408,71 @@ __device__ int32_t read_huf_tree(SmemCore& sm, const uint8_t* p, int64_t n, uint
   if (w0) sm.wgt[nw] = uint8_t(lastw);
   const uint32_t nsym = nw + 1;
   __syncthreads();
-  // libzstd HUF_readStats: at least two weight-1 symbols, and an even count
-  {
-    uint32_t r1 = 0;
-    for (uint32_t i = 0; i < nsym; ++i) r1 += sm.wgt[i] == 1;
-    if (r1 < 2 || (r1 & 1)) return -1;
+  // per weight: symbol counts, then each symbol's rank among the symbols of
+  // its weight (symbol order), by ballots over 64-symbol chunks
+  uint32_t cnt[kHufMaxBits + 1];
+#pragma unroll
+  for (int w = 0; w <= kHufMaxBits; ++w) cnt[w] = 0;
+  for (uint32_t c0 = 0; c0 < nsym; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    const uint32_t w = i < nsym ? sm.wgt[i] : 0u;
+#pragma unroll
+    for (int k = 0; k <= kHufMaxBits; ++k) cnt[k] += uint32_t(__builtin_popcountll(__ballot(w == uint32_t(k) && i < nsym)));
   }
+  // libzstd HUF_readStats: at least two weight-1 symbols, and an even count
+  if (cnt[1] < 2 || (cnt[1] & 1)) return -1;
   // decoding table: entries grouped by weight ascending, symbols ascending
-  // within a weight; symbol of weight w covers 2^(w-1) entries, nbBits = mb + 1 - w
-  if (w0) {
-    for (uint32_t w = 0; w <= kHufMaxBits + 1; ++w) sm.rank[w] = 0;
-    for (uint32_t i = 0; i < nsym; ++i) sm.rank[sm.wgt[i]]++;
+  // within a weight; a symbol of weight w covers 2^(w-1) entries, nbBits = mb + 1 - w
+  uint32_t wstart[kHufMaxBits + 1];
+  {
     uint32_t start = 0;
-    for (uint32_t w = 1; w <= mb; ++w) {
-      const uint32_t cnt = sm.rank[w];
-      sm.rank[w] = start;
-      start += cnt << (w - 1);
+#pragma unroll
+    for (int w = 0; w <= kHufMaxBits; ++w) {
+      wstart[w] = start;
+      if (w >= 1 && uint32_t(w) <= mb) start += cnt[w] << (w - 1);
     }
-    for (uint32_t i = 0; i < nsym; ++i) {
-      const uint32_t w = sm.wgt[i];
-      sm.hstart[i] = uint16_t(w ? sm.rank[w] : 0);
-      if (w) sm.rank[w] += 1u << (w - 1);
+  }
+  uint32_t run[kHufMaxBits + 1];
+#pragma unroll
+  for (int w = 0; w <= kHufMaxBits; ++w) run[w] = 0;
+  for (uint32_t c0 = 0; c0 < nsym; c0 += 64) {
+    const uint32_t i = c0 + lane;
+    const uint32_t w = i < nsym ? sm.wgt[i] : 0u;
+    uint32_t st = 0;
+#pragma unroll
+    for (int k = 1; k <= kHufMaxBits; ++k) {
+      const uint64_t m = __ballot(w == uint32_t(k) && i < nsym);
+      const uint32_t before = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+      if (w == uint32_t(k)) st = wstart[k] + ((run[k] + before) << (k - 1));
+      run[k] += uint32_t(__builtin_popcountll(m));
     }
+    if (i < nsym) sm.hstart[i] = uint16_t(st);
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  for (uint32_t i = 0; i < nsym; ++i) {
-    const uint32_t w = sm.wgt[i];
-    if (!w) continue;
-    const uint32_t len = 1u << (w - 1), st = sm.hstart[i];
-    const uint16_t ent = uint16_t(i | ((mb + 1 - w) << 8));
-    for (uint32_t k = lane; k < len; k += 64) sm.huf[st + k] = ent;
+  // fill: symbols of <= 32 entries one per lane; longer ones by the whole wave
+  uint64_t bigm[4] = {0, 0, 0, 0};
+  for (uint32_t c0 = 0, q = 0; c0 < nsym; c0 += 64, ++q) {
+    const uint32_t i = c0 + lane;
+    const uint32_t w = i < nsym ? sm.wgt[i] : 0u;
+    const bool small = w >= 1 && w <= 6;
+    bigm[q] = __ballot(w > 6);
+    if (small) {
+      const uint32_t len = 1u << (w - 1), st = sm.hstart[i];
+      const uint16_t ent = uint16_t(i | ((mb + 1 - w) << 8));
+      for (uint32_t k = 0; k < len; ++k) sm.huf[st + k] = ent;
+    }
+  }
+  for (uint32_t q = 0; q < 4; ++q) {
+    uint64_t m = bigm[q];
+    while (m) {
+      const uint32_t i = 64 * q + uint32_t(__builtin_ctzll(m));
+      m &= m - 1;
+      const uint32_t w = sm.wgt[i];
+      const uint32_t len = 1u << (w - 1), st = sm.hstart[i];
+      const uint16_t ent = uint16_t(i | ((mb + 1 - w) << 8));
+      for (uint32_t k = lane; k < len; k += 64) sm.huf[st + k] = ent;
+    }
   }
   __syncthreads();
   max_bits = mb;
@@ -613,7 +695,7 @@ __device__ int32_t seq_table(SmemCore& sm, uint32_t* table, uint32_t mode, const
                              const uint8_t* p, int64_t n, bool& ok, uint32_t& al) {
   switch (mode) {
     case 0: {  // Predefined_Mode
-      for (uint32_t s = 0; s < def_n; ++s) sm.norm[s] = def[s];
+      for (uint32_t s = threadIdx.x & 63; s < def_n; s += 64) sm.norm[s] = def[s];
       __syncthreads();
       if (!build_fse(table, sm.norm, def_n, def_al, sm.next)) return -1;
       ok = true;

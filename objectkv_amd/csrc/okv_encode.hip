@@ -955,11 +955,12 @@ __device__ __forceinline__ void lds_copy_field(uint32_t* img, uint32_t d, const 
 template <uint32_t IMG, int V = 0>  // V: diagnostic ablation (OKV_ENC_VARIANT 4: no hash,
                                    // 5: headers only, 6: loads without LDS writes;
                                    // 7: row positions by a workgroup scan, no pl reads (the product);
-                                   // 8: 7 without the register cap)
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(V == 7 ? 8 : 1)))
+                                   // 8: 7 with registers capped for 8 waves)
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(V == 8 ? 8 : 1)))
 void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
-  // V == 7, the product form: registers capped for 8 waves per SIMD (7 at 70
-  // registers uncapped); V == 8 (ablation) is the same code uncapped
+  // V == 7, the product form (70 registers, 7 waves per SIMD); V == 8
+  // (ablation) is the same code capped at 64 registers for 8 waves: it spills
+  // (9 registers) and measured 4.88 vs 3.85 ms (profiles/r3/r3g/ablate_enc.log)
   constexpr int VL = V == 8 ? 7 : V;
   __shared__ uint4 img4[IMG / 16];
   __shared__ uint64_t bfirst[kMaxRegion + 1], brel[kMaxRegion], bbase[kMaxRegion];

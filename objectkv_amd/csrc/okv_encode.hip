@@ -961,7 +961,10 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
   // V == 7, the product form (70 registers, 7 waves per SIMD); V == 8
   // (ablation) is the same code capped at 64 registers for 8 waves: it spills
   // (9 registers) and measured 4.88 vs 3.85 ms (profiles/r3/r3g/ablate_enc.log)
-  constexpr int VL = V == 8 ? 7 : V;
+  // V == 9 (ablation): 7 with the block hashes computed by wave 0 from the
+  // raw image while waves 1-3 store it (no second barrier, no precompute)
+  constexpr bool kOverlap = V == 9;
+  constexpr int VL = (V == 8 || V == 9) ? 7 : V;
   __shared__ uint4 img4[IMG / 16];
   __shared__ uint64_t bfirst[kMaxRegion + 1], brel[kMaxRegion], bbase[kMaxRegion];
   __shared__ uint32_t slim[kMaxRegion], blen[kMaxRegion];  // end of whole stripes, BlockSize
@@ -1050,11 +1053,17 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
     }
   }
   __syncthreads();
+  uint4* dst = reinterpret_cast<uint4*>(P.seg + O0);
+  if constexpr (kOverlap) {
+    if (threadIdx.x >= 64) {
+      for (uint32_t q = threadIdx.x - 64; q < nq; q += kThreads - 64) dst[q] = img4[q];
+      return;
+    }
+  } else {
   // Store the image; each 16 bytes lying in whole 32-byte stripes of its block
   // are then replaced in place (same lane, so no barrier between) by their two
   // XXH64 round inputs x * PRIME64_2, computed by all 256 lanes: the four
   // hashing lanes per block are left with add, rotate, multiply per round.
-  uint4* dst = reinterpret_cast<uint4*>(P.seg + O0);
   for (uint32_t q = threadIdx.x; q < nq; q += kThreads) {
     const uint4 v = img4[q];
     dst[q] = v;
@@ -1078,6 +1087,7 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
   // only LDS has to be ordered here (a __syncthreads would also wait for the
   // image's global stores)
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
   // BlockStat.Hash = XXH64 of the padded block (segment_writer.go:185), from
   // the image: four lanes per block own XXH64's four accumulators.
   if (threadIdx.x < 4 * g) {
@@ -1093,9 +1103,10 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) x[u] = w64[4 * (st + u) + q];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc = xround_pre(acc, x[u]);
+      for (int u = 0; u < 8; ++u) acc = kOverlap ? xround(acc, x[u]) : xround_pre(acc, x[u]);
     }
-    for (; st < nstripe; ++st) acc = xround_pre(acc, w64[4 * st + q]);
+    for (; st < nstripe; ++st)
+      acc = kOverlap ? xround(acc, w64[4 * st + q]) : xround_pre(acc, w64[4 * st + q]);
     const int lane = threadIdx.x & 63;
     const uint64_t a1 = __shfl(acc, (lane & ~3) + 1, 64);
     const uint64_t a2 = __shfl(acc, (lane & ~3) + 2, 64);
@@ -1609,11 +1620,12 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
     else if (img == 12288)
       hipLaunchKernelGGL(okv_enc_pack_lds_kernel<12288>, dim3(ceil_div(pl.nb, GLa)),
                          dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GLa));
-    else if (EV >= 4 && EV <= 8) {
+    else if (EV >= 4 && EV <= 9) {
       auto* kern = EV == 4   ? okv_enc_pack_lds_kernel<kImage, 4>
                    : EV == 5 ? okv_enc_pack_lds_kernel<kImage, 5>
                    : EV == 6 ? okv_enc_pack_lds_kernel<kImage, 6>
                    : EV == 8 ? okv_enc_pack_lds_kernel<kImage, 8>
+                   : EV == 9 ? okv_enc_pack_lds_kernel<kImage, 9>
                              : okv_enc_pack_lds_kernel<kImage, 7>;
       hipLaunchKernelGGL(kern, dim3(ceil_div(pl.nb, GLa)), dim3(kThreads), 0, ctx->stream, pp,
                          pl.nb, uint32_t(GLa));

@@ -186,13 +186,49 @@ __device__ __forceinline__ uint32_t bitr_peek(BitR& b, uint32_t nb) {
 }
 __device__ __forceinline__ void bitr_skip(BitR& b, uint32_t nb) { b.pos -= nb; }
 
+// Wave register window over a short stream (table descriptions): 256 bytes
+// from the stream's aligned base, one dword per lane, bytes outside [0, n)
+// zero.  Reads are wave-uniform: v_readlane of the two dwords around a bit
+// position, so a serial header decode waits on no memory after the one load.
+struct RegWin {
+  uint32_t w;     // this lane's dword
+  int32_t boff;   // window bit of the stream's bit 0
+};
+__device__ __forceinline__ RegWin regwin_load(const uint8_t* p, int64_t n) {
+  const uintptr_t pa = reinterpret_cast<uintptr_t>(p), base = pa & ~uintptr_t(3);
+  const uintptr_t a = base + 4 * (threadIdx.x & 63);
+  const int64_t rel = int64_t(a) - int64_t(pa);  // stream byte of the dword's first byte
+  uint32_t v = 0;
+  if (rel + 4 > 0 && rel < n) v = *reinterpret_cast<const uint32_t*>(a);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (rel + k < 0 || rel + k >= n) v &= ~(0xffu << (8 * k));
+  return RegWin{v, int32_t(8 * (pa - base))};
+}
+// Window bits fit: stream bits [b, b + 32) lie below the window's end.
+__device__ __forceinline__ bool regwin_has(const RegWin& r, int64_t b) {
+  return r.boff + b + 32 <= 64 * 32;
+}
+// Stream bits [b, b + 32) (b may be negative: bits below the stream read 0).
+__device__ __forceinline__ uint32_t regwin_get32(const RegWin& r, int32_t b) {
+  const int32_t A = r.boff + b;
+  const int32_t d = A >> 5;
+  const uint32_t lo = __builtin_amdgcn_readlane(r.w, d & 63);
+  const uint32_t hi = __builtin_amdgcn_readlane(r.w, (d + 1) & 63);
+  return __builtin_amdgcn_alignbit(d + 1 >= 0 && d + 1 < 64 ? hi : 0u, d >= 0 && d < 64 ? lo : 0u,
+                                   uint32_t(A) & 31u);
+}
+
 // ---- FSE ---------------------------------------------------------------------
 // FSE_readNCount (RFC 8878 4.1.1): forward bitstream at p[0, n); fills norm[]
 // (max_sym + 1 entries), returns bytes consumed or -1.
 __device__ int32_t read_ncount(const uint8_t* p, int64_t n, int16_t* norm, uint32_t max_sym,
                                uint32_t max_al, uint32_t& al_out, uint32_t& nsym_out) {
   int64_t bit = 0;
-  auto peek = [&](uint32_t k) -> uint32_t {
+  const RegWin win = regwin_load(p, n);  // the description is read from registers
+  auto peek = [&](uint32_t k) -> uint32_t {  // k <= 10
+    if (regwin_has(win, bit))
+      return regwin_get32(win, int32_t(bit)) & ((1u << k) - 1u);
     const uint64_t v = ld64z(p, bit >> 3, n) >> (bit & 7);
     return uint32_t(v & ((uint64_t(1) << k) - 1));
   };
@@ -343,10 +379,9 @@ __device__ int32_t read_huf_tree(SmemCore& sm, const uint8_t* p, int64_t n, uint
     nw = hb - 127;
     used = 1 + int32_t((nw + 1) / 2);
     if (used > n) return -1;
-    for (uint32_t i = 0; i < nw; ++i) {
+    for (uint32_t i = threadIdx.x & 63; i < nw; i += 64) {
       const uint32_t byte = p[1 + i / 2];
-      const uint32_t v = (i & 1) ? (byte & 15) : (byte >> 4);
-      if (w0) sm.wgt[i] = uint8_t(v);
+      sm.wgt[i] = uint8_t((i & 1) ? (byte & 15) : (byte >> 4));
     }
   } else {  // FSE-compressed weights, two interleaved states
     const int64_t csz = hb;
@@ -355,28 +390,42 @@ __device__ int32_t read_huf_tree(SmemCore& sm, const uint8_t* p, int64_t n, uint
     const int32_t hlen = read_ncount(p + 1, csz, sm.norm, 15, 6, al, nsym);
     if (hlen < 0) return -1;
     if (!build_fse(sm.hw, sm.norm, nsym, al, sm.next)) return -1;
-    BitR br;
-    if (!bitr_init(br, p + 1 + hlen, csz - hlen)) return -1;
-    uint32_t s1 = bitr_read(br, al), s2 = bitr_read(br, al);
+    // The weight stream (< 128 bytes) and the table (<= 64 states, lane =
+    // state) live in registers: the serial decode below reads both with
+    // v_readlane, no memory round trip per weight (bits below the stream
+    // read as 0, RFC 8878 4.2.1.2).
+    const int64_t wn = csz - hlen;
+    if (wn <= 0) return -1;
+    const RegWin win = regwin_load(p + 1 + hlen, wn);
+    const uint32_t last = regwin_get32(win, int32_t(8 * (wn - 1))) & 0xffu;
+    if (last == 0) return -1;  // the final byte holds the end marker
+    int32_t pos = int32_t(8 * (wn - 1)) + (31 - __builtin_clz(last));
+    const uint32_t hwv = sm.hw[(threadIdx.x & 63) & ((1u << al) - 1u)];
+    auto rd = [&](uint32_t k) -> uint32_t {  // bits [pos - k, pos), consumed (k <= 6)
+      pos -= int32_t(k);
+      return k ? (regwin_get32(win, pos) & ((1u << k) - 1u)) : 0u;
+    };
+    auto ent = [&](uint32_t st) { return uint32_t(__builtin_amdgcn_readlane(hwv, st & 63u)); };
+    uint32_t s1 = rd(al), s2 = rd(al);
     nw = 0;
     for (;;) {
       if (nw >= 255) return -1;
-      uint32_t e = sm.hw[s1];
+      uint32_t e = ent(s1);
       if (w0) sm.wgt[nw] = uint8_t(fse_sym(e));
       ++nw;
-      s1 = fse_base(e) + bitr_read(br, fse_nb(e));
-      if (br.pos < 0) {  // overflow: the other state's symbol ends the list
-        if (w0) sm.wgt[nw] = uint8_t(fse_sym(sm.hw[s2]));
+      s1 = fse_base(e) + rd(fse_nb(e));
+      if (pos < 0) {  // overflow: the other state's symbol ends the list
+        if (w0) sm.wgt[nw] = uint8_t(fse_sym(ent(s2)));
         ++nw;
         break;
       }
       if (nw >= 255) return -1;
-      e = sm.hw[s2];
+      e = ent(s2);
       if (w0) sm.wgt[nw] = uint8_t(fse_sym(e));
       ++nw;
-      s2 = fse_base(e) + bitr_read(br, fse_nb(e));
-      if (br.pos < 0) {
-        if (w0) sm.wgt[nw] = uint8_t(fse_sym(sm.hw[s1]));
+      s2 = fse_base(e) + rd(fse_nb(e));
+      if (pos < 0) {
+        if (w0) sm.wgt[nw] = uint8_t(fse_sym(ent(s1)));
         ++nw;
         break;
       }
@@ -503,20 +552,34 @@ __device__ bool huf_stream(const SmemCore& sm, uint32_t mb, const uint8_t* p, in
   uint32_t r[8];  // raw dwords cd - 1 - k
 #pragma unroll
   for (int k = 0; k < 8; ++k) r[k] = raw(cd - 1 - k);
-  for (uint32_t i = 0; i < cnt; ++i) {
-    // invariant: 32 cd <= P < 32 cd + 64; a literal takes <= mb <= 11 bits
-    if (P - int32_t(mb) < 32 * cd) {
+  auto refill = [&](int32_t need) {  // make bits [P - need, P) available
+    if (P - need < 32 * cd) {
       c = (c << 32) | fix(r[0], cd - 1);
       --cd;
 #pragma unroll
       for (int k = 0; k < 7; ++k) r[k] = r[k + 1];
       r[7] = raw(cd - 8);
     }
+  };
+  auto literal = [&](uint32_t i) {
     const int32_t p0 = P - int32_t(mb);
     const uint32_t idx = uint32_t(c >> uint32_t(p0 - 32 * cd)) & ((1u << mb) - 1u);
     const uint32_t e = sm.huf[idx];
     out[i] = uint8_t(e & 0xff);
     P -= int32_t(e >> 8);
+  };
+  // invariant: 32 cd <= P < 32 cd + 64; a literal takes <= mb <= 11 bits, so
+  // one refill check (at most one dword) covers two literals: the lanes are
+  // different streams, and each check is a divergent branch
+  uint32_t i = 0;
+  for (; i + 1 < cnt; i += 2) {
+    refill(2 * int32_t(mb));
+    literal(i);
+    literal(i + 1);
+  }
+  if (i < cnt) {
+    refill(int32_t(mb));
+    literal(i);
   }
   return P == B0;
 }

@@ -31,9 +31,10 @@
 extern "C" {
 #endif
 
-#define OKV_ABI_VERSION 3 /* 2: okv_encode_opts.bloom / bloom_len, and okv_profile_read writes
+#define OKV_ABI_VERSION 4 /* 2: okv_encode_opts.bloom / bloom_len, and okv_profile_read writes
                              4 doubles (ms[4]: the zstd stage slot was added);
-                             3: okv_open_ex / okv_open_opts */
+                             3: okv_open_ex / okv_open_opts
+                             4: okv_decode_chain */
 
 /* ---- return codes (int) -------------------------------------------------- */
 #define OKV_OK 0

@@ -625,8 +625,8 @@ struct ZBlk {
   uint32_t ll_al, of_al, ml_al, rle_byte;
   int32_t kind;           // kKindDone / kKindSeq / kKindSlow
   int32_t st;             // kOK / kErr / kCap of the stage that owns the block
-  uint32_t out_len;       // decompressed bytes
-  uint32_t lsum;          // literals consumed by the sequences (sequence stage)
+  uint32_t nseq_ok;       // sequences the sequence stage decoded (all unless the stream overflowed)
+  uint32_t pad_;
 };
 
 // Prologue context of one block: per-block literal scratch and table slots.
@@ -1629,10 +1629,16 @@ __device__ __forceinline__ void wb_slide(WinBits& w) {
   wb_issue(w);
 }
 
-// Packed sequence: ll (18 bits) | ml (18 bits) << 18 | offset (28 bits) << 36;
-// the executor re-derives nothing, so the checks of stage 2 bound every field.
-__device__ __forceinline__ uint64_t seq_pack(uint32_t ll, uint32_t ml, uint32_t off) {
-  return uint64_t(ll) | (uint64_t(ml) << 18) | (uint64_t(off) << 36);
+// Packed sequence, as the bitstream gives it: literal-length code (6 bits) |
+// its extra bits (16) << 6 | match-length code (6) << 22 | extra bits (16) << 28
+// | offset (20, saturated) << 44.  The executor turns codes into lengths and
+// makes the execution checks (RFC 8878 3.1.1.4) in sequence order; an offset
+// past 2^20 - 1 is past any single-block frame's output (<= 128 KiB), so the
+// saturated value fails the same check.
+__device__ __forceinline__ uint64_t seq_pack(uint32_t llc, uint32_t llx, uint32_t mlc, uint32_t mlx,
+                                             uint32_t off) {
+  return uint64_t(llc | (llx << 6) | (mlc << 22)) | (uint64_t(mlx) << 28) |
+         (uint64_t(min(off, 0xfffffu)) << 44);
 }
 }  // namespace zst
 
@@ -1710,7 +1716,7 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
   const uint16_t* T = tl + lane * zst::kTabEnt;
   uint64_t* S = seqs + seq_off[b];
   int32_t st = zst::kOK;
-  uint32_t lsum = 0, osum = 0;
+  uint32_t nok = 0;  // sequences decoded before any overflow
   zst::WinBits br;
   {
     const uintptr_t a = reinterpret_cast<uintptr_t>(z.stream);
@@ -1775,13 +1781,12 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
       eml = T[768 + (sml & 511)];
       br.f.P -= int32_t(ofs + xml + xll + nsb);
       zst::wb_slide(br);
-      const uint32_t ml = zst::ml_base(M.sym) + mlx;
-      const uint32_t ll = zst::ll_base(L.sym) + llx;
       const uint32_t ofv = (1u << ofs) + ofx;
       // repeat offsets (RFC 8878 3.1.1.5), branch-free: ofv > 3 is a new
-      // offset; else idx = ofv - 1 (+1 when ll == 0) picks rep0/rep1/rep2/rep0-1
+      // offset; else idx = ofv - 1 (+1 when ll == 0, i.e. literal-length
+      // code 0: every other code's baseline is >= 1) picks rep0/rep1/rep2/rep0-1
       const bool fresh = ofv > 3;
-      const uint32_t idx = ofv - 1 + (ll == 0 ? 1u : 0u);  // 0..3 when !fresh
+      const uint32_t idx = ofv - 1 + (L.sym == 0 ? 1u : 0u);  // 0..3 when !fresh
       uint32_t t = idx == 3 ? rep0 - 1 : (idx == 1 ? rep1 : rep2);
       t += t == 0;  // libzstd: offset 0 is corrupt input, forced to 1
       const uint32_t off = fresh ? ofv - 3 : (idx == 0 ? rep0 : t);
@@ -1789,30 +1794,17 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
       rep2 = sh2 ? rep1 : rep2;
       rep1 = sh1 ? rep0 : rep1;
       rep0 = sh1 ? off : rep0;
-      // execution checks (3.1.1.4), in the general kernel's order; totals stay
-      // those of the sequences before a failing one
-      // (32-bit: ll, ml < 2^17 and osum <= cap, lsum <= lit_total < 2^31 while
-      // the block is live)
-      const uint32_t mstart = osum + ll;
-      st = over || lsum + ll > z.lit_total ? zst::kErr
-           : mstart + ml > z.cap          ? zst::kCap
-           : off > mstart                 ? zst::kErr
-                                          : zst::kOK;
-      // kept unconditionally (a failed block's sequences are never read)
-      pend_seq = zst::seq_pack(ll, ml, off);
-      const bool ok = st == zst::kOK;
-      lsum += ok ? ll : 0u;
-      osum += ok ? ll + ml : 0u;
+      // the stream overflowed before this sequence: it is not stored; the
+      // execution checks of the sequences before it come first (executor)
+      st = over ? zst::kErr : zst::kOK;
+      pend_seq = zst::seq_pack(L.sym, llx, M.sym, mlx, off);
+      nok += over ? 0u : 1u;
     }
     if (st == zst::kOK && z.nseq) S[z.nseq - 1] = pend_seq;
     if (st == zst::kOK && br.f.P > P0) st = zst::kErr;  // unread bits
-    if (st == zst::kOK && uint64_t(osum) + (z.lit_total - lsum) > z.cap) st = zst::kCap;
-    if (st == zst::kOK && (z.flags & zst::kFlagFcs) && uint64_t(osum) + (z.lit_total - lsum) != z.fcs)
-      st = zst::kErr;  // Frame_Content_Size check
   }
-  zb[b].st = st;
-  zb[b].lsum = lsum;
-  zb[b].out_len = osum + (z.lit_total - lsum);
+  zb[b].st = st;  // the executor ranks it after the sequences' own checks
+  zb[b].nseq_ok = nok;
 }
 
 // ---- stage 3: execution, one wave per segment block --------------------------------
@@ -1856,33 +1848,111 @@ static_assert(kExecOut <= zst::kChunkOut && kExecOut % 1024 == 0, "exec chunk");
 constexpr uint32_t kExecGridMax = 16384;
 __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
     const zst::ZBlk* __restrict__ zb, uint32_t nblk, const uint64_t* __restrict__ seq_off,
-    const uint64_t* __restrict__ seqs, const uint64_t* __restrict__ cap_off,
+    uint64_t* __restrict__ seqs, const uint64_t* __restrict__ cap_off,
     uint8_t* __restrict__ dec, uint64_t* __restrict__ dec_len, int32_t* __restrict__ zstatus,
     unsigned long long* __restrict__ prof) {
   __shared__ uint4 rec[zst::kSeqChunk + 1];
   __shared__ uint32_t srcx[kExecOut];
   __shared__ uint8_t map[kExecOut];
+  __shared__ uint32_t lbase[64], mbase[64];  // literal / match length baselines by code
   const int lane = threadIdx.x & 63;
+  lbase[lane] = zst::ll_base(uint32_t(lane) < 36 ? uint32_t(lane) : 0u);
+  mbase[lane] = zst::ml_base(uint32_t(lane) < 53 ? uint32_t(lane) : 0u);
+  __syncthreads();
   unsigned long long pacc[10] = {};
   for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
     const int32_t kind = zst::rfl(uint32_t(zb[b].kind));
     if (kind != zst::kKindSeq) continue;
+    // the sequence stage's outcome (stream overflow, unread bits) ranks after
+    // the execution checks of the sequences it decoded: those run here, in
+    // sequence order, before any sequence is executed (RFC 8878 3.1.1.4; the
+    // general kernel's order).  A failed block executes nothing more.
     const int32_t st0 = zst::rfl(uint32_t(zb[b].st));
-    if (st0 != zst::kOK) {
-      if (lane == 0) {
-        zstatus[b] = st0 == zst::kCap ? OKV_BLK_CAPACITY : OKV_BLK_ZSTD_ERROR;
-        dec_len[b] = 0;
-      }
-      continue;
-    }
-    const uint32_t nseq = zst::rfl(zb[b].nseq), lit_total = zst::rfl(zb[b].lit_total);
+    const bool exec = st0 == zst::kOK;
+    int32_t bst = zst::kOK;
+    const uint32_t nseq = zst::rfl(zb[b].nseq_ok), lit_total = zst::rfl(zb[b].lit_total);
+    const uint32_t zcap = zst::rfl(zb[b].cap);
     const uint32_t flags = zst::rfl(zb[b].flags);
     const bool rle = flags & zst::kFlagRle;
     const uint8_t rle_byte = uint8_t(zst::rfl(zb[b].rle_byte));
     const uint8_t* lits = zst::rflp(zb[b].lits);
     uint8_t* out = dec + zst::rfl64(cap_off[b]);
-    const uint64_t* S = seqs + zst::rfl64(seq_off[b]);
+    uint64_t* S = seqs + zst::rfl64(seq_off[b]);
+    // execution checks (3.1.1.4) in sequence order, before anything runs; the
+    // block's totals for the end checks.  A failed block executes nothing.
     uint32_t O = 0, lp = 0;
+    // (the next window's sequences are loaded while this one is checked: the
+    // pass is a chain of windows per block)
+    uint64_t nx[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) nx[u] = nseq ? S[min(4u * lane + u, nseq - 1)] : 0;
+    for (uint32_t i0 = 0; i0 < nseq; i0 += 256) {
+      const uint32_t nrem = nseq - i0;
+      uint64_t cur[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        cur[u] = nx[u];
+        nx[u] = S[min(i0 + 256 + 4u * lane + u, nseq - 1)];
+      }
+      uint32_t lt = 0, ot = 0, ll[4], ml[4], of[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t k = 4 * lane + u;
+        const uint64_t vr = cur[u];
+        const uint32_t lo = uint32_t(vr), hi = uint32_t(vr >> 32);
+        const bool live = k < nrem;
+        ll[u] = live ? lbase[lo & 63u] + ((lo >> 6) & 0xffffu) : 0u;
+        ml[u] = live ? mbase[(lo >> 22) & 63u] + (((lo >> 28) | (hi << 4)) & 0xffffu) : 0u;
+        of[u] = live ? hi >> 12 : 0u;
+        lt += ll[u];
+        ot += ll[u] + ml[u];
+      }
+      uint32_t lpx = wave_incl_scan32(lt, lane) - lt, opx = wave_incl_scan32(ot, lane) - ot;
+      // the lengths back in place for the execution pass: ll (18 bits) | ml (18)
+      // << 18 | offset (28) << 36 (lengths < 2^18; a block that fails a check
+      // below is never executed)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t k = 4 * lane + u;
+        if (k < nrem)
+          S[i0 + k] = uint64_t(ll[u]) | (uint64_t(ml[u]) << 18) | (uint64_t(of[u]) << 36);
+      }
+      uint32_t fcode = 0;  // the lane's first failing sequence: 1 / 3 kErr, 2 kCap
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        // (32-bit: lengths < 2^18, 256 per window, totals <= cap < 2^31)
+        const uint32_t mst = O + opx + ll[u];  // match start in the block output
+        const uint32_t code = 4 * lane + u >= nrem            ? 0u
+                              : lp + lpx + ll[u] > lit_total  ? 1u
+                              : mst + ml[u] > zcap            ? 2u
+                              : of[u] > mst                   ? 3u
+                                                              : 0u;
+        fcode = fcode ? fcode : code;
+        lpx += ll[u];
+        opx += ll[u] + ml[u];
+      }
+      const uint64_t fm = __ballot(fcode != 0);
+      if (fm) {
+        const uint32_t c = __builtin_amdgcn_readlane(fcode, __ffsll(static_cast<unsigned long long>(fm)) - 1);
+        bst = c == 2 ? zst::kCap : zst::kErr;
+        break;
+      }
+      O += __builtin_amdgcn_readlane(opx, 63);
+      lp += __builtin_amdgcn_readlane(lpx, 63);
+    }
+    if (bst == zst::kOK && !exec) bst = st0;
+    if (bst == zst::kOK && uint64_t(O) + (lit_total - lp) > zcap) bst = zst::kCap;
+    if (bst == zst::kOK && (flags & zst::kFlagFcs) && uint64_t(O) + (lit_total - lp) != zb[b].fcs)
+      bst = zst::kErr;  // Frame_Content_Size check
+    if (bst != zst::kOK) {
+      if (lane == 0) {
+        zstatus[b] = bst == zst::kCap ? OKV_BLK_CAPACITY : OKV_BLK_ZSTD_ERROR;
+        dec_len[b] = 0;
+      }
+      continue;
+    }
+    O = 0;
+    lp = 0;
     for (uint32_t i0 = 0; i0 < nseq;) {
       long long tp0 = prof ? clock64() : 0;
       const uint32_t nrem = nseq - i0;

@@ -1,0 +1,61 @@
+"""The product library ships only the kernels the product paths launch and reads
+no environment (the measured alternatives and their OKV_* knobs live in the
+ablation build, -DOKV_ABLATE).  Checked on the built files, no GPU needed:
+kernel symbol names of the embedded gfx950 code object and the string
+literals of the host code are plain bytes in the shared object."""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PRODUCT = os.path.join(ROOT, "objectkv_amd", "libokv_sst.so")
+ABLATE = os.path.join(ROOT, "objectkv_amd", "libokv_sst_ablate.so")
+
+# kernels of the measured alternative forms: ablation build only
+ABLATION_ONLY = [b"okv_value_sweep_kernel", b"okv_rows_kernel", b"okv_gather_staged_kernel",
+                 b"okv_gather_kernel", b"okv_tile_kernel_w7", b"okv_scan_kernel"]
+KNOBS = [b"OKV_GATHER_THREADS", b"OKV_GATHER_GRID", b"OKV_DECODE_FUSED", b"OKV_GATHER_STAGED",
+         b"OKV_VALUE_SWEEP", b"OKV_TILE", b"OKV_ZSTD_GENERAL", b"OKV_ZSTD_PROF",
+         b"OKV_ENC_VARIANT", b"OKV_ENC_IMAGE"]
+
+
+def _bytes(path):
+    if not os.path.exists(path):
+        pytest.skip(f"{os.path.basename(path)} not built")
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def test_product_ships_one_tile_pass_form():
+    data = _bytes(PRODUCT)
+    forms = set(re.findall(rb"_ZN3okv15okv_tile_kernelI[A-Za-z0-9_]+", data))
+    assert forms == {b"_ZN3okv15okv_tile_kernelILj16384ELj256ELb1ELi0EEEvNS_10CopyParamsEjj"}, forms
+    for name in ABLATION_ONLY:
+        assert name not in data, name
+    # the shipping kernels are all there
+    for name in (b"okv_count_kernel", b"okv_gather_small_kernel", b"okv_decode_fused_kernel",
+                 b"okv_copy_kernel", b"okv_index_kernel", b"okv_hash_kernel",
+                 b"okv_enc_pack_lds_kernel", b"okv_zstd_seq_kernel", b"okv_zstd_exec_kernel",
+                 b"okv_merge_rank"):
+        assert name in data, name
+
+
+def test_product_reads_no_environment():
+    data = _bytes(PRODUCT)
+    for knob in KNOBS:
+        assert knob not in data, knob
+    dyn = subprocess.run(["nm", "-D", "--undefined-only", PRODUCT], capture_output=True,
+                         text=True, check=True).stdout
+    assert not re.search(r"\bgetenv\b", dyn), "the product library imports getenv"
+
+
+def test_ablation_build_carries_the_alternatives():
+    data = _bytes(ABLATE)
+    for name in (b"okv_value_sweep_kernel", b"okv_gather_staged_kernel", b"okv_tile_kernel_w7"):
+        assert name in data, name
+    for knob in (b"OKV_VALUE_SWEEP", b"OKV_TILE", b"OKV_ZSTD_PROF"):
+        assert knob in data, knob

@@ -1854,11 +1854,7 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
   __shared__ uint4 rec[zst::kSeqChunk + 1];
   __shared__ uint32_t srcx[kExecOut];
   __shared__ uint8_t map[kExecOut];
-  __shared__ uint32_t lbase[64], mbase[64];  // literal / match length baselines by code
   const int lane = threadIdx.x & 63;
-  lbase[lane] = zst::ll_base(uint32_t(lane) < 36 ? uint32_t(lane) : 0u);
-  mbase[lane] = zst::ml_base(uint32_t(lane) < 53 ? uint32_t(lane) : 0u);
-  __syncthreads();
   unsigned long long pacc[10] = {};
   for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
     const int32_t kind = zst::rfl(uint32_t(zb[b].kind));
@@ -1901,8 +1897,10 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
         const uint64_t vr = cur[u];
         const uint32_t lo = uint32_t(vr), hi = uint32_t(vr >> 32);
         const bool live = k < nrem;
-        ll[u] = live ? lbase[lo & 63u] + ((lo >> 6) & 0xffffu) : 0u;
-        ml[u] = live ? mbase[(lo >> 22) & 63u] + (((lo >> 28) | (hi << 4)) & 0xffffu) : 0u;
+        // (baselines computed, not looked up: an LDS table would cost this
+        // kernel a workgroup per CU, 11 -> 10)
+        ll[u] = live ? zst::ll_base(lo & 63u) + ((lo >> 6) & 0xffffu) : 0u;
+        ml[u] = live ? zst::ml_base((lo >> 22) & 63u) + (((lo >> 28) | (hi << 4)) & 0xffffu) : 0u;
         of[u] = live ? hi >> 12 : 0u;
         lt += ll[u];
         ot += ll[u] + ml[u];

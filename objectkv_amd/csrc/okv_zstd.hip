@@ -1825,6 +1825,12 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
   } while (0)
 namespace zst {
 constexpr uint32_t kTerm = 0x80000000u, kLit = 0x40000000u, kIdx = 0x3fffffffu;
+// a global (not flat) byte load: the literal pointer comes from a ZBlk field, so
+// the compiler cannot tell its address space; flat loads would count in lgkmcnt
+// too and make every LDS wait of the gather drain them
+__device__ __forceinline__ uint32_t gload_u8(const uint8_t* p) {
+  return *(const __attribute__((address_space(1))) uint8_t*)p;
+}
 }
 
 // Executor chunk: output bytes covered by one byte map (kEU 16-byte map
@@ -2029,19 +2035,21 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
         __syncthreads();
         PMARK(1);
         // each byte's source, resolved to a terminal (a literal or output before
-        // the chunk) in byte order, 64 bytes (one per lane) at a time: a source
-        // before the group is already terminal, one read; a source inside the
-        // group (match offset < 64) is resolved by pointer jumping within the
-        // group.  Eight groups' immediate sources are computed first (their map
-        // and record reads all in flight); LDS operations of one wave complete
-        // in order, so each group sees the previous groups' writes.
+        // the chunk) a batch of kGB 64-byte groups at a time: the batch's
+        // immediate sources are computed and stored (map and record reads all in
+        // flight), then followed by pointer jumping over the whole batch.  A
+        // source before the batch is already terminal (one read); chains inside
+        // the batch halve each round.  Every entry always holds a source of its
+        // byte (its own, or one further along its chain), and LDS operations of
+        // one wave complete in order, so the rounds' reads and writes need no
+        // other ordering.
         uint32_t rounds = 0;
         for (uint32_t x0 = 0; x0 < osum; x0 += 64 * kGB) {
           uint32_t kk[kGB];
 #pragma unroll
           for (int u = 0; u < kGB; ++u) {
             const uint32_t x = x0 + 64 * u + lane;
-            kk[u] = x < osum ? map[x] : 0;
+            kk[u] = map[x];  // (x < x0 + 64 kGB <= kExecOut; past osum: ignored below)
           }
           uint4 R[kGB];
 #pragma unroll
@@ -2049,30 +2057,40 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
           uint32_t sv[kGB];
 #pragma unroll
           for (int u = 0; u < kGB; ++u) {
+            // branch-free: a literal byte, or a match byte whose source is
+            // before the chunk (terminal) or inside it; the modulo only for
+            // bytes past the first period of an overlapping match
             const uint32_t x = x0 + 64 * u + lane;
-            const uint32_t in = x - R[u].x;
-            if (in < R[u].y) {
-              sv[u] = zst::kTerm | zst::kLit | (lp + R[u].w + in);
-            } else {
-              const uint32_t t = in - R[u].y, off = R[u].z;
-              const uint32_t mo = t < off ? t : t % off;
-              const int32_t sx = int32_t(R[u].x + R[u].y + mo) - int32_t(off);
-              sv[u] = sx < 0 ? (zst::kTerm | uint32_t(int32_t(O) + sx)) : uint32_t(sx);
-            }
-            if (x >= osum) sv[u] = zst::kTerm;
+            const uint32_t in = x - R[u].x, t = in - R[u].y, off = R[u].z;
+            const bool lit = in < R[u].y;
+            uint32_t mo = t;
+            if (!lit && t >= off) mo = t % off;
+            const int32_t sx = int32_t(R[u].x + R[u].y + mo) - int32_t(off);
+            const uint32_t vm = sx < 0 ? (zst::kTerm | uint32_t(int32_t(O) + sx)) : uint32_t(sx);
+            const uint32_t vl = zst::kTerm | zst::kLit | (lp + R[u].w + in);
+            sv[u] = x >= osum ? zst::kTerm : lit ? vl : vm;
           }
+          bool pend = false;
 #pragma unroll
           for (int u = 0; u < kGB; ++u) {
-            const uint32_t g0 = x0 + 64 * u;
-            if (g0 >= osum) break;
-            const uint32_t x = g0 + lane;
-            if (!(sv[u] & zst::kTerm) && sv[u] < g0) sv[u] = srcx[sv[u]];
+            const uint32_t x = x0 + 64 * u + lane;
             if (x < osum) srcx[x] = sv[u];
-            while (__any(!(sv[u] & zst::kTerm))) {
-              if (!(sv[u] & zst::kTerm)) sv[u] = srcx[sv[u]];
-              if (x < osum) srcx[x] = sv[u];
-              ++rounds;
+            pend |= !(sv[u] & zst::kTerm);
+          }
+          while (__any(pend)) {
+            bool nt[kGB];
+#pragma unroll
+            for (int u = 0; u < kGB; ++u) {
+              nt[u] = !(sv[u] & zst::kTerm);
+              if (nt[u]) sv[u] = srcx[sv[u]];
             }
+            pend = false;
+#pragma unroll
+            for (int u = 0; u < kGB; ++u) {
+              if (nt[u]) srcx[x0 + 64 * u + lane] = sv[u];  // (x >= osum is terminal)
+              pend |= !(sv[u] & zst::kTerm);
+            }
+            ++rounds;
           }
         }
         __syncthreads();
@@ -2083,25 +2101,34 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
         // byte loads in flight, one dword store each).  A head byte before O is
         // re-read from the previous chunk's output; tail bytes past the chunk
         // are written as 0 and overwritten by the next chunk the same way.
+        // Branch-free: every source entry is read first (the index clamped into
+        // the map: a head byte's wraps, a tail byte's is stale, both ignored),
+        // then every byte is loaded from a valid address (an RLE literal or a
+        // zero byte reads the block's first output byte) and selected.
         const uint32_t g0 = O >> 2, g1 = (O + osum + 3) >> 2;
+        const uint64_t out_a = reinterpret_cast<uint64_t>(out);
+        const uint64_t lit_a = reinterpret_cast<uint64_t>(lits);
         for (uint32_t gb = g0 + lane; gb < g1; gb += 64 * kGQ) {
-          const uint8_t* ptr[4 * kGQ];
-          uint32_t spec[4 * kGQ];  // 0 load, 1 RLE literal, 2 zero
+          uint32_t sv[4 * kGQ];
+#pragma unroll
+          for (int u = 0; u < 4 * kGQ; ++u) {
+            const uint32_t a = 4 * (gb + 64 * (u >> 2)) + (u & 3);
+            sv[u] = srcx[min(a - O, kExecOut - 1)];
+          }
+          uint32_t bv[4 * kGQ], sel[4 * kGQ];  // sel: 0 zero, 1 RLE literal, 2 loaded
 #pragma unroll
           for (int u = 0; u < 4 * kGQ; ++u) {
             const uint32_t g = gb + 64 * (u >> 2);
             const uint32_t a = 4 * g + (u & 3);
-            const uint32_t x = a - O;
-            const bool in = g < g1 && a >= O && x < osum;
-            const uint32_t sv = in ? srcx[x] : 0u;
-            const uint32_t idx = sv & zst::kIdx;
-            const bool lit = in && (sv & zst::kLit);
-            spec[u] = (g >= g1 || (a >= O && !in)) ? 2u : ((lit && rle) ? 1u : 0u);
-            ptr[u] = spec[u] ? out : (!in ? out + a : (lit ? lits + idx : out + idx));
+            const bool in = g < g1 && a - O < osum;  // (a < O wraps)
+            const bool head = g < g1 && a < O;
+            const bool lit = in && (sv[u] & zst::kLit);
+            const bool rl = lit && rle;
+            const uint64_t base = lit && !rle ? lit_a : out_a;
+            const uint32_t idx = in && !rl ? (sv[u] & zst::kIdx) : head ? a : 0u;
+            bv[u] = zst::gload_u8(reinterpret_cast<const uint8_t*>(base + idx));
+            sel[u] = in || head ? (rl ? 1u : 2u) : 0u;
           }
-          uint32_t bv[4 * kGQ];
-#pragma unroll
-          for (int u = 0; u < 4 * kGQ; ++u) bv[u] = *ptr[u];
 #pragma unroll
           for (int q = 0; q < kGQ; ++q) {
             const uint32_t g = gb + 64 * q;
@@ -2109,7 +2136,7 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const int u = 4 * q + j;
-              const uint32_t v = spec[u] == 2 ? 0u : spec[u] == 1 ? rle_byte : (bv[u] & 0xffu);
+              const uint32_t v = sel[u] == 2 ? (bv[u] & 0xffu) : sel[u] == 1 ? rle_byte : 0u;
               w |= v << (8 * j);
             }
             if (g < g1) reinterpret_cast<uint32_t*>(out)[g] = w;
@@ -2144,7 +2171,7 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
           }
           uint32_t bv[4 * kGQ];
 #pragma unroll
-          for (int u = 0; u < 4 * kGQ; ++u) bv[u] = *ptr[u];
+          for (int u = 0; u < 4 * kGQ; ++u) bv[u] = zst::gload_u8(ptr[u]);
 #pragma unroll
           for (int q = 0; q < kGQ; ++q) {
             const uint32_t g = gb + 64 * q;
@@ -2183,7 +2210,7 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
           const bool in = g < g1 && a >= O && a - O < tl;
           spec[u] = (g >= g1 || (a >= O && !in)) ? 2u : ((in && rle) ? 1u : 0u);
           const uint8_t* ptr = spec[u] ? out : (!in ? out + a : lits + lp + (a - O));
-          bv[u] = *ptr;
+          bv[u] = zst::gload_u8(ptr);
         }
 #pragma unroll
         for (int q = 0; q < kGQ; ++q) {

@@ -1,5 +1,5 @@
 """zstd decode diagnostics on the CZ workload: phase cycle counters
-(OKV_ZSTD_PROF) and an A/B of LDS staging (OKV_ZSTD_STAGE)."""
+(OKV_ZSTD_PROF).  ZP_LIB=<path to a libokv_sst build> times that build instead."""
 import os as _os
 _os.environ.setdefault("OKV_ABLATE", "1")  # the ablation build (its OKV_* knobs)
 
@@ -7,6 +7,9 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("ZP_LIB"):  # A/B of library builds: one process per build
+    from objectkv_amd import _lib  # noqa: E402
+    _lib.LIB_PATH = os.path.abspath(os.environ["ZP_LIB"])
 import objectkv_amd as okv  # noqa: E402
 from tools.zstd_gen import text_zstd_segment  # noqa: E402
 

@@ -1848,11 +1848,17 @@ constexpr int kEU = int(kExecOut / 1024);
 #endif
 constexpr int kGQ = OKV_ZSTD_GQ;  // gather: output dwords per lane per step
 constexpr int kGB = OKV_ZSTD_GB;  // source resolution: 64-byte groups per batch
-static_assert(kExecOut <= zst::kChunkOut && kExecOut % 1024 == 0, "exec chunk");
+static_assert(kExecOut <= zst::kChunkOut && kExecOut % 1024 == 0 && (kExecOut & (kExecOut - 1)) == 0,
+              "exec chunk");
 // Executor grid (blocks are strided over it); the profiling slots are sized
 // for the largest grid.
 constexpr uint32_t kExecGridMax = 16384;
-__global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
+#ifdef OKV_ZSTD_EXEC_WPE  // (build-time occupancy probe: waves per SIMD the registers must allow)
+#define OKV_ZSTD_EXEC_ATTR __attribute__((amdgpu_waves_per_eu(OKV_ZSTD_EXEC_WPE)))
+#else
+#define OKV_ZSTD_EXEC_ATTR
+#endif
+__global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
     const zst::ZBlk* __restrict__ zb, uint32_t nblk, const uint64_t* __restrict__ seq_off,
     uint64_t* __restrict__ seqs, const uint64_t* __restrict__ cap_off,
     uint8_t* __restrict__ dec, uint64_t* __restrict__ dec_len, int32_t* __restrict__ zstatus,
@@ -2058,43 +2064,45 @@ __global__ __launch_bounds__(64) void okv_zstd_exec_kernel(
 #pragma unroll
           for (int u = 0; u < kGB; ++u) {
             // branch-free: a literal byte, or a match byte whose source is
-            // before the chunk (terminal) or inside it; the modulo only for
-            // bytes past the first period of an overlapping match
+            // before the chunk (terminal) or inside it.  A byte past the first
+            // period of an overlapping match (offset < match length) points at
+            // the byte one period earlier, which the pointer jumping resolves (a
+            // modulo here cost more than the extra rounds: 8.3K -> 5.3K cycles
+            // per chunk, profiles/r3/r3t)
             const uint32_t x = x0 + 64 * u + lane;
-            const uint32_t in = x - R[u].x, t = in - R[u].y, off = R[u].z;
+            const uint32_t in = x - R[u].x;
             const bool lit = in < R[u].y;
-            uint32_t mo = t;
-            if (!lit && t >= off) mo = t % off;
-            const int32_t sx = int32_t(R[u].x + R[u].y + mo) - int32_t(off);
+            const int32_t sx = int32_t(x) - int32_t(R[u].z);
             const uint32_t vm = sx < 0 ? (zst::kTerm | uint32_t(int32_t(O) + sx)) : uint32_t(sx);
             const uint32_t vl = zst::kTerm | zst::kLit | (lp + R[u].w + in);
             sv[u] = x >= osum ? zst::kTerm : lit ? vl : vm;
           }
+          PMARK(2);
+          // (reads and writes unconditional and branch-free: x < x0 + 64 kGB <=
+          // kExecOut, and a terminal entry's index bits read some entry of the
+          // map, whose value is dropped; entries past osum are never used)
           bool pend = false;
 #pragma unroll
           for (int u = 0; u < kGB; ++u) {
-            const uint32_t x = x0 + 64 * u + lane;
-            if (x < osum) srcx[x] = sv[u];
+            srcx[x0 + 64 * u + lane] = sv[u];
             pend |= !(sv[u] & zst::kTerm);
           }
           while (__any(pend)) {
-            bool nt[kGB];
+            uint32_t r[kGB];
 #pragma unroll
-            for (int u = 0; u < kGB; ++u) {
-              nt[u] = !(sv[u] & zst::kTerm);
-              if (nt[u]) sv[u] = srcx[sv[u]];
-            }
+            for (int u = 0; u < kGB; ++u) r[u] = srcx[sv[u] & (kExecOut - 1)];
             pend = false;
 #pragma unroll
             for (int u = 0; u < kGB; ++u) {
-              if (nt[u]) srcx[x0 + 64 * u + lane] = sv[u];  // (x >= osum is terminal)
+              sv[u] = (sv[u] & zst::kTerm) ? sv[u] : r[u];
+              srcx[x0 + 64 * u + lane] = sv[u];
               pend |= !(sv[u] & zst::kTerm);
             }
             ++rounds;
           }
+          PMARK(3);
         }
         __syncthreads();
-        PMARK(2);
         PMARK(3);
         pacc[8] += rounds;
         // gather: lanes own aligned output dwords (four per lane per step, 16
@@ -2384,7 +2392,7 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
       for (int k = 0; k < 16; ++k) h[k] += hs[w * 16 + k];
     const double c = h[9] ? double(h[9]) : 1.0;
     fprintf(stderr,
-            "[zstd exec] chunks %llu, cycles/chunk: load+scan %.0f map %.0f init %.0f jump %.0f "
+            "[zstd exec] chunks %llu, cycles/chunk: load+scan %.0f map %.0f sources %.0f jump %.0f "
             "(rounds %.2f) gather %.0f commit %.0f\n",
             h[9], h[0] / c, h[1] / c, h[2] / c, h[3] / c, h[8] / c, h[4] / c, h[5] / c);
     unsigned long long pp[16] = {};

@@ -1841,12 +1841,13 @@ __device__ __forceinline__ uint32_t gload_u8(const uint8_t* p) {
 constexpr uint32_t kExecOut = OKV_ZSTD_EXEC_OUT;
 constexpr int kEU = int(kExecOut / 1024);
 #ifndef OKV_ZSTD_GQ
-#define OKV_ZSTD_GQ 4
+#define OKV_ZSTD_GQ 2
 #endif
 #ifndef OKV_ZSTD_GB
 #define OKV_ZSTD_GB 8
 #endif
-constexpr int kGQ = OKV_ZSTD_GQ;  // gather: output dwords per lane per step
+constexpr int kGQ = OKV_ZSTD_GQ;  // gather: output dwords per lane per step (2: 128 registers,
+                                  // 4: 163 -- and slower, profiles/r3/r3v)
 constexpr int kGB = OKV_ZSTD_GB;  // source resolution: 64-byte groups per batch
 static_assert(kExecOut <= zst::kChunkOut && kExecOut % 1024 == 0 && (kExecOut & (kExecOut - 1)) == 0,
               "exec chunk");
@@ -2105,7 +2106,7 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
         __syncthreads();
         PMARK(3);
         pacc[8] += rounds;
-        // gather: lanes own aligned output dwords (four per lane per step, 16
+        // gather: lanes own aligned output dwords (kGQ per lane per step, 4 kGQ
         // byte loads in flight, one dword store each).  A head byte before O is
         // re-read from the previous chunk's output; tail bytes past the chunk
         // are written as 0 and overwritten by the next chunk the same way.

@@ -1834,9 +1834,11 @@ __device__ __forceinline__ uint32_t gload_u8(const uint8_t* p) {
 }
 
 // Executor chunk: output bytes covered by one byte map (kEU 16-byte map
-// pieces per lane).  2 KiB keeps the workgroup at 14 KiB of LDS.
+// pieces per lane).  1 KiB keeps the workgroup at 9 KiB of LDS: with the
+// gather's 128 registers, 16 workgroups per CU (2 KiB: 14 KiB, 11 per CU;
+// executor 2.95 -> 2.70 ms, profiles/r3/r3w).
 #ifndef OKV_ZSTD_EXEC_OUT
-#define OKV_ZSTD_EXEC_OUT 2048
+#define OKV_ZSTD_EXEC_OUT 1024
 #endif
 constexpr uint32_t kExecOut = OKV_ZSTD_EXEC_OUT;
 constexpr int kEU = int(kExecOut / 1024);

@@ -1848,6 +1848,14 @@ constexpr int kEU = int(kExecOut / 1024);
 #ifndef OKV_ZSTD_GB
 #define OKV_ZSTD_GB 8
 #endif
+#ifndef OKV_ZSTD_SU
+#define OKV_ZSTD_SU 2
+#endif
+// sequences loaded per chunk: kSU per lane (each chunk loads, scans and records its whole
+// window, and a 1 KiB chunk executes far fewer than 256 of them)
+constexpr int kSU = OKV_ZSTD_SU;
+constexpr uint32_t kSW = 64u * kSU;
+static_assert(kSW <= zst::kSeqChunk, "sequence window (byte map entries are 8-bit)");
 constexpr int kGQ = OKV_ZSTD_GQ;  // gather: output dwords per lane per step (2: 128 registers,
                                   // 4: 163 -- and slower, profiles/r3/r3v)
 constexpr int kGB = OKV_ZSTD_GB;  // source resolution: 64-byte groups per batch
@@ -1866,7 +1874,7 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
     uint64_t* __restrict__ seqs, const uint64_t* __restrict__ cap_off,
     uint8_t* __restrict__ dec, uint64_t* __restrict__ dec_len, int32_t* __restrict__ zstatus,
     unsigned long long* __restrict__ prof) {
-  __shared__ uint4 rec[zst::kSeqChunk + 1];
+  __shared__ uint4 rec[kSW + 1];
   __shared__ uint32_t srcx[kExecOut];
   __shared__ uint8_t map[kExecOut];
   const int lane = threadIdx.x & 63;
@@ -1969,12 +1977,12 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
     for (uint32_t i0 = 0; i0 < nseq;) {
       long long tp0 = prof ? clock64() : 0;
       const uint32_t nrem = nseq - i0;
-      // up to 256 sequences: lane holds sequences 4 lane .. 4 lane + 3
-      uint32_t ll[4], ml[4], of[4];
+      // up to kSW sequences: lane holds sequences kSU lane .. kSU lane + kSU - 1
+      uint32_t ll[kSU], ml[kSU], of[kSU];
       uint32_t lt = 0, ot = 0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t k = 4 * lane + u;
+      for (int u = 0; u < kSU; ++u) {
+        const uint32_t k = kSU * lane + u;
         const uint64_t vr = S[i0 + (k < nrem ? k : 0)];
         const uint64_t v = k < nrem ? vr : 0;
         ll[u] = uint32_t(v) & 0x3ffff;
@@ -1986,14 +1994,14 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
       uint32_t lpx = wave_incl_scan32(lt, lane) - lt, opx = wave_incl_scan32(ot, lane) - ot;
       uint32_t fit = 0;  // sequences of this lane that end within the byte map
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t k = 4 * lane + u;
+      for (int u = 0; u < kSU; ++u) {
+        const uint32_t k = kSU * lane + u;
         rec[k] = make_uint4(opx, ll[u], of[u], lpx);
         lpx += ll[u];
         opx += ll[u] + ml[u];
         fit += (k < nrem && opx <= kExecOut) ? 1u : 0u;
       }
-      if (lane == 63) rec[256] = make_uint4(opx, 0, 0, lpx);
+      if (lane == 63) rec[kSW] = make_uint4(opx, 0, 0, lpx);
       for (int d = 32; d; d >>= 1) fit += __shfl_xor(fit, d, 64);
       const uint32_t cnt = fit ? fit : 1;  // a single long sequence when none fits
       __syncthreads();

@@ -98,7 +98,7 @@ def test_zstd_bench_shape_blocks(zdec):
 
 
 def test_zstd_long_runs_and_rle_literals(zdec):
-    """Matches far longer than the executor's 4 KiB byte map, offset-1 runs,
+    """Matches far longer than the executor's 1 KiB byte map, offset-1 runs,
     and blocks whose literals are RLE."""
     rows = []
     for i in range(120):

@@ -111,6 +111,26 @@ def test_zstd_long_runs_and_rle_literals(zdec):
     assert int(got.status.max()) == 0
 
 
+def test_zstd_dense_short_sequences(zdec):
+    """Values of 5-byte words from a vocabulary of 8, each followed by one random
+    byte: libzstd emits a short sequence (one literal, one short match) every ~6
+    bytes, more per KiB of output than the executor's 128-sequence window holds,
+    so chunks end at the window instead of at the byte map."""
+    rng = np.random.default_rng(11)
+    vocab = [bytes(rng.integers(97, 123, size=5, dtype=np.uint8)) for _ in range(8)]
+    rows = []
+    for i in range(400):
+        n = 200 + (i % 97)
+        v = b"".join(vocab[int(t)] + bytes([int(r)])
+                     for t, r in zip(rng.integers(0, 8, n), rng.integers(0, 256, n)))
+        rows.append((b"d%06d" % i, v))
+    seg, _, _ = ZC.Z.zstd_segment(rows, 57344, 65536, level=3)
+    from oracle import pyoracle as P2
+    md = P2.bytes_to_metadata(ZC._meta_of(seg))
+    got = _check(zdec, seg, [st.desc() for st in md.entries])
+    assert int(got.status.max()) == 0
+
+
 def test_zstd_staged_equals_general_under_corruption(decoder, one_pass_decoder):
     """Byte flips in the sequence sections of 48 blocks.  Two-sided against the
     oracle (libzstd as the decoder checker): every block's status must equal

@@ -86,7 +86,9 @@ void okv_meta_free(okv_meta *m);
 
 /* ---- SegmentReader / RowIter over the GPU decode -------------------------- */
 /* A row as Go's KVPair (segment_reader.go:285-288): NULL pointer = nil slice.
- * Pointers stay valid until okv_reader_free. */
+ * Rows returned by okv_reader_read_block / _get_row / _get_range stay valid
+ * until the next such call on the reader (or okv_reader_free); the rows an
+ * iterator returns stay valid while it serves the same block. */
 typedef struct okv_row {
   const uint8_t *key;
   uint64_t key_len;
@@ -98,9 +100,12 @@ typedef struct okv_reader okv_reader;
 typedef struct okv_iter okv_iter;
 
 /* NewSegmentReader (segment_reader.go:65-72) over `len` bytes (what the
- * io.ReadSeeker holds; copied) with the file length `file_bytes`.  Block
- * reads decode the whole index in one batched GPU call on `ctx` the first
- * time any block is needed; rows are then served from that decode. */
+ * io.ReadSeeker holds; copied) with the file length `file_bytes`.  Block reads
+ * are GPU calls on `ctx` bounded as the cgo shim's ReadBlocks:
+ * GetRow / ReadBlockWithStat decode one block, GetRange the blocks its btree
+ * walks select, RowIter the block and the next 255 in its direction (the
+ * iteration window, which later reads are served from); each call stages
+ * only its blocks' span of the bytes. */
 okv_reader *okv_reader_open(okv_ctx *ctx, const uint8_t *data, uint64_t len, int64_t file_bytes);
 int okv_reader_fetch_metadata(okv_reader *r);                                  /* :91-141 */
 int okv_reader_load_metadata(okv_reader *r, const uint8_t *meta, uint64_t len); /* :147 + :75 */
@@ -115,6 +120,12 @@ int okv_reader_get_range(okv_reader *r, const uint8_t *start, size_t slen, const
                          size_t elen, const okv_row **rows, uint64_t *n);
 int okv_reader_close(okv_reader *r); /* :481-487 (OKV_R_ALREADY_CLOSED the second time) */
 void okv_reader_free(okv_reader *r);
+/* I/O of the reader's block reads so far: GPU decode calls, blocks decoded,
+ * bytes staged (the storage bytes the calls read). */
+typedef struct okv_reader_io {
+  uint64_t calls, blocks, bytes_staged;
+} okv_reader_io;
+int okv_reader_io_stats(const okv_reader *r, okv_reader_io *io);
 
 /* RowIter (segment_row_iter.go:11-212); direction 0 ascending, 1 descending. */
 okv_iter *okv_reader_row_iter(okv_reader *r, int direction);

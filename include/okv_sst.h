@@ -61,8 +61,8 @@ extern "C" {
 #define OKV_BLK_SHORT 2       /* short read, ErrUnexpectedBytesRead (:314-316) -> Go error */
 #define OKV_BLK_PANIC 3       /* record overruns the block buffer: mustReadBytes panics (:338-352, :506-512) */
 #define OKV_BLK_UNSUPPORTED 4 /* zstd block under OKV_F_INDEX_ONLY (no spans into seg exist) */
-#define OKV_BLK_CAPACITY 5    /* output capacity exceeded, or a zstd block decompressing past
-                                 its OriginalSize (library-specific; never a Go-written block) */
+#define OKV_BLK_CAPACITY 5    /* the caller's output capacity (row_cap / key_cap / val_cap) is
+                                 exceeded (library-specific; never with okv_decode_plan sizes) */
 #define OKV_BLK_ZSTD_ERROR 6  /* zstd.NewReader / io.Copy error (:321-330) -> Go error */
 
 /* ---- compression byte of the meta block (segment_reader.go:166-172) ----- */
@@ -381,6 +381,8 @@ int okv_profile_read(okv_ctx *ctx, double *ms, uint64_t *calls);
 #define OKV_PATH_BIG 64u    /* okv_copy_kernel / okv_index_kernel for big blocks (always
                                launched after a non-fused pass; exits when none) */
 #define OKV_PATH_ZSTD 128u  /* the zstd stage ran first */
+#define OKV_PATH_ZSTD_REGROW 256u /* zstd frames outgrew their first output region and were
+                                     measured and decoded again (io.Copy inflates them all) */
 uint32_t okv_last_path(const okv_ctx *ctx);
 
 /* Device / pinned-host memory helpers for callers without another allocator. */

@@ -24,6 +24,7 @@ OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS = 1, 2
 # okv_last_path bits (include/okv_sst.h OKV_PATH_*)
 PATH_FUSED, PATH_SMALL, PATH_TILE, PATH_SWEEP = 1, 2, 4, 8
 PATH_STAGED, PATH_GATHER, PATH_BIG, PATH_ZSTD = 16, 32, 64, 128
+PATH_ZSTD_REGROW = 256
 # SegmentWriter sentinels (okv_sst.h OKV_W_*)
 W_KEY_TOO_LARGE, W_VALUE_TOO_LARGE, W_CLOSED, W_INVALID_KEY = -101, -102, -103, -104
 W_NIL_WRITER, W_UNSUPPORTED, W_NO_ROWS = -105, -106, -107
@@ -50,7 +51,7 @@ SYMBOLS = [
     "okv_reader_open", "okv_reader_fetch_metadata", "okv_reader_load_metadata",
     "okv_reader_num_blocks", "okv_reader_read_block", "okv_reader_get_row",
     "okv_reader_get_range", "okv_reader_close", "okv_reader_free", "okv_reader_row_iter",
-    "okv_iter_next", "okv_iter_seek", "okv_iter_free",
+    "okv_iter_next", "okv_iter_seek", "okv_iter_free", "okv_reader_io_stats",
 ]
 
 
@@ -61,6 +62,10 @@ class OpenOpts(C.Structure):
 class Row(C.Structure):
     _fields_ = [("key", C.c_void_p), ("key_len", C.c_uint64), ("val", C.c_void_p),
                 ("val_len", C.c_uint64)]
+
+
+class ReaderIO(C.Structure):
+    _fields_ = [("calls", C.c_uint64), ("blocks", C.c_uint64), ("bytes_staged", C.c_uint64)]
 
 
 class BlockDesc(C.Structure):
@@ -215,6 +220,7 @@ def lib():
         "okv_iter_next": (i32, [p, C.POINTER(Row)]),
         "okv_iter_seek": (i32, [p, p, C.c_size_t]),
         "okv_iter_free": (None, [p]),
+        "okv_reader_io_stats": (i32, [p, C.POINTER(ReaderIO)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -23,8 +23,10 @@ void launch_hash(hipStream_t stream, const uint8_t* seg, uint64_t seg_bytes, con
                  uint32_t nblk, uint64_t* out);
 // okv_zstd.hip: zstd block decompression into per-block scratch regions.
 void launch_zstd_cap(hipStream_t s, const Desc* descs, uint32_t nblk, uint64_t* cap_off);
+// total: in, the first regions' total (cap_off[nblk]); out, the scratch bytes
+// in use after the frames that outgrew their regions were decoded again
 int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
-             uint32_t nblk, uint64_t total);
+             uint32_t nblk, uint64_t* total);
 void launch_zstd_desc(hipStream_t s, const Desc* descs, uint32_t nblk, const uint64_t* cap_off,
                       const uint64_t* dec_len, Desc* out);
 constexpr uint32_t kZstdLitBytes = 1u << 17;  // per-wave literal scratch (Block_Maximum_Size)
@@ -118,6 +120,11 @@ struct okv_ctx {
   size_t z_cap_seq_off = 0;
   uint64_t* z_seqs = nullptr;     // packed sequences
   size_t z_cap_seqs = 0;
+  uint32_t* z_list = nullptr;     // [nblk] blocks decoded again (+ the count after them)
+  size_t z_cap_list = 0;
+  uint64_t* z_need = nullptr;     // [n] measured outputs, [n + 1] their regions
+  size_t z_cap_need = 0;
+  uint32_t z_retried = 0;         // blocks the last zstd decode decoded again
 };
 
 namespace okv {

@@ -97,15 +97,13 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     const int32_t pre = pre_status ? pre_status[b] : int32_t(OKV_BLK_OK);
     if (pre != OKV_BLK_OK) {
       st = pre;  // outcome of the zstd stage (raw-block bounds, decoder error)
-    } else if (int64_t(d.offset) < 0 || d.offset >= seg_bytes) {
-      st = OKV_BLK_EOF;  // Seek error / bytes.Reader io.EOF (:303-313)
-    } else if (seg_bytes - d.offset < d.block_size) {
-      st = OKV_BLK_SHORT;  // ErrUnexpectedBytesRead (:314-316)
+    } else if ((st = go_read_status(d, seg_bytes)) != OKV_BLK_OK) {
+      // Seek error / makeslice panic / io.EOF / ErrUnexpectedBytesRead (:303-316)
     } else if (comp == OKV_COMP_ZSTD) {
       st = OKV_BLK_UNSUPPORTED;  // index-only spans cannot point into decompressed bytes
     } else {
       len = (comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
-      orig = d.original_size;
+      orig = go_walk_bound(d.original_size);  // int(OriginalSize) < 0: no iteration (:340)
       off = d.offset;
       walking = true;
       if (prefetch && orig && len) {
@@ -1582,8 +1580,7 @@ __global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, Fuse
   {
     const int32_t pre = F.pre ? F.pre[b] : int32_t(OKV_BLK_OK);
     if (pre != OKV_BLK_OK) st = pre;  // outcome of the zstd stage
-    else if (int64_t(d.offset) < 0 || d.offset >= P.seg_bytes) st = OKV_BLK_EOF;  // :303-313
-    else if (P.seg_bytes - d.offset < d.block_size) st = OKV_BLK_SHORT;          // :314-316
+    else if ((st = go_read_status(d, P.seg_bytes)) != OKV_BLK_OK) {}  // :303-316
     else if (P.comp == OKV_COMP_ZSTD) st = OKV_BLK_UNSUPPORTED;
   }
   const uint32_t need = 16 + shift + uint32_t(len < kSmallStage ? len : kSmallStage) + 32;
@@ -1602,7 +1599,7 @@ __global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, Fuse
   const StageWin lsrc{stage, 16 + shift};
   uint64_t rows = 0, kb = 0, vb = 0, p = 0;
   if (lane == 0 && st == OKV_BLK_OK) {
-    const uint64_t orig = d.original_size;
+    const uint64_t orig = go_walk_bound(d.original_size);
     while (p < orig) {  // :340
       if (len - p < 6) { st = OKV_BLK_PANIC; break; }  // :342-345
       uint32_t kl, vl;
@@ -2164,6 +2161,7 @@ struct Work {
 int prepare(okv_ctx* ctx, const uint8_t* d_seg, uint64_t seg_bytes, const Desc* d_desc,
             uint32_t nblk, int comp, bool index_only, Work* w) {
   *w = Work{d_seg, seg_bytes, d_desc, comp, nullptr};
+  ctx->z_retried = 0;
   if (comp != OKV_COMP_ZSTD || index_only || nblk == 0) return OKV_OK;
   int rc;
   if (nblk + 1 > ctx->z_cap_blocks || !ctx->z_cap_off) {
@@ -2185,7 +2183,7 @@ int prepare(okv_ctx* ctx, const uint8_t* d_seg, uint64_t seg_bytes, const Desc* 
   OKV_HIP(hipStreamSynchronize(ctx->stream));
   if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_dec), &ctx->z_cap_dec, total + 64)))
     return rc;
-  if ((rc = zstd_run(ctx, d_seg, seg_bytes, d_desc, nblk, total))) return rc;
+  if ((rc = zstd_run(ctx, d_seg, seg_bytes, d_desc, nblk, &total))) return rc;
   launch_zstd_desc(ctx->stream, d_desc, nblk, ctx->z_cap_off, ctx->z_dec_len, ctx->z_desc);
   OKV_HIP(hipGetLastError());
   // offsets <= total < seg_bytes, so no decompressed block reads as EOF
@@ -2418,6 +2416,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   }
   const uint32_t gt = nblk ? gather_threads(ctx, w, nblk) : 0;
   ctx->last_path = (comp ? OKV_PATH_ZSTD : 0u) |
+                   (comp == OKV_COMP_ZSTD && !index_only && ctx->z_retried ? OKV_PATH_ZSTD_REGROW : 0u) |
                    (!nblk ? 0u
                     : fused ? OKV_PATH_FUSED
                     : OKV_PATH_BIG | (tile ? OKV_PATH_TILE
@@ -2748,6 +2747,8 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->z_zb);
   (void)hipFree(ctx->z_seq_off);
   (void)hipFree(ctx->z_seqs);
+  (void)hipFree(ctx->z_list);
+  (void)hipFree(ctx->z_need);
   okv::enc_release(ctx);
   okv::merge_release(ctx);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -5,9 +5,23 @@
 // statement, quirks included (they are cited inline); only ReadBlockWithStat's
 // record loop moved to the device.  No CPU decode fallback exists: without a
 // GPU context block reads fail with OKV_R_GPU.
+//
+// Block reads are bounded exactly as the cgo shim's (INTEGRATION.md
+// ReadBlocks): a GPU call decodes
+//   * GetRow / ReadBlockWithStat (:362-404, :295): the one block it reads;
+//   * GetRange (:410-475): the block set its btree walks select (:421-458);
+//   * RowIter.Next / Seek (segment_row_iter.go:83, :143, :165): the block and
+//     the next kIterWindow - 1 in the iteration direction, kept as the
+//     iteration window (later reads of those blocks are served from it);
+// and stages only the bytes [min Offset, max Offset + BlockSize) of the batch
+// (clamped to the storage), with the offsets rebased onto that span so Go's
+// outcomes are kept: a block at or past the end reads as io.EOF, one running
+// past it is short, a negative Offset is a Seek error, an oversized BlockSize
+// the makeslice panic (segment_reader.go:303-316).
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -50,9 +64,31 @@ struct Entry {  // BlockStat (block_stat.go:9-24) as stored in the btree
 
 }  // namespace
 
+namespace {
+
+// iterWindow: blocks per GPU call while iterating.
+constexpr size_t kIterWindow = 256;
+
+// One GPU decode of a batch of blocks (okv_decode_blocks), with the rows of
+// each batch entry built lazily.  Shared: the iteration window, an iterator's
+// current block and the last GetRow / GetRange results may all hold it.
+struct Batch {
+  std::vector<uint32_t> entries;  // file_entries index of each batch entry
+  std::vector<int32_t> status;
+  std::vector<uint64_t> row_start, key_off, val_off;
+  std::vector<uint16_t> key_len;
+  std::vector<uint32_t> val_len;
+  std::vector<uint8_t> key_arena, val_arena;
+  std::vector<std::vector<okv_row>> rows;
+  std::vector<bool> built;
+};
+typedef std::shared_ptr<Batch> BatchP;
+
+}  // namespace
+
 struct okv_reader {
   okv_ctx* ctx = nullptr;
-  std::vector<uint8_t> data;
+  std::vector<uint8_t> data;  // what the io.ReadSeeker reads (the storage)
   int64_t file_bytes = 0;
   bool closed = false;
   // metadata (SegmentMetadata, segment_reader.go:43-55)
@@ -61,17 +97,13 @@ struct okv_reader {
   GoBytes first_key, last_key;
   std::vector<Entry> file_entries;  // meta block order
   std::vector<Entry> tree;          // google/btree.BTreeG ordered by FirstKey (ReplaceOrInsert)
-  // batched GPU decode of every file entry, done on first block read
-  bool decoded = false;
-  int decode_rc = 0;
-  std::vector<uint64_t> row_start, key_off, val_off;
-  std::vector<uint16_t> key_len;
-  std::vector<uint32_t> val_len;
-  std::vector<int32_t> status;
-  std::vector<uint8_t> key_arena, val_arena;
-  std::vector<std::vector<okv_row>> block_rows;  // per file entry, built lazily
-  std::vector<bool> block_built;
+  // the iteration window: its batch and each file entry's slot in it (-1: absent)
+  BatchP window;
+  std::vector<int32_t> window_slot;
+  BatchP last_read;    // the last ReadBlockWithStat batch outside the window (GetRow)
+  BatchP range_batch;  // the last GetRange batch
   std::vector<okv_row> range_out;
+  okv_reader_io io{};  // GPU calls, blocks decoded, bytes staged
 };
 
 struct okv_iter {
@@ -80,6 +112,7 @@ struct okv_iter {
   GoBytes stat_last_key;               // statLastKey
   bool rows_nil = true;                // blockRows == nil
   std::vector<okv_row> rows;           // blockRows
+  BatchP rows_batch;                   // keeps blockRows' bytes alive
   int64_t idx = 0;                     // blockRowIdx
 };
 
@@ -136,7 +169,10 @@ int load_meta(okv_reader* r, okv_meta* m) {
   }
   okv_meta_free(m);
   r->have_meta = true;
-  r->decoded = false;
+  r->window.reset();
+  r->window_slot.assign(r->file_entries.size(), -1);
+  r->last_read.reset();
+  r->range_batch.reset();
   return OKV_OK;
 }
 
@@ -145,81 +181,145 @@ int ensure_meta(okv_reader* r) {  // "Fetches the metadata if not already loaded
   return okv_reader_fetch_metadata(r);
 }
 
-// One batched GPU decode of every entry of the meta block.
-int ensure_decoded(okv_reader* r) {
-  if (r->decoded) return r->decode_rc;
-  r->decoded = true;
-  if (!r->ctx) return r->decode_rc = OKV_R_GPU;
-  const uint32_t nb = uint32_t(r->file_entries.size());
+// ReadBlocks: one GPU decode of the given file entries,
+// staging only their span of the storage.
+int decode_batch(okv_reader* r, const std::vector<uint32_t>& entries, BatchP* out) {
+  if (!r->ctx) return OKV_R_GPU;
+  const uint64_t nbytes = r->data.size();
+  const uint32_t nb = uint32_t(entries.size());
+  // the span: blocks with a non-negative Offset inside the storage (the others
+  // fail before any read: Seek error, or io.EOF at / past the end)
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (uint32_t e : entries) {
+    const okv_block_desc& d = r->file_entries[e].d;
+    if (int64_t(d.offset) < 0 || d.offset >= nbytes) continue;
+    lo = std::min(lo, d.offset);
+    hi = std::max(hi, d.offset + std::min(d.block_size, nbytes - d.offset));
+  }
+  if (lo > hi) lo = hi = 0;
   std::vector<okv_block_desc> descs(nb);
-  for (uint32_t i = 0; i < nb; ++i) descs[i] = r->file_entries[i].d;
-  const uint8_t* seg = r->data.empty() ? nullptr : r->data.data();
+  for (uint32_t i = 0; i < nb; ++i) {
+    descs[i] = r->file_entries[entries[i]].d;
+    // rebased onto the span: offsets >= the storage end stay >= the span end
+    // (io.EOF), a BlockSize past the end stays short; negative ones keep their sign
+    if (int64_t(descs[i].offset) >= 0) descs[i].offset -= lo;
+  }
+  const uint8_t* seg = hi > lo ? r->data.data() + lo : nullptr;
+  const uint64_t n = hi - lo;
   uint64_t rows = 0, kb = 0, vb = 0;
-  int rc = okv_decode_plan(r->ctx, seg, r->data.size(), descs.data(), nb, r->compression, 0,
-                           &rows, &kb, &vb);
-  if (rc) return r->decode_rc = OKV_R_GPU;
-  r->row_start.assign(nb + 1, 0);
-  r->status.assign(nb, 0);
-  r->key_off.assign(rows + 1, 0);
-  r->val_off.assign(rows + 1, 0);
-  r->key_len.assign(rows + 1, 0);
-  r->val_len.assign(rows + 1, 0);
-  r->key_arena.assign(kb + 16, 0);
-  r->val_arena.assign(vb + 16, 0);
+  int rc = okv_decode_plan(r->ctx, seg, n, descs.data(), nb, r->compression, 0, &rows, &kb, &vb);
+  if (rc) return OKV_R_GPU;
+  BatchP B = std::make_shared<Batch>();
+  B->entries = entries;
+  B->row_start.assign(nb + 1, 0);
+  B->status.assign(nb, 0);
+  B->key_off.assign(rows + 1, 0);
+  B->val_off.assign(rows + 1, 0);
+  B->key_len.assign(rows + 1, 0);
+  B->val_len.assign(rows + 1, 0);
+  B->key_arena.assign(kb + 16, 0);
+  B->val_arena.assign(vb + 16, 0);
   std::vector<uint64_t> kbase(nb + 1), vbase(nb + 1);
   okv_decode_out o;
   std::memset(&o, 0, sizeof(o));
-  o.row_start = r->row_start.data();
+  o.row_start = B->row_start.data();
   o.key_base = kbase.data();
   o.val_base = vbase.data();
-  o.blk_status = r->status.data();
-  o.key_off = r->key_off.data();
-  o.key_len = r->key_len.data();
-  o.val_off = r->val_off.data();
-  o.val_len = r->val_len.data();
-  o.key_arena = r->key_arena.data();
-  o.val_arena = r->val_arena.data();
+  o.blk_status = B->status.data();
+  o.key_off = B->key_off.data();
+  o.key_len = B->key_len.data();
+  o.val_off = B->val_off.data();
+  o.val_len = B->val_len.data();
+  o.key_arena = B->key_arena.data();
+  o.val_arena = B->val_arena.data();
   o.row_cap = rows;
   o.key_cap = kb;
   o.val_cap = vb;
-  rc = okv_decode_blocks(r->ctx, seg, r->data.size(), descs.data(), nb, r->compression, &o, 0);
-  if (rc) return r->decode_rc = OKV_R_GPU;
-  r->block_rows.assign(nb, {});
-  r->block_built.assign(nb, false);
-  return r->decode_rc = OKV_OK;
+  rc = okv_decode_blocks(r->ctx, seg, n, descs.data(), nb, r->compression, &o, 0);
+  if (rc) return OKV_R_GPU;
+  B->rows.assign(nb, {});
+  B->built.assign(nb, false);
+  r->io.calls++;
+  r->io.blocks += nb;
+  r->io.bytes_staged += n;
+  *out = B;
+  return OKV_OK;
 }
 
-// ReadBlockWithStat(stat) (segment_reader.go:295-355) for a btree entry:
-// the Go outcome of the block (rows, error or panic) from the batch decode.
-int read_block(okv_reader* r, const Entry& e, const std::vector<okv_row>** rows) {
-  int rc = ensure_meta(r);
-  if (rc) return rc;
-  if ((rc = ensure_decoded(r))) return rc;
-  // the btree holds copies of meta entries; find the decoded one by position
-  const uint64_t i = e.file_index;
-  switch (r->status[i]) {
+// ReadBlockWithStat's outcome (segment_reader.go:295-355) for batch entry
+// `slot`: its rows, or the Go error / panic.
+int batch_rows(Batch& B, uint32_t slot, const std::vector<okv_row>** rows) {
+  switch (B.status[slot]) {
     case OKV_BLK_OK: break;
     case OKV_BLK_EOF: return OKV_R_BLOCK_EOF;
     case OKV_BLK_SHORT: return OKV_R_BLOCK_SHORT;
     case OKV_BLK_PANIC: return OKV_R_PANIC;
     case OKV_BLK_UNSUPPORTED: return OKV_R_UNSUPPORTED;
     case OKV_BLK_ZSTD_ERROR: return OKV_R_ZSTD;
-    default: return OKV_R_GPU;
+    default: return OKV_R_GPU;  // (capacity: the plan sized every output)
   }
-  if (!r->block_built[i]) {
-    std::vector<okv_row>& out = r->block_rows[i];
-    for (uint64_t g = r->row_start[i]; g < r->row_start[i + 1]; ++g) {
+  if (!B.built[slot]) {
+    std::vector<okv_row>& out = B.rows[slot];
+    for (uint64_t g = B.row_start[slot]; g < B.row_start[slot + 1]; ++g) {
       okv_row row;
-      row.key_len = r->key_len[g];
-      row.val_len = r->val_len[g];
-      row.key = row.key_len ? r->key_arena.data() + r->key_off[g] : nullptr;  // nil (Q4)
-      row.val = row.val_len ? r->val_arena.data() + r->val_off[g] : nullptr;
+      row.key_len = B.key_len[g];
+      row.val_len = B.val_len[g];
+      row.key = row.key_len ? B.key_arena.data() + B.key_off[g] : nullptr;  // nil (Q4)
+      row.val = row.val_len ? B.val_arena.data() + B.val_off[g] : nullptr;
       out.push_back(row);
     }
-    r->block_built[i] = true;
+    B.built[slot] = true;
   }
-  *rows = &r->block_rows[i];
+  *rows = &B.rows[slot];
   return OKV_OK;
+}
+
+// ReadBlockWithStat(stat) for the btree entry at tree position t: served from
+// the iteration window when it holds the block, else a one-block GPU call
+// (GetRow stages BlockSize bytes, not the segment).  *keep owns the rows.
+int read_block(okv_reader* r, size_t t, const std::vector<okv_row>** rows, BatchP* keep) {
+  int rc = ensure_meta(r);
+  if (rc) return rc;
+  const uint32_t e = uint32_t(r->tree[t].file_index);
+  if (r->window && r->window_slot[e] >= 0) {
+    *keep = r->window;
+    return batch_rows(*r->window, uint32_t(r->window_slot[e]), rows);
+  }
+  BatchP B;
+  if ((rc = decode_batch(r, {e}, &B))) return rc;
+  r->last_read = B;
+  *keep = B;
+  return batch_rows(*B, 0, rows);
+}
+
+// RowIter's block read (segment_row_iter.go:83, :143, :165): on a window miss
+// it decodes this block and the next kIterWindow - 1 btree entries in the
+// iteration direction in one batch, which becomes the window.
+int read_block_iter(okv_reader* r, size_t t, int direction, const std::vector<okv_row>** rows,
+                    BatchP* keep) {
+  int rc = ensure_meta(r);
+  if (rc) return rc;
+  const uint32_t e = uint32_t(r->tree[t].file_index);
+  if (r->window && r->window_slot[e] >= 0) {
+    *keep = r->window;
+    return batch_rows(*r->window, uint32_t(r->window_slot[e]), rows);
+  }
+  std::vector<uint32_t> batch{e};  // the block itself first
+  if (direction == 1) {
+    for (size_t i = t; i-- > 0 && batch.size() < kIterWindow;)
+      batch.push_back(uint32_t(r->tree[i].file_index));
+  } else {
+    for (size_t i = t + 1; i < r->tree.size() && batch.size() < kIterWindow; ++i)
+      batch.push_back(uint32_t(r->tree[i].file_index));
+  }
+  BatchP B;
+  if ((rc = decode_batch(r, batch, &B))) return rc;
+  if (r->window)
+    for (uint32_t x : r->window->entries) r->window_slot[x] = -1;
+  r->window = B;
+  for (uint32_t i = 0; i < uint32_t(batch.size()); ++i) r->window_slot[batch[i]] = int32_t(i);
+  *keep = B;
+  return batch_rows(*B, 0, rows);
 }
 
 }  // namespace
@@ -261,7 +361,8 @@ int okv_reader_read_block(okv_reader* r, uint64_t i, const okv_row** rows, uint6
   if (rc) return rc;
   if (i >= r->tree.size()) return OKV_E_ARG;
   const std::vector<okv_row>* v = nullptr;
-  if ((rc = read_block(r, r->tree[i], &v))) return rc;
+  BatchP keep;
+  if ((rc = read_block(r, size_t(i), &v, &keep))) return rc;
   *rows = v->empty() ? nullptr : v->data();
   *n = v->size();
   return OKV_OK;
@@ -275,7 +376,8 @@ int okv_reader_get_row(okv_reader* r, const uint8_t* key, size_t klen, okv_row* 
   const size_t up = upper(r, key, klen);  // DescendLessOrEqual first item (:381-385)
   if (up == 0) return OKV_R_NO_ROWS;
   const std::vector<okv_row>* rows = nullptr;
-  if ((rc = read_block(r, r->tree[up - 1], &rows))) return rc;
+  BatchP keep;
+  if ((rc = read_block(r, up - 1, &rows, &keep))) return rc;
   for (const okv_row& row : *rows)
     if (bcmp(row.key, row.key_len, key, klen) == 0) {  // bytes.Equal (:398)
       *out = row;
@@ -309,12 +411,26 @@ int okv_reader_get_range(okv_reader* r, const uint8_t* start, size_t slen, const
       break;
     pick[i] = true;
   }
+  // the candidate blocks in one batch (Go ranges over a map, in random order;
+  // ascending FirstKey order here, :457), served from the window when it holds
+  // every one of them
+  std::vector<uint32_t> list;
+  for (size_t i = 0; i < N; ++i)
+    if (pick[i]) list.push_back(uint32_t(r->tree[i].file_index));
+  BatchP B;
+  bool from_window = r->window != nullptr;
+  for (uint32_t e : list) from_window = from_window && r->window_slot[e] >= 0;
+  if (from_window) {
+    B = r->window;
+  } else if (!list.empty() && (rc = decode_batch(r, list, &B))) {
+    return rc;
+  }
+  r->range_batch = B;
   r->range_out.clear();
-  // Go ranges over a map (random order); ascending FirstKey order here (:457)
-  for (size_t i = 0; i < N; ++i) {
-    if (!pick[i]) continue;
+  for (uint32_t k = 0; k < uint32_t(list.size()); ++k) {
+    const uint32_t slot = from_window ? uint32_t(r->window_slot[list[k]]) : k;
     const std::vector<okv_row>* rows = nullptr;
-    if ((rc = read_block(r, r->tree[i], &rows))) return rc;
+    if ((rc = batch_rows(*B, slot, &rows))) return rc;
     for (const okv_row& row : *rows) {  // :462-471
       if (bcmp(start, slen, row.key, row.key_len) <= 0) {
         if (!unbound_end && bcmp(row.key, row.key_len, end, elen) >= 0) break;
@@ -335,6 +451,12 @@ int okv_reader_close(okv_reader* r) {  // Close :481-487
 
 void okv_reader_free(okv_reader* r) { delete r; }
 
+int okv_reader_io_stats(const okv_reader* r, okv_reader_io* io) {
+  if (!r || !io) return OKV_E_ARG;
+  *io = r->io;
+  return OKV_OK;
+}
+
 okv_iter* okv_reader_row_iter(okv_reader* r, int direction) {  // RowIter :264-283
   if (ensure_meta(r)) return nullptr;
   okv_iter* it = new okv_iter();
@@ -353,14 +475,14 @@ int okv_iter_next(okv_iter* it, okv_row* out) {  // RowIter.Next segment_row_ite
     it->idx++;
     return OKV_OK;
   }
-  const Entry* stat = nullptr;
+  size_t stat = SIZE_MAX;
   if (it->direction == 1) {  // DirectionDescending (:45-61)
     if (it->stat_last_key.nil && it->idx > -1) it->stat_last_key = s->last_key;
     const Bytes& k = it->stat_last_key.b;
     for (size_t i = upper(s, k.data(), k.size()); i-- > 0;) {
       if (bcmp(k, s->tree[i].first_key) == 0) continue;  // same key: keep going
       it->stat_last_key = GoBytes::of(s->tree[i].first_key.data(), s->tree[i].first_key.size());
-      stat = &s->tree[i];
+      stat = i;
       break;
     }
   } else {  // ascending (:62-75)
@@ -368,15 +490,17 @@ int okv_iter_next(okv_iter* it, okv_row* out) {  // RowIter.Next segment_row_ite
     for (size_t i = lower(s, k.data(), k.size()); i < s->tree.size(); ++i) {
       if (bcmp(k, s->tree[i].first_key) == 0) continue;
       it->stat_last_key = GoBytes::of(s->tree[i].first_key.data(), s->tree[i].first_key.size());
-      stat = &s->tree[i];
+      stat = i;
       break;
     }
   }
-  if (!stat) return OKV_R_EOF;  // :78-81
+  if (stat == SIZE_MAX) return OKV_R_EOF;  // :78-81
   const std::vector<okv_row>* rows = nullptr;
-  const int rc = read_block(s, *stat, &rows);  // :83-86
+  BatchP keep;
+  const int rc = read_block_iter(s, stat, it->direction, &rows, &keep);  // :83-86
   if (rc) return rc;
   it->rows = *rows;
+  it->rows_batch = keep;
   it->rows_nil = rows->empty();  // a block with no rows decodes to a nil slice
   if (it->direction == 1) std::reverse(it->rows.begin(), it->rows.end());  // :89-92
   it->idx = 1;                                                            // :94
@@ -389,51 +513,55 @@ int okv_iter_seek(okv_iter* it, const uint8_t* key, size_t klen) {  // Seek :102
   okv_reader* s = it->s;
   const bool unbound_start = klen == 0;                  // :105
   const bool unbound_end = klen == 1 && key[0] == 0xff;  // :106
-  const Entry* stat = nullptr;
+  size_t stat = SIZE_MAX;
   if (s->tree.empty()) return OKV_R_PANIC;
   if (unbound_start) {
-    stat = &s->tree.front();  // Min (:108-109)
+    stat = 0;  // Min (:108-109)
   } else if (unbound_end) {
-    stat = &s->tree.back();  // Max (:110-112)
+    stat = s->tree.size() - 1;  // Max (:110-112)
   } else {
     for (size_t i = upper(s, key, klen); i-- > 0;) {  // DescendLessOrEqual (:114-117)
-      stat = &s->tree[i];
+      stat = i;
       if (!(bcmp(key, klen, s->tree[i].first_key.data(), s->tree[i].first_key.size()) <= 0))
         break;
     }
   }
   std::vector<okv_row> rows;  // `rows` (:121), nil until assigned
   it->idx = 0;                // :123
-  if (!stat) {                // :124-156
+  if (stat == SIZE_MAX) {     // :124-156
     if (it->direction == 0) {
       const Entry& first = s->tree.front();
       if (bcmp(key, klen, first.first_key.data(), first.first_key.size()) < 0) {
-        stat = &first;
+        stat = 0;
       } else {
-        stat = &s->tree.back();
+        stat = s->tree.size() - 1;
         it->idx = int64_t(rows.size()) - 1;  // len(nil) - 1 == -1 (:137)
       }
     } else {
-      const Entry& last = s->tree.back();
+      const size_t last = s->tree.size() - 1;
       const std::vector<okv_row>* lr = nullptr;
-      const int rc = read_block(s, last, &lr);  // :143-146
+      BatchP keep;
+      const int rc = read_block_iter(s, last, it->direction, &lr, &keep);  // :143-146
       if (rc) return rc;
       if (lr->empty()) return OKV_R_PANIC;  // rows[len(rows)-1] (:147)
       const okv_row& lastrow = lr->back();
       if (bcmp(key, klen, lastrow.key, lastrow.key_len) > 0) {
-        stat = &last;
+        stat = last;
       } else {
-        stat = &s->tree.front();
+        stat = 0;
         it->idx = int64_t(lr->size()) - 1;  // (:154)
       }
     }
   }
-  it->stat_last_key = GoBytes::of(stat->first_key.data(), stat->first_key.size());  // :162
+  const Entry& se = s->tree[stat];
+  it->stat_last_key = GoBytes::of(se.first_key.data(), se.first_key.size());  // :162
   const std::vector<okv_row>* br = nullptr;
-  const int rrc = read_block(s, *stat, &br);  // :165-168 -- the error is discarded
+  BatchP keep;
+  const int rrc = read_block_iter(s, stat, it->direction, &br, &keep);  // :165-168 -- the error is discarded
   if (rrc == OKV_R_PANIC) return rrc;
   it->rows_nil = rrc != OKV_OK || br->empty();
   it->rows = (rrc == OKV_OK) ? *br : std::vector<okv_row>();
+  it->rows_batch = rrc == OKV_OK ? keep : BatchP();
   if (it->direction == 1) std::reverse(it->rows.begin(), it->rows.end());  // :170-172
   if ((it->direction == 0 && unbound_end) || (it->direction == 1 && unbound_start)) {
     it->idx = int64_t(it->rows.size());  // :174-175

@@ -600,6 +600,8 @@ struct Out {
   uint64_t pos;        // bytes written
   uint64_t committed;  // bytes known visible to every lane
   uint64_t frame0;     // first output byte of the current frame
+  uint32_t bmax;       // Block_Maximum_Size of the current frame (RFC 8878 3.1.1.2.4)
+  bool dry;            // measuring pass: positions advance, no byte is read or written
 };
 
 // Per segment block, written by the prologue (okv_zstd_pro_kernel) for the
@@ -626,7 +628,7 @@ struct ZBlk {
   int32_t kind;           // kKindDone / kKindSeq / kKindSlow
   int32_t st;             // kOK / kErr / kCap of the stage that owns the block
   uint32_t nseq_ok;       // sequences the sequence stage decoded (all unless the stream overflowed)
-  uint32_t pad_;
+  uint32_t bmax;          // Block_Maximum_Size of the block's frame (<= 128 KiB)
 };
 
 // Prologue context of one block: per-block literal scratch and table slots.
@@ -654,7 +656,8 @@ __device__ __forceinline__ void commit(Out& o) {
 // Lane-parallel byte copy of n bytes from src (global) to the output.
 __device__ __forceinline__ void out_copy(Out& o, const uint8_t* src, uint64_t n) {
   const int lane = threadIdx.x & 63;
-  for (uint64_t j = lane; j < n; j += 64) o.base[o.pos + j] = src[j];
+  if (!o.dry)
+    for (uint64_t j = lane; j < n; j += 64) o.base[o.pos + j] = src[j];
   o.pos += n;
 }
 
@@ -796,6 +799,8 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
   o.cap = rfl64(o.cap);
   o.frame0 = rfl64(o.frame0);
   if (n < 1) return kErr;
+  // the block's output may not exceed Block_Maximum_Size (RFC 8878 3.1.1.2.4)
+  const uint64_t blk_end = o.pos + rfl(o.bmax);
   const long long t0 = o.prof ? clock64() : 0;
   // ---- literals section header (3.1.1.3.1.1)
   const uint32_t b0 = p[0];
@@ -923,7 +928,8 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
     if (o.pos + ll > o.cap) return false;
     if (rle) {
       const int lane = threadIdx.x & 63;
-      for (uint64_t j = lane; j < ll; j += 64) o.base[o.pos + j] = rle_byte;
+      if (!o.dry)
+        for (uint64_t j = lane; j < ll; j += 64) o.base[o.pos + j] = rle_byte;
       o.pos += ll;
     } else {
       out_copy(o, lits + lit_pos, ll);
@@ -933,6 +939,7 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
     return true;
   };
   if (nseq == 0) {  // literals only (bytes after the header are not read, as libzstd)
+    if (o.pos + lit_left > blk_end) return kErr;
     if (o.pos + lit_left > o.cap) return kCap;
     emit_lits(lit_left);
     return kOK;
@@ -982,6 +989,7 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       z.of_al = fs.of_al;
       z.ml_al = fs.ml_al;
       z.rle_byte = rle_byte;
+      z.bmax = o.bmax;
     }
     return kDefer;
   } else {
@@ -1022,6 +1030,7 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
     // ---- phase A: decode up to kSeqChunk sequences (wave-uniform, SALU) ----
     const long long ta = o.prof ? clock64() : 0;
     const uint32_t cap_lim = uint32_t(min<uint64_t>(o.cap - o.pos, 0x7fffffffu));
+    const uint32_t bm_lim = uint32_t(blk_end - o.pos);  // <= 128 KiB
     const uint32_t back = uint32_t(min<uint64_t>(o.pos - o.frame0, 0x7fffffffu));
     const uint32_t lit_done = uint32_t(lit_pos);
     uint32_t cnt = 0, lsum = 0, osum = 0;
@@ -1057,11 +1066,18 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       // execution checks (3.1.1.4): literals available, match inside the frame
       if (lsum + ll > lit_lim - lit_done) return kErr;
       const uint32_t mstart = osum + ll;  // relative to o.pos
-      if (mstart + ml > cap_lim) return kCap;
+      if (mstart + ml > bm_lim) return kErr;  // the block outgrows Block_Maximum_Size
       if (off > back + mstart) return kErr;  // before the frame start (no dictionary)
+      if (mstart + ml > cap_lim) return kCap;  // (the retry pass sizes the output exactly)
       if (w0) sm.rec[cnt] = make_uint4(ll, ml, uint32_t(off), 0);
       lsum += ll;
       osum += ll + ml;
+    }
+    if (o.dry) {  // measuring pass: the chunk's bytes are not produced
+      o.pos += osum;
+      lit_pos += lsum;
+      lit_left -= lsum;
+      continue;
     }
     const long long tb = o.prof ? clock64() : 0;
     prof_add(o, 2, tb - ta);
@@ -1194,6 +1210,7 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
   if (br.pos > 0) return kErr;  // unread bits: corrupt (an over-read on the last one passes)
   if (o.prof) prof_add(o, 1, clock64() - t1);
   prof_add(o, 4, nseq);
+  if (o.pos + lit_left > blk_end) return kErr;
   if (o.pos + lit_left > o.cap) return kCap;
   emit_lits(lit_left);
   return kOK;
@@ -1277,9 +1294,15 @@ __device__ int32_t decode_frames(SM& sm, const uint8_t* src, int64_t n, Out& o, 
     const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, reserved = (fhd >> 3) & 1;
     const uint32_t has_csum = (fhd >> 2) & 1, did_flag = fhd & 3;
     if (reserved) return kErr;
-    if (!single) {
+    uint64_t window = 0;
+    if (!single) {  // Window_Descriptor (3.1.1.1.2)
       if (at >= n) return kErr;
-      at += 1;  // Window_Descriptor
+      const uint32_t wd = src[at++];
+      const uint32_t wlog = 10 + (wd >> 3);
+      // libzstd: windowLog above ZSTD_WINDOWLOG_MAX (31 on 64-bit hosts) is
+      // frameParameter_windowTooLarge
+      if (wlog > 31) return kErr;
+      window = (uint64_t(1) << wlog) + ((uint64_t(1) << wlog) / 8) * (wd & 7);
     }
     const uint32_t did_size = did_flag == 0 ? 0 : did_flag == 1 ? 1 : did_flag == 2 ? 2 : 4;
     if (at + did_size > n) return kErr;
@@ -1293,6 +1316,8 @@ __device__ int32_t decode_frames(SM& sm, const uint8_t* src, int64_t n, Out& o, 
     for (uint32_t k = 0; k < fcs_size; ++k) fcs |= uint64_t(src[at + k]) << (8 * k);
     if (fcs_size == 2) fcs += 256;
     at += fcs_size;
+    if (single) window = fcs;  // Single_Segment_flag: Window_Size = Frame_Content_Size
+    o.bmax = uint32_t(min<uint64_t>(window, kBlockMax));  // Block_Maximum_Size
     FrameState fs;
     fs.rep0 = 1;
     fs.rep1 = 4;
@@ -1309,15 +1334,18 @@ __device__ int32_t decode_frames(SM& sm, const uint8_t* src, int64_t n, Out& o, 
       const uint32_t last = bh & 1, btype = (bh >> 1) & 3, bsize = bh >> 3;
       if (btype == 0) {  // Raw_Block
         if (int64_t(bsize) > n - at) return kErr;
+        if (bsize > o.bmax) return kErr;  // Block_Size > Block_Maximum_Size (3.1.1.2.3)
         if (o.pos + bsize > o.cap) return kCap;
         out_copy(o, src + at, bsize);
         at += bsize;
       } else if (btype == 1) {  // RLE_Block
         if (at >= n) return kErr;
+        if (bsize > o.bmax) return kErr;
         if (o.pos + bsize > o.cap) return kCap;
         const uint8_t v = src[at];
         const int lane = threadIdx.x & 63;
-        for (uint64_t j = lane; j < bsize; j += 64) o.base[o.pos + j] = v;
+        if (!o.dry)
+          for (uint64_t j = lane; j < bsize; j += 64) o.base[o.pos + j] = v;
         o.pos += bsize;
         at += 1;
       } else if (btype == 2) {  // Compressed_Block (libzstd: < 128 KiB)
@@ -1345,12 +1373,12 @@ __device__ int32_t decode_frames(SM& sm, const uint8_t* src, int64_t n, Out& o, 
     if (fcs_size && o.pos - o.frame0 != fcs) return kErr;  // Frame_Content_Size check
     if (has_csum) {
       if (n - at < 4) return kErr;
-      commit(o);
-      const long long tc = o.prof ? clock64() : 0;
-      const uint32_t want = ld32z(src, at, n);
-      const uint64_t h = xxh64_out(o.base + o.frame0, o.pos - o.frame0);
-      (void)tc;
-      if (uint32_t(h) != want) return kErr;
+      if (!o.dry) {  // (content-dependent: checked by the retry's producing pass)
+        commit(o);
+        const uint32_t want = ld32z(src, at, n);
+        const uint64_t h = xxh64_out(o.base + o.frame0, o.pos - o.frame0);
+        if (uint32_t(h) != want) return kErr;
+      }
       at += 4;
     }
   }
@@ -1359,10 +1387,30 @@ __device__ int32_t decode_frames(SM& sm, const uint8_t* src, int64_t n, Out& o, 
 
 }  // namespace zst
 
+// Blocks whose frames outgrow their first output region are decoded again
+// (zstd_run): a measuring pass sizes each one's whole output, then a producing
+// pass writes it into a region of that size.  Go inflates every frame before
+// its record walk (io.Copy, segment_reader.go:326), whatever OriginalSize says.
+struct ZRetry {
+  const uint32_t* list;  // the blocks, or null: every block the prologue handed over
+  uint32_t n;
+  int dry;               // 1: measuring pass (need[i]); 0: producing pass (roff)
+  const uint64_t* roff;  // [n + 1] output offsets in dec (producing pass)
+  uint64_t* need;        // [n] decompressed bytes (measuring pass)
+  uint64_t* cap_off;     // [nblk + 1]: a produced block's region offset is stored here
+};
+
+// Raw-block outcome of ReadBlockWithStat before the decompression
+// (:303-316 in Go's order, then the rawBlockBytes[:CompressedSize] slice, :321).
+__device__ __forceinline__ int32_t zstd_raw_status(const Desc& d, uint64_t seg_bytes) {
+  const int32_t st = go_read_status(d, seg_bytes);
+  if (st != OKV_BLK_OK) return st;
+  return d.compressed_size > d.block_size ? int32_t(OKV_BLK_PANIC) : int32_t(OKV_BLK_OK);
+}
+
 // One wave per segment block, persistent over the batch.  Inputs: the raw
 // descriptors; outputs: decompressed bytes at dec + cap_off[b], their length,
 // and a per-block status (OKV_BLK_*).  lit = per-wave literal scratch.
-
 __global__ __launch_bounds__(64) void okv_zstd_kernel(const uint8_t* __restrict__ seg,
                                                       uint64_t seg_bytes, const Desc* __restrict__ descs,
                                                       uint32_t nblk, const uint64_t* __restrict__ cap_off,
@@ -1370,27 +1418,35 @@ __global__ __launch_bounds__(64) void okv_zstd_kernel(const uint8_t* __restrict_
                                                       int32_t* __restrict__ zstatus,
                                                       uint8_t* __restrict__ lit,
                                                       unsigned long long* __restrict__ prof,
-                                                      const zst::ZBlk* __restrict__ zb) {
+                                                      const zst::ZBlk* __restrict__ zb, ZRetry R) {
   __shared__ zst::Smem sm;
   uint8_t* lit_buf = lit + uint64_t(blockIdx.x) * zst::kBlockMax;
-
-  for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
-    if (zb && zst::rfl(uint32_t(zb[b].kind)) != zst::kKindSlow) continue;
+  const uint32_t count = R.list ? R.n : nblk;
+  for (uint32_t i = blockIdx.x; i < count; i += gridDim.x) {
+    const uint32_t b = R.list ? R.list[i] : i;
+    if (!R.list && zb && zst::rfl(uint32_t(zb[b].kind)) != zst::kKindSlow) continue;
+    // producing pass: only the blocks the measuring pass sized
+    if (R.list && !R.dry && zst::rfl(uint32_t(zstatus[b])) != OKV_BLK_CAPACITY) continue;
     const Desc d = descs[b];
     int32_t st = OKV_BLK_OK;
     zst::Out o;
     o.prof = prof;
     const long long tb = prof ? clock64() : 0;
-    o.base = dec + cap_off[b];
-    o.cap = cap_off[b + 1] - cap_off[b];
-    o.pos = o.committed = o.frame0 = 0;
-    if (int64_t(d.offset) < 0 || d.offset >= seg_bytes) {
-      st = OKV_BLK_EOF;  // :303-313
-    } else if (seg_bytes - d.offset < d.block_size) {
-      st = OKV_BLK_SHORT;  // :314-316
-    } else if (d.compressed_size > d.block_size) {
-      st = OKV_BLK_PANIC;  // rawBlockBytes[:CompressedSize] out of range (:321)
+    o.dry = R.dry != 0;
+    o.bmax = 0;
+    if (!R.list) {
+      o.base = dec + cap_off[b];
+      o.cap = cap_off[b + 1] - cap_off[b];
+    } else if (R.dry) {
+      o.base = nullptr;
+      o.cap = uint64_t(1) << 62;  // no frame set reaches it
     } else {
+      o.base = dec + R.roff[i];
+      o.cap = R.roff[i + 1] - R.roff[i];
+    }
+    o.pos = o.committed = o.frame0 = 0;
+    st = zstd_raw_status(d, seg_bytes);
+    if (st == OKV_BLK_OK) {
       const uint8_t* src = seg + d.offset;
       const int32_t r = zst::decode_frames<false>(sm, src, int64_t(d.compressed_size), o, lit_buf,
                                                          nullptr);
@@ -1398,8 +1454,18 @@ __global__ __launch_bounds__(64) void okv_zstd_kernel(const uint8_t* __restrict_
       st = r == zst::kOK ? OKV_BLK_OK : r == zst::kCap ? OKV_BLK_CAPACITY : OKV_BLK_ZSTD_ERROR;
     }
     if ((threadIdx.x & 63) == 0) {
-      zstatus[b] = st;
-      dec_len[b] = st == OKV_BLK_OK ? o.pos : 0;
+      if (R.list && R.dry) {
+        // sized: stays OKV_BLK_CAPACITY for the producing pass
+        R.need[i] = st == OKV_BLK_OK ? o.pos : 0;
+        if (st != OKV_BLK_OK) {
+          zstatus[b] = st;
+          dec_len[b] = 0;
+        }
+      } else {
+        zstatus[b] = st;
+        dec_len[b] = st == OKV_BLK_OK ? o.pos : 0;
+        if (R.list && st == OKV_BLK_OK) R.cap_off[b] = R.roff[i];
+      }
     }
     if (prof) {
       zst::prof_add(o, 3, clock64() - tb);
@@ -1407,6 +1473,48 @@ __global__ __launch_bounds__(64) void okv_zstd_kernel(const uint8_t* __restrict_
     }
     __builtin_amdgcn_s_waitcnt(0);
   }
+}
+
+// The blocks the first pass left at OKV_BLK_CAPACITY (frames decompressing
+// past their first region) -> list[*count].
+__global__ __launch_bounds__(256) void okv_zstd_list_kernel(const int32_t* __restrict__ zstatus,
+                                                            uint32_t nblk, uint32_t* __restrict__ list,
+                                                            uint32_t* __restrict__ count) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  const bool hit = b < nblk && zstatus[b] == OKV_BLK_CAPACITY;
+  const uint64_t m = __ballot(hit);
+  if (!m) return;
+  const int lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  if (lane == __ffsll(static_cast<unsigned long long>(m)) - 1)
+    base = atomicAdd(count, uint32_t(__popcll(m)));
+  base = __shfl(base, __ffsll(static_cast<unsigned long long>(m)) - 1, 64);
+  if (hit) list[base + __popcll(m & ((uint64_t(1) << lane) - 1))] = b;
+}
+
+// roff[i] = base + sum_{j < i} round16(need[j]); roff[n] = base + total.
+__global__ __launch_bounds__(1024) void okv_zstd_roff_kernel(const uint64_t* __restrict__ need,
+                                                             uint32_t n, uint64_t base,
+                                                             uint64_t* __restrict__ roff) {
+  __shared__ uint64_t sm[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t carry = base;
+  for (uint32_t i0 = 0; i0 < n; i0 += 1024) {
+    const uint32_t i = i0 + threadIdx.x;
+    const uint64_t v = i < n ? round16(need[i]) : 0;
+    const uint64_t inc = wave_incl_scan(v, lane);
+    if (lane == 63) sm[wave] = inc;
+    __syncthreads();
+    uint64_t before = 0, tot = 0;
+    for (int w = 0; w < 16; ++w) {
+      before += w < wave ? sm[w] : 0;
+      tot += sm[w];
+    }
+    if (i < n) roff[i] = carry + before + inc - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) roff[n] = carry;
 }
 
 // ---- stage 1: prologue, one wave per segment block -------------------------------
@@ -1431,12 +1539,10 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
     o.base = dec + cap_off[b];
     o.cap = cap_off[b + 1] - cap_off[b];
     o.pos = o.committed = o.frame0 = 0;
-    if (int64_t(d.offset) < 0 || d.offset >= seg_bytes) {
-      st = OKV_BLK_EOF;  // :303-313
-    } else if (seg_bytes - d.offset < d.block_size) {
-      st = OKV_BLK_SHORT;  // :314-316
-    } else if (d.compressed_size > d.block_size) {
-      st = OKV_BLK_PANIC;  // rawBlockBytes[:CompressedSize] out of range (:321)
+    o.dry = false;
+    o.bmax = 0;
+    if ((st = zstd_raw_status(d, seg_bytes)) != OKV_BLK_OK) {
+      // Seek / makeslice / EOF / short read / slice bounds (:303-321)
     } else {
       zst::Pro pro;
       pro.lit_blk = lits + cap_off[b];
@@ -1633,8 +1739,9 @@ __device__ __forceinline__ void wb_slide(WinBits& w) {
 // its extra bits (16) << 6 | match-length code (6) << 22 | extra bits (16) << 28
 // | offset (20, saturated) << 44.  The executor turns codes into lengths and
 // makes the execution checks (RFC 8878 3.1.1.4) in sequence order; an offset
-// past 2^20 - 1 is past any single-block frame's output (<= 128 KiB), so the
-// saturated value fails the same check.
+// past 2^20 - 1 is past any single-block frame's output, which the executor
+// holds to Block_Maximum_Size (<= 128 KiB, ZBlk::bmax) before the offset check,
+// so the saturated value fails the same check.
 __device__ __forceinline__ uint64_t seq_pack(uint32_t llc, uint32_t llx, uint32_t mlc, uint32_t mlx,
                                              uint32_t off) {
   return uint64_t(llc | (llx << 6) | (mlc << 22)) | (uint64_t(mlx) << 28) |
@@ -1891,6 +1998,7 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
     int32_t bst = zst::kOK;
     const uint32_t nseq = zst::rfl(zb[b].nseq_ok), lit_total = zst::rfl(zb[b].lit_total);
     const uint32_t zcap = zst::rfl(zb[b].cap);
+    const uint32_t bmax = zst::rfl(zb[b].bmax);  // Block_Maximum_Size (<= 128 KiB)
     const uint32_t flags = zst::rfl(zb[b].flags);
     const bool rle = flags & zst::kFlagRle;
     const uint8_t rle_byte = uint8_t(zst::rfl(zb[b].rle_byte));
@@ -1938,15 +2046,18 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
         if (k < nrem)
           S[i0 + k] = uint64_t(ll[u]) | (uint64_t(ml[u]) << 18) | (uint64_t(of[u]) << 36);
       }
-      uint32_t fcode = 0;  // the lane's first failing sequence: 1 / 3 kErr, 2 kCap
+      uint32_t fcode = 0;  // the lane's first failing sequence: 1 / 3 / 4 kErr, 2 kCap
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         // (32-bit: lengths < 2^18, 256 per window, totals <= cap < 2^31)
         const uint32_t mst = O + opx + ll[u];  // match start in the block output
+        // (the general kernel's order; a block past Block_Maximum_Size is
+        // corrupt whatever its region, so that check precedes the capacity)
         const uint32_t code = 4 * lane + u >= nrem            ? 0u
                               : lp + lpx + ll[u] > lit_total  ? 1u
-                              : mst + ml[u] > zcap            ? 2u
+                              : mst + ml[u] > bmax            ? 4u
                               : of[u] > mst                   ? 3u
+                              : mst + ml[u] > zcap            ? 2u
                                                               : 0u;
         fcode = fcode ? fcode : code;
         lpx += ll[u];
@@ -1962,6 +2073,7 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
       lp += __builtin_amdgcn_readlane(lpx, 63);
     }
     if (bst == zst::kOK && !exec) bst = st0;
+    if (bst == zst::kOK && uint64_t(O) + (lit_total - lp) > bmax) bst = zst::kErr;
     if (bst == zst::kOK && uint64_t(O) + (lit_total - lp) > zcap) bst = zst::kCap;
     if (bst == zst::kOK && (flags & zst::kFlagFcs) && uint64_t(O) + (lit_total - lp) != zb[b].fcs)
       bst = zst::kErr;  // Frame_Content_Size check
@@ -2262,7 +2374,17 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
     for (int k = 0; k < 10; ++k) prof[blockIdx.x * 16 + k] = pacc[k];
 }
 
-// Exclusive scan of per-block decompressed capacities (round16(OriginalSize)).
+// First output region of a block: round16(OriginalSize), which is exactly the
+// frame's output for Go-written blocks -- bounded, so a descriptor claiming a
+// huge OriginalSize does not size the scratch (int(OriginalSize) < 0 walks no
+// record at all, :340).  Frames that decompress past the region are decoded
+// again into a region of their measured size (zstd_run).
+__device__ __forceinline__ uint64_t first_region(const Desc& d) {
+  const uint64_t bound = (uint64_t(1) << 20) + 32 * min(d.compressed_size, uint64_t(1) << 32);
+  return round16(min(d.original_size, bound));
+}
+
+// Exclusive scan of per-block first regions (first_region).
 __global__ __launch_bounds__(1024) void okv_zstd_cap_kernel(const Desc* __restrict__ descs,
                                                             uint32_t nblk,
                                                             uint64_t* __restrict__ cap_off) {
@@ -2271,7 +2393,7 @@ __global__ __launch_bounds__(1024) void okv_zstd_cap_kernel(const Desc* __restri
   uint64_t carry = 0;
   for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
     const uint32_t i = b0 + threadIdx.x;
-    const uint64_t v = i < nblk ? round16(descs[i].original_size) : 0;
+    const uint64_t v = i < nblk ? first_region(descs[i]) : 0;
     const uint64_t inc = wave_incl_scan(v, lane);
     if (lane == 63) sm[wave] = inc;
     __syncthreads();
@@ -2303,15 +2425,74 @@ __global__ void okv_zstd_desc_kernel(const Desc* __restrict__ descs, uint32_t nb
   out[b] = d;
 }
 
+// Frames that decompress past their first region (first_region): the general
+// kernel measures each one's whole output (a pass that reads and writes no
+// byte), then decodes it into a region of that size appended to the scratch
+// (kept: the other blocks' bytes are already there).  Go's io.Copy inflates
+// the whole frame set before the record walk (segment_reader.go:320-330), so
+// these blocks decode and walk like any other; no OKV_BLK_CAPACITY status
+// leaves the zstd stage.  One extra host round trip per zstd decode (the
+// retry count); Go-written blocks never need the retry.
+int zstd_regrow(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
+                uint32_t nblk, uint64_t* total_io) {
+  hipStream_t s = ctx->stream;
+  int rc;
+  if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_list), &ctx->z_cap_list,
+                 (size_t(nblk) + 1) * 4 + 64)))
+    return rc;
+  uint32_t* d_count = ctx->z_list + nblk;
+  OKV_HIP(hipMemsetAsync(d_count, 0, 4, s));
+  hipLaunchKernelGGL(okv_zstd_list_kernel, dim3((nblk + 255) / 256), dim3(256), 0, s, ctx->z_status,
+                     nblk, ctx->z_list, d_count);
+  uint32_t n = 0;
+  OKV_HIP(hipMemcpyAsync(&n, d_count, 4, hipMemcpyDeviceToHost, s));
+  OKV_HIP(hipStreamSynchronize(s));
+  ctx->z_retried = n;
+  if (n == 0) return OKV_OK;
+  if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_need), &ctx->z_cap_need,
+                 (size_t(n) * 2 + 2) * 8)))
+    return rc;
+  uint64_t* need = ctx->z_need;
+  uint64_t* roff = ctx->z_need + n;
+  const uint32_t grid = std::min<uint32_t>(n, 2048);
+  // the literal scratch is sized for the first pass's grid (>= this one)
+  hipLaunchKernelGGL(okv_zstd_kernel, dim3(grid), dim3(64), 0, s, seg, seg_bytes, descs, nblk,
+                     ctx->z_cap_off, ctx->z_dec, ctx->z_dec_len, ctx->z_status, ctx->z_lit, nullptr,
+                     nullptr, ZRetry{ctx->z_list, n, 1, nullptr, need, nullptr});
+  const uint64_t base = (*total_io + 15) & ~uint64_t(15);
+  hipLaunchKernelGGL(okv_zstd_roff_kernel, dim3(1), dim3(1024), 0, s, need, n, base, roff);
+  OKV_HIP(hipGetLastError());
+  uint64_t end = 0;
+  OKV_HIP(hipMemcpyAsync(&end, roff + n, 8, hipMemcpyDeviceToHost, s));
+  OKV_HIP(hipStreamSynchronize(s));
+  if (end + 64 > ctx->z_cap_dec) {  // grow the scratch, keeping the first pass's bytes
+    uint8_t* nd = nullptr;
+    const size_t c = (size_t(end) + 64 + 4095) & ~size_t(4095);
+    OKV_HIP(hipMalloc(&nd, c));
+    OKV_HIP(hipMemcpyAsync(nd, ctx->z_dec, *total_io, hipMemcpyDeviceToDevice, s));
+    OKV_HIP(hipStreamSynchronize(s));
+    (void)hipFree(ctx->z_dec);
+    ctx->z_dec = nd;
+    ctx->z_cap_dec = c;
+  }
+  hipLaunchKernelGGL(okv_zstd_kernel, dim3(grid), dim3(64), 0, s, seg, seg_bytes, descs, nblk,
+                     ctx->z_cap_off, ctx->z_dec, ctx->z_dec_len, ctx->z_status, ctx->z_lit, nullptr,
+                     nullptr, ZRetry{ctx->z_list, n, 0, roff, nullptr, ctx->z_cap_off});
+  OKV_HIP(hipGetLastError());
+  *total_io = end;
+  return OKV_OK;
+}
+
 // Decompress every block into dec + cap_off[b] (capacities already scanned;
 // total = cap_off[nblk]).  Stages: prologue -> sequence offsets -> sequences ->
 // executor -> general kernel for the blocks the prologue handed over.
 // OKV_ZSTD_GENERAL=1 sends every block through the general kernel (A/B);
 // OKV_ZSTD_PROF=1 prints per-stage milliseconds to stderr (diagnostics only).
 int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
-             uint32_t nblk, uint64_t total) {
+             uint32_t nblk, uint64_t* total_io) {
   hipStream_t s = ctx->stream;
   int rc;
+  const uint64_t total = *total_io;
   const bool general = ctx->zstd_one_pass || okv::knob("OKV_ZSTD_GENERAL") != nullptr;
   const bool prof = okv::knob("OKV_ZSTD_PROF") != nullptr;
   hipEvent_t ev[6] = {};
@@ -2383,8 +2564,9 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
     return rc;
   hipLaunchKernelGGL(okv_zstd_kernel, dim3(grid), dim3(64), 0, s, seg, seg_bytes, descs, nblk,
                      ctx->z_cap_off, ctx->z_dec, ctx->z_dec_len, ctx->z_status, ctx->z_lit,
-                     nullptr, zb);
+                     nullptr, zb, ZRetry{nullptr, 0, 0, nullptr, nullptr, nullptr});
   OKV_HIP(hipGetLastError());
+  if ((rc = zstd_regrow(ctx, seg, seg_bytes, descs, nblk, total_io))) return rc;
   if (prof) {
     (void)hipEventRecord(ev[4], s);
     (void)hipStreamSynchronize(s);

@@ -3,8 +3,10 @@
 Mirrors /root/reference/sst/segment_reader.go and segment_row_iter.go:
 method names, argument meaning, row order and error behaviour.  Errors carry
 the Go sentinel name in ``.kind`` (ErrNoRows, EOF, ErrAlreadyClosed, ...);
-Go panics raise ``GoPanic``.  Every block read is served from one batched
-okv_decode_blocks call on the GPU -- there is no CPU decode path.
+Go panics raise ``GoPanic``.  Every block read is a batched okv_decode_blocks
+call on the GPU, bounded as the cgo shim's ReadBlocks (one block for GetRow,
+the selected set for GetRange, a 256-block window for RowIter) -- there is no
+CPU decode path.
 """
 from __future__ import annotations
 
@@ -133,6 +135,12 @@ class SegmentReader:
 
     def Close(self):
         _check(lib().okv_reader_close(self._h))
+
+    def io_stats(self) -> dict:
+        """GPU decode calls, blocks decoded and storage bytes staged so far."""
+        io = _lib.ReaderIO()
+        _check(lib().okv_reader_io_stats(self._h, C.byref(io)))
+        return {"calls": io.calls, "blocks": io.blocks, "bytes_staged": io.bytes_staged}
 
 
 class RowIter:

@@ -424,9 +424,30 @@ int oref_fetch_meta(const uint8_t *buf, uint64_t buf_len, int64_t file_bytes, or
 typedef size_t (*zstd_dec_fn)(void *, size_t, const void *, size_t);
 typedef unsigned (*zstd_iserr_fn)(size_t);
 typedef int (*zstd_code_fn)(size_t);
+typedef void *(*zstd_mkd_fn)(void);
+typedef size_t (*zstd_freed_fn)(void *);
+typedef size_t (*zstd_begin_fn)(void *);
+typedef size_t (*zstd_fh_fn)(void *, const void *, size_t);
+typedef size_t (*zstd_next_fn)(void *);
+typedef int (*zstd_nit_fn)(void *);
+typedef size_t (*zstd_cont_fn)(void *, void *, size_t, const void *, size_t);
+/* ZSTD_frameHeader (zstd.h 1.4.x) */
+typedef struct {
+  unsigned long long frameContentSize, windowSize;
+  unsigned blockSizeMax;
+  int frameType;
+  unsigned headerSize, dictID, checksumFlag;
+} zstd_fh_t;
 static zstd_dec_fn z_dec;
 static zstd_iserr_fn z_iserr;
 static zstd_code_fn z_code;
+static zstd_mkd_fn z_mkd;
+static zstd_freed_fn z_freed;
+static zstd_begin_fn z_begin;
+static zstd_fh_fn z_fh;
+static zstd_next_fn z_next;
+static zstd_nit_fn z_nit;
+static zstd_cont_fn z_cont;
 static pthread_once_t z_once = PTHREAD_ONCE_INIT;
 static void zstd_load(void) {
   void *h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL);
@@ -434,16 +455,72 @@ static void zstd_load(void) {
   z_dec = (zstd_dec_fn)dlsym(h, "ZSTD_decompress");
   z_iserr = (zstd_iserr_fn)dlsym(h, "ZSTD_isError");
   z_code = (zstd_code_fn)dlsym(h, "ZSTD_getErrorCode");
+  z_mkd = (zstd_mkd_fn)dlsym(h, "ZSTD_createDCtx");
+  z_freed = (zstd_freed_fn)dlsym(h, "ZSTD_freeDCtx");
+  z_begin = (zstd_begin_fn)dlsym(h, "ZSTD_decompressBegin");
+  z_fh = (zstd_fh_fn)dlsym(h, "ZSTD_getFrameHeader");
+  z_next = (zstd_next_fn)dlsym(h, "ZSTD_nextSrcSizeToDecompress");
+  z_nit = (zstd_nit_fn)dlsym(h, "ZSTD_nextInputType");
+  z_cont = (zstd_cont_fn)dlsym(h, "ZSTD_decompressContinue");
 }
+/* RFC 8878 3.1.1.2.3-4: a block decompresses to at most Block_Maximum_Size =
+ * min(Window_Size, 128 KiB) (ZSTD_frameHeader.blockSizeMax).  libzstd 1.4.8's
+ * one-shot decoder does not enforce it (a 200 KiB RLE block decodes); the
+ * device decoder does, as the RFC and newer libzstd do.  Replays the frames
+ * block by block (ZSTD_decompressContinue) into out (out_len bytes, the
+ * one-shot result's length); 0 if any block exceeds its limit or the
+ * block-wise API rejects the input (e.g. legacy v0.5-v0.7 frames, which the
+ * 1.4.8 one-shot path still accepts and RFC 8878 does not define). */
+static int zstd_blocks_within_max(const uint8_t *src, uint64_t n, uint8_t *out, uint64_t out_len) {
+  void *d = z_mkd();
+  if (!d) return 0;
+  uint64_t at = 0, pos = 0;
+  int ok = 1;
+  while (ok && at < n) {
+    zstd_fh_t fh;
+    size_t r = z_fh(&fh, src + at, (size_t)(n - at));
+    if (z_iserr(r) || r != 0 || z_iserr(z_begin(d))) {
+      ok = 0;
+      break;
+    }
+    for (;;) {
+      size_t need = z_next(d);
+      if (need == 0) break;
+      if (need > n - at) {
+        ok = 0;
+        break;
+      }
+      int kind = z_nit(d); /* ZSTDnit_block = 2, ZSTDnit_lastBlock = 3 */
+      size_t m = z_cont(d, out + pos, (size_t)(out_len + 64 - pos), src + at, need);
+      if (z_iserr(m) || ((kind == 2 || kind == 3) && fh.frameType == 0 && m > fh.blockSizeMax)) {
+        ok = 0;
+        break;
+      }
+      at += need;
+      pos += m;
+    }
+  }
+  z_freed(d);
+  return ok && pos == out_len;
+}
+/* Every frame of src[0, n), the whole output whatever OriginalSize says (Go's
+ * io.Copy inflates the frames before its record walk); hint sizes the first
+ * buffer only. */
 static int zstd_block(const uint8_t *src, uint64_t n, uint64_t hint, uint8_t **out,
                       uint64_t *out_len) {
   pthread_once(&z_once, zstd_load);
-  if (!z_dec || !z_iserr || !z_code) return OREF_BLK_UNSUPPORTED;
-  uint64_t cap = hint + 65536;
+  if (!z_dec || !z_iserr || !z_code || !z_mkd || !z_freed || !z_begin || !z_fh || !z_next ||
+      !z_nit || !z_cont)
+    return OREF_BLK_UNSUPPORTED;
+  uint64_t cap = (hint < (1ull << 24) ? hint : (1ull << 24)) + 65536;
   for (;;) {
-    uint8_t *buf = (uint8_t *)malloc(cap);
+    uint8_t *buf = (uint8_t *)malloc(cap + 64);
     size_t r = z_dec(buf, cap, n ? src : (const uint8_t *)"", n);
     if (!z_iserr(r)) {
+      if (!zstd_blocks_within_max(n ? src : (const uint8_t *)"", n, buf, r)) {
+        free(buf);
+        return OREF_BLK_ZSTD;
+      }
       *out = buf;
       *out_len = r;
       return OREF_BLK_OK;
@@ -462,6 +539,11 @@ static int block_buffer(const uint8_t *seg, uint64_t seg_len, const oref_block_d
                         uint8_t **owned) {
   *owned = NULL;
   if ((int64_t)d->offset < 0) return OREF_BLK_EOF; /* Seek error :303-306 */
+  /* make([]byte, stat.BlockSize) (:309): the uint64 converts to int; a length
+   * that is negative as int or above the runtime's maxAlloc panics
+   * ("makeslice: len out of range", runtime/slice.go makeslice; maxAlloc =
+   * 1 << heapAddrBits = 2^48 on linux/amd64 and linux/arm64, runtime/malloc.go) */
+  if (d->block_size > OREF_GO_MAX_ALLOC) return OREF_BLK_PANIC;
   if (d->offset >= seg_len) return OREF_BLK_EOF;   /* bytes.Reader.Read io.EOF :310-313 */
   uint64_t avail = seg_len - d->offset;
   if (avail < d->block_size) return OREF_BLK_SHORT; /* :314-316 */
@@ -486,6 +568,9 @@ static int block_buffer(const uint8_t *seg, uint64_t seg_len, const oref_block_d
 typedef void (*row_cb)(void *ctx, uint64_t rec, uint64_t klen, uint64_t vlen);
 static int walk_records(const uint8_t *buf, uint64_t len, uint64_t orig, row_cb cb, void *ctx) {
   uint64_t p = 0;
+  /* `totalReadBytes < int(stat.OriginalSize)` (:340): int(OriginalSize) is
+   * negative from 2^63 on, so the loop runs no iteration (nil rows, no error) */
+  if ((int64_t)orig < 0) orig = 0;
   while (p < orig) {
     if (len - p < 2) return OREF_BLK_PANIC; /* p <= len always holds here */
     uint64_t kl = rd16(buf + p);

@@ -51,6 +51,10 @@ extern "C" {
 #define OREF_BLK_UNSUPPORTED 4 /* index-only spans of a zstd block; libzstd missing */
 #define OREF_BLK_ZSTD 6        /* zstd.NewReader / io.Copy error (:321-330) */
 
+/* Go runtime maxAlloc on 64-bit linux (1 << heapAddrBits, heapAddrBits = 48):
+ * make([]byte, n) panics for n above it (runtime/malloc.go, runtime/slice.go) */
+#define OREF_GO_MAX_ALLOC (1ull << 48)
+
 #define OREF_COMP_NONE 0
 #define OREF_COMP_ZSTD 1
 #define OREF_COMP_LZ4 2

@@ -385,6 +385,11 @@ def bytes_to_metadata(meta: bytes) -> SegmentMetadata:
     return md
 
 
+# Go runtime maxAlloc on 64-bit linux: 1 << heapAddrBits (48) (runtime/malloc.go);
+# make([]byte, n) panics above it (runtime/slice.go makeslice)
+GO_MAX_ALLOC = 1 << 48
+
+
 def read_block(seg: bytes, desc, compression: int):
     """ReadBlockWithStat segment_reader.go:295-355 on raw bytes.
 
@@ -392,8 +397,14 @@ def read_block(seg: bytes, desc, compression: int):
     ``desc`` = (offset, block_size, original_size[, compressed_size]).
     """
     off, bsize, orig = desc[0], desc[1], desc[2]
-    if off >= (1 << 63) or off >= len(seg):
-        return BLK_EOF, None  # Seek error / io.EOF :303-313
+    if off >= (1 << 63):
+        return BLK_EOF, None  # Seek(int64(Offset)) error: negative position (:303-306)
+    if bsize > GO_MAX_ALLOC:
+        # make([]byte, stat.BlockSize) (:309): negative as int, or above the
+        # runtime's maxAlloc -> "makeslice: len out of range" panic
+        return BLK_PANIC, None
+    if off >= len(seg):
+        return BLK_EOF, None  # bytes.Reader.Read io.EOF (:310-313)
     if len(seg) - off < bsize:
         return BLK_SHORT, None  # :314-316
     if compression == COMP_ZSTD:
@@ -412,6 +423,8 @@ def read_block(seg: bytes, desc, compression: int):
     rows = None
     p = 0
     n = len(buf)
+    if orig >= (1 << 63):
+        orig = 0  # `totalReadBytes < int(stat.OriginalSize)` (:340): negative bound, no iteration
     while p < orig:  # :340
         if n - p < 2:
             return BLK_PANIC, None

@@ -44,6 +44,18 @@ def lib():
         L.ZSTD_isError.argtypes = [sz]
         L.ZSTD_getErrorCode.restype = C.c_int
         L.ZSTD_getErrorCode.argtypes = [sz]
+        L.ZSTD_createDCtx.restype = p
+        L.ZSTD_freeDCtx.argtypes = [p]
+        L.ZSTD_decompressBegin.restype = sz
+        L.ZSTD_decompressBegin.argtypes = [p]
+        L.ZSTD_getFrameHeader.restype = sz
+        L.ZSTD_getFrameHeader.argtypes = [p, p, sz]
+        L.ZSTD_nextSrcSizeToDecompress.restype = sz
+        L.ZSTD_nextSrcSizeToDecompress.argtypes = [p]
+        L.ZSTD_nextInputType.restype = C.c_int
+        L.ZSTD_nextInputType.argtypes = [p]
+        L.ZSTD_decompressContinue.restype = sz
+        L.ZSTD_decompressContinue.argtypes = [p, p, sz, p, sz]
         _L = L
     return _L
 
@@ -73,12 +85,9 @@ def compress(data: bytes, level: int = 3, checksum: bool = True, content_size: b
         L.ZSTD_freeCCtx(cctx)
 
 
-def decompress(frames: bytes, hint: int = 0):
-    """All frames of `frames` -> bytes, or None on a decode error (Go: the
-    io.Copy error of segment_reader.go:326-330)."""
-    L = lib()
+def _oneshot(L, frames: bytes, hint: int):
     src = C.create_string_buffer(bytes(frames), max(len(frames), 1))
-    cap = max(hint, 64) + 65536
+    cap = max(min(hint, 1 << 24), 64) + 65536
     while True:
         dst = C.create_string_buffer(cap)
         n = L.ZSTD_decompress(dst, cap, src, len(frames))
@@ -87,6 +96,70 @@ def decompress(frames: bytes, hint: int = 0):
         if L.ZSTD_getErrorCode(n) != ERR_DST_TOO_SMALL or cap > (1 << 31):
             return None
         cap *= 2
+
+
+class _FrameHeader(C.Structure):  # ZSTD_frameHeader (zstd.h, 1.4.x)
+    _fields_ = [("frameContentSize", C.c_ulonglong), ("windowSize", C.c_ulonglong),
+                ("blockSizeMax", C.c_uint), ("frameType", C.c_int), ("headerSize", C.c_uint),
+                ("dictID", C.c_uint), ("checksumFlag", C.c_uint)]
+
+
+NIT_BLOCK, NIT_LAST_BLOCK = 2, 3  # ZSTD_nextInputType_e
+
+
+def _blocks_within_max(L, frames: bytes, out_len: int) -> bool:
+    """Replays the frames block by block (ZSTD_decompressContinue) and checks
+    every block's decompressed size against its frame's Block_Maximum_Size =
+    min(Window_Size, 128 KiB) (RFC 8878 3.1.1.2.3-4; ZSTD_frameHeader.blockSizeMax).
+    libzstd 1.4.8's one-shot decoder does not enforce that limit (an RLE block
+    of 200 KiB decodes); the device decoder does, as the RFC -- and newer
+    libzstd -- require.  Also False for input the block-wise API rejects
+    (e.g. the legacy v0.5-v0.7 frames 1.4.8's one-shot path still accepts)."""
+    d = L.ZSTD_createDCtx()
+    try:
+        src = bytes(frames)
+        sbuf = C.create_string_buffer(src, max(len(src), 1))
+        dst = C.create_string_buffer(out_len + 64)
+        at = pos = 0
+        while at < len(src):
+            fh = _FrameHeader()
+            r = L.ZSTD_getFrameHeader(C.byref(fh), C.byref(sbuf, at), len(src) - at)
+            if L.ZSTD_isError(r) or r != 0:
+                return False
+            bmax = fh.blockSizeMax
+            if L.ZSTD_isError(L.ZSTD_decompressBegin(d)):
+                return False
+            while True:
+                need = L.ZSTD_nextSrcSizeToDecompress(d)
+                if need == 0:
+                    break
+                if need > len(src) - at:
+                    return False
+                kind = L.ZSTD_nextInputType(d)
+                n = L.ZSTD_decompressContinue(d, C.byref(dst, pos), out_len + 64 - pos,
+                                              C.byref(sbuf, at), need)
+                if L.ZSTD_isError(n):
+                    return False
+                if kind in (NIT_BLOCK, NIT_LAST_BLOCK) and fh.frameType == 0 and n > bmax:
+                    return False
+                at += need
+                pos += n
+        return pos == out_len
+    finally:
+        L.ZSTD_freeDCtx(d)
+
+
+def decompress(frames: bytes, hint: int = 0):
+    """All frames of `frames` -> bytes, or None on a decode error (Go: the
+    io.Copy error of segment_reader.go:326-330).  libzstd's one-shot decode,
+    plus RFC 8878's Block_Maximum_Size rule (_blocks_within_max).  The whole
+    frame set is inflated whatever the caller's OriginalSize (`hint` only
+    sizes the first buffer): Go's io.Copy does the same before its record walk."""
+    L = lib()
+    out = _oneshot(L, frames, hint)
+    if out is None or not _blocks_within_max(L, frames, len(out)):
+        return None
+    return out
 
 
 def skippable_frame(payload: bytes, nibble: int = 0) -> bytes:

@@ -157,6 +157,19 @@ def crafted_case():
     blocks.append({"note": "offset past end", "desc": [len(seg) + 100, 16, 4, 0]})
     # 12: zero-length block at a valid offset, OriginalSize 0
     blocks.append({"note": "empty block", "desc": [0, 0, 0, 0]})
+    # Go's int() conversions (segment_reader.go:303-340)
+    # 13/14: int(OriginalSize) < 0 -> the loop runs no iteration: nil rows, no error
+    blocks.append({"note": "OriginalSize 2^63", "desc": [0, 64, 1 << 63, 0]})
+    blocks.append({"note": "OriginalSize 2^64-1", "desc": [0, 64, (1 << 64) - 1, 0]})
+    # 15/16: make([]byte, BlockSize) above maxAlloc (2^48) / negative as int -> panic
+    blocks.append({"note": "BlockSize 2^48+1 (makeslice panic)", "desc": [0, (1 << 48) + 1, 8, 0]})
+    blocks.append({"note": "BlockSize 2^63 (makeslice panic)", "desc": [0, 1 << 63, 8, 0]})
+    # 17: BlockSize == maxAlloc is allocatable: the read is short
+    blocks.append({"note": "BlockSize 2^48 (short)", "desc": [0, 1 << 48, 8, 0]})
+    # 18: make panics before the read would see io.EOF
+    blocks.append({"note": "past end, BlockSize 2^50", "desc": [len(seg) + 7, 1 << 50, 4, 0]})
+    # 19: the Seek error (negative int64 Offset) comes before make
+    blocks.append({"note": "Offset 2^63+1, BlockSize 2^60", "desc": [(1 << 63) + 1, 1 << 60, 4, 0]})
     seg_b = bytes(seg)
     for bl in blocks:
         st, rws = P.read_block(seg_b, bl["desc"], P.COMP_NONE)

@@ -92,3 +92,175 @@ def test_product_reader_matches_oracle_on_random_iteration(decoder):
                 continue
             got = it.Next()
             assert (got.Key, got.Value) == (want.Key, want.Value), step
+
+
+# ---- bounded block reads (the cgo shim's ReadBlocks) --------
+
+def _segment(nrows=6000, vmax=300, seed=9):
+    import random
+    rng = random.Random(seed)
+    rows = [(b"k%06d" % i, bytes(rng.getrandbits(8) for _ in range(rng.randint(0, vmax))))
+            for i in range(nrows)]
+    w = okv.SegmentWriter()
+    for k, v in rows:
+        w.WriteRow(k, v)
+    flen, meta = w.Close()
+    return rows, w.data().tobytes(), flen, meta
+
+
+def test_getrow_stages_one_block(decoder):
+    """GetRow decodes exactly the block the btree floor picks
+    (segment_reader.go:381-392): one GPU call staging that block's BlockSize."""
+    from oracle import pyoracle as P
+    rows, data, flen, meta = _segment()
+    md = P.bytes_to_metadata(meta)
+    pr = R.SegmentReader(data, flen, decoder)
+    for k, v in (rows[0], rows[2999], rows[-1]):
+        before = pr.io_stats()
+        assert pr.GetRow(k).Value == (v or None)
+        after = pr.io_stats()
+        assert after["calls"] - before["calls"] == 1
+        assert after["blocks"] - before["blocks"] == 1
+        st = max((e for e in md.entries if e.FirstKey <= k), key=lambda e: e.FirstKey)
+        assert after["bytes_staged"] - before["bytes_staged"] == st.BlockSize
+
+
+def test_rowiter_window_batches(decoder):
+    """RowIter decodes 256 blocks per GPU call in its direction and serves the
+    rest of the window without a call; rows equal the oracle's."""
+    from oracle import pyoracle as P
+    rows, data, flen, meta = _segment(nrows=30000, vmax=120)
+    nb = len(P.bytes_to_metadata(meta).entries)
+    assert nb > 600
+    for direction in (0, 1):
+        pr = R.SegmentReader(data, flen, decoder)
+        it = pr.RowIter(direction)
+        got = []
+        while True:
+            try:
+                p = it.Next()
+            except R.GoError as e:
+                assert e.kind == "EOF"
+                break
+            got.append((p.Key, p.Value or b""))
+        want = rows if direction == 0 else rows[::-1]
+        assert got == want
+        io = pr.io_stats()
+        assert io["calls"] == -(-nb // 256) and io["blocks"] == nb
+
+
+def test_getrange_stages_selected_blocks(decoder):
+    """GetRange decodes the block set its btree walks select (:421-458) in one
+    call; rows equal the oracle's."""
+    from oracle import pyoracle as P
+    rows, data, flen, meta = _segment()
+    md = P.bytes_to_metadata(meta)
+    pr = R.SegmentReader(data, flen, decoder)
+    orr = P.SegmentReader(data, flen)
+    start, end = rows[1000][0], rows[1400][0]
+    got = pr.GetRange(start, end)
+    want = orr.GetRange(start, end)
+    assert [(r.Key, r.Value) for r in got] == [(r.Key, r.Value) for r in want]
+    io = pr.io_stats()
+    # the walks pick the blocks from the floor of start to the floor of end
+    keys = sorted(e.FirstKey for e in md.entries)
+    lo = max(i for i, k in enumerate(keys) if k <= start)
+    if keys[lo] == start and lo:  # the descending walk goes on past an equal key (:434)
+        lo -= 1
+    hi = max(i for i, k in enumerate(keys) if k <= end)
+    assert io["calls"] == 1 and io["blocks"] == hi - lo + 1
+    by_key = {e.FirstKey: e for e in md.entries}
+    span = by_key[keys[hi]].Offset + by_key[keys[hi]].BlockSize - by_key[keys[lo]].Offset
+    assert io["bytes_staged"] == span
+
+
+def _with_descs(data, meta, edit):
+    """The segment with its meta block rewritten: edit(i, BlockStat) changes
+    entries in place; the meta hash is recomputed so the metadata loads."""
+    import struct
+    from oracle import pyoracle as P
+    md = P.bytes_to_metadata(meta)
+    for i, st in enumerate(md.entries):
+        edit(i, st)
+    moff, = struct.unpack_from("<Q", data, len(data) - 25)
+    head_len = 2 + struct.unpack_from("<H", meta, 0)[0]
+    head_len += 2 + struct.unpack_from("<H", meta, head_len)[0]
+    head = meta[:head_len] + bytes([0, 0, 0]) + struct.pack("<Q", len(md.entries))
+    new_meta = head + b"".join(st.to_bytes() for st in md.entries)
+    seg = data[:moff] + new_meta
+    return seg + struct.pack("<QQBQ", moff, P.xxh64(new_meta), 1, P.MAGIC)
+
+
+def test_go_int_conversions_through_reader(decoder):
+    """Descriptors past Go's int() conversions (segment_reader.go:303-340):
+    a negative Offset is a Seek error, a BlockSize above the runtime's maxAlloc
+    (2^48) panics in make before any read, OriginalSize >= 2^63 walks no record
+    (nil rows, no error).  Product reader == oracle ReadBlockWithStat."""
+    from oracle import pyoracle as P
+    rows, data, flen, meta = _segment(nrows=400)
+    n = len(data)
+
+    def edit(i, st):
+        if i == 0:
+            st.OriginalSize = 1 << 63
+        elif i == 1:
+            st.OriginalSize = (1 << 64) - 1
+        elif i == 2:
+            st.BlockSize = (1 << 48) + 1
+        elif i == 3:
+            st.BlockSize = 1 << 63
+        elif i == 4:
+            st.BlockSize = 1 << 48  # allocatable: short read
+        elif i == 5:
+            st.Offset, st.BlockSize = n + 10, 1 << 50  # make panics before io.EOF
+        elif i == 6:
+            st.Offset = (1 << 63) + 5  # Seek error before the make panic
+            st.BlockSize = 1 << 60
+        elif i == 7:
+            st.Offset = n + 100  # io.EOF
+    seg = _with_descs(data, meta, edit)
+    md = P.bytes_to_metadata(seg[struct_off(seg):len(seg) - 25])
+    pr = R.SegmentReader(seg, len(seg), decoder)
+    tree = sorted(md.entries, key=lambda e: e.FirstKey)
+    assert pr.NumBlocks() == len(tree)
+    seen = set()
+    for i, st in enumerate(tree):
+        status, want = P.read_block(seg, st.desc(), P.COMP_NONE)
+        seen.add(status)
+        if status == P.BLK_OK:
+            got = pr.ReadBlock(i)
+            assert [(r.Key, r.Value) for r in (got or [])] == \
+                [(r.Key, r.Value) for r in (want or [])], i
+        elif status == P.BLK_PANIC:
+            with pytest.raises(R.GoPanic):
+                pr.ReadBlock(i)
+        else:
+            with pytest.raises(R.GoError) as e:
+                pr.ReadBlock(i)
+            assert e.value.kind == ("EOF" if status == P.BLK_EOF else "ErrUnexpectedBytesRead")
+    assert seen >= {P.BLK_OK, P.BLK_PANIC, P.BLK_EOF, P.BLK_SHORT}
+    # OriginalSize >= 2^63: no record walked, nil rows, no error
+    assert P.read_block(seg, md.entries[0].desc(), P.COMP_NONE) == (P.BLK_OK, None)
+    assert pr.ReadBlock([e.FirstKey for e in tree].index(md.entries[0].FirstKey)) is None
+
+
+def struct_off(seg):
+    import struct
+    return struct.unpack_from("<Q", seg, len(seg) - 25)[0]
+
+
+@pytest.mark.parametrize("nblk", [1, 4096, 65536])
+def test_getrow_on_large_segment_stages_one_block(decoder, nblk):
+    """GetRow on C3-shaped segments up to 65 536 x 64 KiB (4.3 GB, offsets past
+    4 GiB): one block staged, the row equals the writer's."""
+    from objectkv_amd import sst as S
+    w = S.synth_segment(1, 3, nblocks=nblk, threshold=57344, block_size=65536)
+    data = w.data()
+    pr = R.SegmentReader(data, len(data), decoder)
+    n = pr.NumBlocks()
+    last = pr.ReadBlock(n - 1)
+    io = pr.io_stats()
+    assert io["calls"] == 1 and io["blocks"] == 1 and io["bytes_staged"] == 65536
+    k = last[-1].Key
+    assert pr.GetRow(k).Key == k
+    assert pr.io_stats()["bytes_staged"] == 2 * 65536

@@ -153,3 +153,17 @@ def test_zstd_staged_equals_general_under_corruption(decoder, one_pass_decoder):
     assert staged.val_arena.tobytes() == general.val_arena.tobytes()
     # the flips must actually exercise both outcomes
     assert 0 < int((staged.status != 0).sum()) < len(dl)
+
+
+@pytest.mark.parametrize("case", ZC.past_original_cases(), ids=lambda c: c[0])
+def test_zstd_past_original_size(zdec, case):
+    """Frames that inflate past OriginalSize decode in full on the device (Go's
+    io.Copy, segment_reader.go:320-330) and walk to OriginalSize (:338-352);
+    OriginalSize >= 2^63 walks nothing (:340); blocks past Block_Maximum_Size
+    (RFC 8878 3.1.1.2.4) and windowLog > 31 fail.  No block ends at
+    OKV_BLK_CAPACITY; frames larger than their first output region take the
+    regrow pass (OKV_PATH_ZSTD_REGROW), the others do not."""
+    name, seg, descs, want, regrow = case
+    got = _check(zdec, seg, descs)
+    assert [int(x) for x in got.status] == want, name
+    assert bool(zdec.last_path() & okv._lib.PATH_ZSTD_REGROW) == regrow, name

@@ -37,7 +37,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s device-resident SST block decode + M rows/s, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_ROUND = "r3"  # profiles/<round>/pmc_<config>_<mode>.json (FETCH/WRITE_SIZE passes)
+PMC_ROUND = "r4"  # profiles/<round>/pmc_<config>_<mode>.json (FETCH/WRITE_SIZE passes)
 
 CONFIGS = {
     # name: (synth kind, seed, nblocks, threshold, block size, description)
@@ -156,6 +156,29 @@ def pmc_traffic(config, mode, kernel, sources=DECODE_SOURCES):
     if hits:  # per launch, summed over the kernels of the pass
         return sum(hits), os.path.relpath(path, ROOT)
     return None, None
+
+
+def trace_roofline(config, alg):
+    """The rocprofv3 kernel-trace average of the roofline kernel from
+    profiles/<PMC_ROUND>/trace_<config>.json (tools/trace_summary.py), and the
+    roofline fraction it implies for `alg` bytes -- attached only if the trace
+    was taken of the kernel sources being timed (same source_sha)."""
+    path = os.path.join(ROOT, "profiles", PMC_ROUND, f"trace_{config}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    if d.get("source_sha") != source_sha():
+        return {"source": os.path.relpath(path, ROOT),
+                "stale": "kernel sources changed since the trace"}
+    ms = d["avg_ns_timed"] / 1e6
+    out = {"kernel": d["kernel"], "avg_ms": round(ms, 4), "launches": d["timed_launches"],
+           "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "source": os.path.relpath(path, ROOT)}
+    if d.get("bench_event_ms_same_process"):
+        out["event_ms_same_process"] = round(d["bench_event_ms_same_process"], 4)
+        out["event_over_trace_same_process"] = round(d["bench_event_vs_trace"], 4)
+    return out
 
 
 # ---- process launch ---------------------------------------------------------------
@@ -531,7 +554,10 @@ def run_decode(args, torch, okv, D):
                      "algorithmic_bytes_per_launch": int(alg),
                      "timing": "HIP events around the kernel on its stream, averaged over a "
                                "second run of the same steps (the timed run carries no events)",
-                     "traffic_source": traffic_src, "decode_source_sha": source_sha()},
+                     "traffic_source": traffic_src, "decode_source_sha": source_sha(),
+                     # the same kernel's rocprofv3 trace average (another process, maybe
+                     # another box) and the event time the traced process measured itself
+                     "trace": None if comp else trace_roofline(args.config, alg)},
         "cpu_baseline": cpu,
         "verify": ver,
         "dist": D.info(),
@@ -703,9 +729,12 @@ def run_encode(args, torch, okv, D):
     achieved = alg / (ph["pack"] * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic("c4", "encode", "okv_enc_pack_lds_kernel", ENCODE_SOURCES)
 
+    # ---- CPU baseline (rank 0, after every rank's timing has finished) ------------
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         cpu = cpu_encode_baseline(args, rows, n, th, bs)
+        if world > 1:
+            cpu["sample"] += f"; run on rank 0 of {world} after the timed region"
 
     line = {
         "metric": ENC_METRIC, "value": round(data_bytes * world / t_step / 2**30, 3),

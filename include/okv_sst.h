@@ -381,6 +381,8 @@ int okv_profile_read(okv_ctx *ctx, double *ms, uint64_t *calls);
 #define OKV_PATH_BIG 64u    /* okv_copy_kernel / okv_index_kernel for big blocks (always
                                launched after a non-fused pass; exits when none) */
 #define OKV_PATH_ZSTD 128u  /* the zstd stage ran first */
+#define OKV_PATH_ENC_ONEPASS 512u /* okv_encode_rows: the single-pass plan (okv_enc_plan_kernel);
+                                     clear: the general E1-E9 kernels (a block > 256 rows) */
 #define OKV_PATH_ZSTD_REGROW 256u /* zstd frames outgrew their first output region and were
                                      measured and decoded again (io.Copy inflates them all) */
 uint32_t okv_last_path(const okv_ctx *ctx);

@@ -345,3 +345,32 @@ def test_bloom_pass_through(enc, decoder):
     dec = decoder.decode(want, md.descs)
     assert [(k, v or b"") for b in range(md.descs.shape[0]) for k, v in dec.block_rows(b)] == \
         [(k, v) for k, v in rows]
+
+
+@pytest.mark.parametrize("T,vmax,onepass", [(50, 60, True), (3584, 120, True),
+                                            (9000, 60, True), (20000, 12, False),
+                                            (3584, 3000, True)])
+def test_single_pass_plan_multi_chunk(enc, T, vmax, onepass):
+    """Segments of 9 000 - 30 000 rows (5 - 15 chunks of 2 048 rows) through the
+    single-pass plan (okv_enc_plan_kernel: per-chunk chain tables, look-back,
+    blocks emitted per chunk): byte-equal to the oracle writer.  Blocks of
+    more than 256 rows (T = 20 000 over ~26-byte records) take the general
+    kernels instead (OKV_PATH_ENC_ONEPASS clear), also byte-equal."""
+    rng = random.Random(T + vmax)
+    n = 30000 if vmax <= 120 else 9000
+    rows = _random_rows(rng, n, 8, vmax)
+    rc, want, meta = oracle_segment(rows, T, 4096)
+    strict = rc == 0
+    got = enc.encode(rows, T, 4096, strict_go=strict)
+    if strict:
+        assert got.seg.tobytes() == want and got.meta() == meta
+    else:  # the last row closed a block (Q1): compare with the host writer's footer
+        hw = okv.SegmentWriter(T, 4096, 0, False)
+        for k, v in rows:
+            hw.WriteRow(k, v)
+        hw.Close(strict_go=False)
+        assert got.seg.tobytes() == hw.data().tobytes()
+    assert bool(enc.last_path() & _lib.PATH_ENC_ONEPASS) == onepass
+    # a second encode reuses the per-block capacity and the look-back state (epochs)
+    got2 = enc.encode(rows, T, 4096, strict_go=strict)
+    assert got2.seg.tobytes() == got.seg.tobytes()

@@ -86,3 +86,61 @@ def test_c4_full_encode_vs_oracle():
         j = min(want.file.size, i + CHUNK)
         assert np.array_equal(seg_t[i:j].cpu().numpy(), want.file[i:j]), f"bytes {i}..{j}"
     enc.close()
+
+
+# ---- every rank's workload of the multi-GPU configs, on one GPU ---------------
+# (bench.py CONFIGS: C5 rank k decodes its own 16 384-block segment of seed 3 + k;
+# C4 at N GPUs encodes rows [100 M k / N, 100 M (k + 1) / N) of seed 1 as one segment)
+
+@pytest.mark.parametrize("rank", range(1, 8))
+def test_c5_rank_segment_vs_oracle(decoder, rank):
+    """C5 rank k's 1 GiB segment (16 384 x 64 KiB, seed 3 + k): every output
+    array equals the oracle's (rank 0's is the C3 prefix, covered above)."""
+    w = okv.synth_segment(okv.sst.SYNTH_ZIPF, 3 + rank, nblocks=16384, threshold=57344,
+                          block_size=65536)
+    seg = w.data_view()
+    d = w.descs()[:16384]
+    got = decoder.decode(seg, d)
+    ref = CO.decode_soa(seg, _oracle_descs(d))
+    assert int(got.status.max()) == 0
+    for k in ("status", "row_start", "key_base", "val_base", "key_off", "key_len", "val_off",
+              "val_len"):
+        assert _same(getattr(got, k), ref[k]), k
+    assert _same(got.key_arena, ref["key_arena"]), "key_arena"
+    assert _same(got.val_arena, ref["val_arena"]), "val_arena"
+
+
+@pytest.mark.parametrize("rank", [1, 7])
+def test_c4_key_range_shard_vs_oracle(rank):
+    """C4 at 8 GPUs: rank k's key-range shard (rows 12.5 M k .. 12.5 M (k + 1) - 1,
+    i.e. 87.5 M .. 99 999 999 for the last) encoded as its own segment: the
+    whole file equals the oracle writer's over the same rows."""
+    total, world, kl, vl = 100_000_000, 8, 16, 64
+    lo, hi = total * rank // world, total * (rank + 1) // world
+    n = hi - lo
+    enc = okv.Encoder(0)
+    dev = torch.device("cuda", 0)
+    t = dict(key_arena=torch.empty(n * kl, dtype=torch.uint8, device=dev),
+             key_off=torch.empty(n, dtype=torch.int64, device=dev),
+             key_len=torch.empty(n, dtype=torch.int16, device=dev),
+             val_arena=torch.empty(n * vl, dtype=torch.uint8, device=dev),
+             val_off=torch.empty(n, dtype=torch.int64, device=dev),
+             val_len=torch.empty(n, dtype=torch.int32, device=dev))
+    enc.synth_fixed_device(1, lo, n, kl, vl, t)
+    nb = -(-n // 42)
+    seg_t = torch.empty(nb * 4096 + (nb + 1) * (42 + kl) + 4096, dtype=torch.uint8, device=dev)
+    eo = enc.encode_device(t, n, {"seg": seg_t}, strict_go=True)
+    assert eo.n_blocks == nb and eo.data_bytes == nb * 4096
+    host = {k: v.cpu().numpy() for k, v in t.items()}
+    del t
+    for k, dt in (("key_off", np.uint64), ("val_off", np.uint64), ("key_len", np.uint16),
+                  ("val_len", np.uint32)):
+        host[k] = host[k].view(dt)
+    # the shard's first key is row lo's big-endian index
+    assert host["key_arena"][:kl].tobytes() == lo.to_bytes(kl, "big")
+    want = CO.encode_soa(host, n, 3584, 4096)
+    assert want.rc == 0 and eo.file_bytes == want.file.size
+    for i in range(0, want.file.size, CHUNK):
+        j = min(want.file.size, i + CHUNK)
+        assert np.array_equal(seg_t[i:j].cpu().numpy(), want.file[i:j]), f"bytes {i}..{j}"
+    enc.close()

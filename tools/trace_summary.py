@@ -4,14 +4,26 @@ roofline fraction the timed average implies.
 
 usage: python tools/trace_summary.py <run_kernel_trace.csv> <kernel substring>
            <untimed launches> <algorithmic bytes per launch> <out.json> [note]
+           [--sha <decode source sha>] [--bench-log <the traced bench's stdout/stderr>]
+
+--sha lets bench.py attach the trace to its roofline only while the kernel
+sources are the traced ones; --bench-log records the bench's own HIP-event
+time for the same kernel in the traced process (kernel_ms.copy of its JSON
+line), so event and trace timings are compared on one box and one process.
 """
 import csv
 import json
 import sys
 
-path, kern, skip, alg, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), \
-    sys.argv[5]
-note = sys.argv[6] if len(sys.argv) > 6 else ""
+argv = sys.argv[1:]
+opts = {}
+for flag in ("--sha", "--bench-log"):
+    if flag in argv:
+        i = argv.index(flag)
+        opts[flag] = argv[i + 1]
+        del argv[i:i + 2]
+path, kern, skip, alg, out = argv[0], argv[1], int(argv[2]), int(argv[3]), argv[4]
+note = argv[5] if len(argv) > 5 else ""
 rows = [r for r in csv.DictReader(open(path)) if kern in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ns = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
@@ -23,6 +35,17 @@ res = {"kernel": rows[0]["Kernel_Name"].split("(")[0] if rows else kern, "source
        "avg_ns_all": sum(ns) / len(ns), "per_launch_ns": ns,
        "algorithmic_bytes_per_launch": alg, "achieved_GB_s": alg / avg,
        "frac_of_8TB_s": alg / avg / 8000.0, "note": note}
+if "--sha" in opts:
+    res["source_sha"] = opts["--sha"]
+if "--bench-log" in opts:
+    line = None
+    for ln in open(opts["--bench-log"], errors="replace"):
+        if ln.startswith("{") and '"metric"' in ln:
+            line = json.loads(ln)
+    if line:
+        res["bench_event_ms_same_process"] = line.get("kernel_ms", {}).get("copy")
+        res["bench_event_vs_trace"] = (res["bench_event_ms_same_process"] * 1e6 / avg
+                                       if res["bench_event_ms_same_process"] else None)
 with open(out, "w") as f:
     json.dump(res, f, indent=1)
 print(out, json.dumps({k: res[k] for k in ("kernel", "timed_launches", "avg_ns_timed",

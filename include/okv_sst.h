@@ -179,7 +179,8 @@ int okv_decode_blocks(okv_ctx *ctx, const uint8_t *seg, uint64_t seg_bytes,
  * to each other, decoding alternate segments on their own streams, run each
  * decode's header walk (pass 1, latency-bound) under the other's pass 3,
  * while their pass-3 kernels never run concurrently.  after = NULL unchains.
- * Both contexts must be on the same device and stay open while chained.
+ * Both contexts must be on the same device and be driven from one host thread;
+ * okv_close of either unchains the pair.  The caller's current device is kept.
  */
 int okv_decode_chain(okv_ctx *ctx, okv_ctx *after);
 

@@ -60,6 +60,7 @@ struct okv_ctx {
   uint32_t last_path = 0;          // OKV_PATH_* of the last decode (okv_last_path)
   // okv_decode_chain: this context's pass 3 waits for chain's last pass 3
   okv_ctx* chain = nullptr;
+  std::vector<okv_ctx*> chained_by;  // contexts whose chain is this one (unchained at close)
   hipEvent_t p3_done = nullptr;    // recorded after every pass 3 once created
   bool p3_rec = false;             // p3_done has been recorded
   size_t f_cap = 0;

@@ -225,10 +225,13 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     lp[b] = e;
   }
   // Pass 2 in the same launch: the workgroup whose arrival is counted last
-  // scans the tile totals.  Hand-off (MI355X_MICROARCH.md, inter-workgroup
-  // visibility, row 1): one lane per workgroup stores its totals with sc1
-  // stores, drains them, then adds to one counter; the last adder (told by
-  // the value its add returns) reads every total with sc1 loads.
+  // scans the tile totals.  Hand-off: one lane per workgroup stores its totals
+  // with sc1 stores, drains them, then adds to one counter with release
+  // semantics; the last adder (told by the value its add returns) issues an
+  // agent-scope acquire and reads every total with sc1 loads.  (The sc1 form
+  // alone is the measured-valid row 1 of MI355X_MICROARCH.md's hand-off table;
+  // the release/acquire pair makes the ordering the memory model's, at one
+  // L2 write-back per workgroup and one invalidate in the last.)
   __shared__ uint32_t s_last;
   if (tid == kThreads - 1) {
     const Prefix t{inc[0] + v[0], inc[1] + v[1], inc[2] + v[2], inc[3] + v[3]};
@@ -245,8 +248,12 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
       __hip_atomic_store(&q->bad, t.bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint32_t a =
-          __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       s_last = a == gridDim.x - 1;
+      if (s_last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
   }
   __syncthreads();
@@ -586,405 +593,6 @@ __device__ __forceinline__ void sweep_handoff(const CopyParams& P, const GatherS
     P.vtile[x / kSwTile] = uint32_t(g);
 }
 
-// Pass 3: one workgroup per block reads the block straight from HBM.  NT = 64
-// (one wave per block) for small blocks, where a block has only a few 1 KiB
-// tiles and more blocks in flight hide the row-table -> gather latency chain;
-// NT = 256 otherwise.  The row table's header reads also pull the record
-// boundary lines on chip just before the key and value passes need them.
-template <int NT>
-__global__ __launch_bounds__(NT) void okv_gather_kernel(CopyParams P) {
-  __shared__ GatherSmem sm;
-  for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
-    const BlockMeta m = block_meta(P, b);
-    if (block_head(P, b, m)) {
-      const int rows = int(m.c.rows);
-      const GlobalWin src{P.seg, P.seg_bytes, m.off};
-      if (threadIdx.x < 64) {
-        const uint32_t t = threadIdx.x;
-        const uint32_t rec = int(t) < rows ? P.rt_pos[rec_index(P.nblk, b, t)] : 0u;
-        build_row_table(src, sm, rows, rec);
-      }
-      __syncthreads();
-      write_row_index(P, sm, m, rows);
-      if (!P.index_only) {
-        gather_region<false>(src, sm, rows, P.key_arena, m.B.kb0, threadIdx.x >> 6, NT / 64);
-        gather_region<true>(src, sm, rows, P.val_arena, m.B.vb0, threadIdx.x >> 6, NT / 64);
-      }
-    }
-    if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
-  }
-}
-
-// Pass 3a of the value sweep: one wave per block writes the row index and
-// the key region and hands the values to okv_value_sweep_kernel.  A latency
-// chain (metadata -> record positions -> headers -> keys), so it is sized for
-// occupancy: one window per lane in flight.  When the sweep is unsafe (big
-// blocks, capacity) it gathers the values itself.
-#ifdef OKV_ABLATE  // the round-2 row pass of the value sweep (ablation build only)
-__global__ __launch_bounds__(64) void okv_rows_kernel(CopyParams P) {
-  __shared__ GatherSmem sm;
-  // unsafe for the sweep (big blocks, capacity): okv_gather_staged_kernel,
-  // launched after the sweep, does the whole pass instead
-  if (!sweep_safe(*P.tot, *P.big_count, P.row_cap, P.key_cap, P.val_cap)) return;
-  for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
-    // record positions and headers with the metadata (one trip; the slots
-    // exist for every block, only the first `rows` are meaningful)
-    const uint32_t t = threadIdx.x;
-    const uint32_t rec = P.rt_pos[rec_index(P.nblk, b, t)];
-    const uint32_t kl = P.rt_kl ? P.rt_kl[rec_index(P.nblk, b, t)] : 0u;
-    const BlockMeta m = block_meta(P, b);
-    if (block_head(P, b, m)) {
-      const int rows = int(m.c.rows);
-      const GlobalWin src{P.seg, P.seg_bytes, m.off};
-      if (P.rt_kl) {
-        // value length from the next record's position (the walk's end after the last)
-        const bool live = int(t) < rows;
-        uint32_t nxt = __shfl_down(rec, 1, 64);
-        if (int(t) == rows - 1) nxt = uint32_t(m.c.pend);
-        fill_row_table(sm, rows, live ? rec : 0u, live ? kl : 0u,
-                       live ? nxt - rec - 6 - kl : 0u);
-      } else {
-        build_row_table(src, sm, rows, int(t) < rows ? rec : 0u);
-      }
-      __syncthreads();
-      write_row_index(P, sm, m, rows);
-      const uint4 bc = boundary_chunk(P, sm, m, rows);
-      gather_tiles<false, GlobalWin, 1>(src, sm, rows, P.key_arena, m.B.kb0, 0,
-                                        (sm.kpre[rows] + 1023) >> 10, 1);
-      sweep_handoff(P, sm, m, rows, bc);
-    }
-    if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
-  }
-}
-#endif
-
-// ---------------------------------------------------------------------------
-// Pass 3, wave-staged form (experimental, OKV_GATHER_STAGED=1): the value
-// region's tiles are produced from a per-wave LDS image of the iteration's
-// source span, filled by LDS-DMA (global_load_lds_dwordx4, no VGPR landing):
-// the loads in flight no longer cost registers, and a chunk's spill windows
-// come from the same image (no second trip).  Keys keep the global windows.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kStU = 5;                        // value tiles (1 KiB) per iteration
-template <uint32_t U> struct StCfg { static constexpr uint32_t cap = U * 1024 + 1024; };
-
-// Row holding region byte x (wave-uniform search over the LDS prefix).
-__device__ __forceinline__ uint32_t row_of(const uint32_t* pre, uint32_t last, uint32_t x) {
-  uint32_t pos = 0;
-#pragma unroll
-  for (uint32_t st = 32; st; st >>= 1) {
-    const uint32_t j = pos + st;
-    if (j <= last && pre[j] <= x) pos = j;
-  }
-  return pos;
-}
-
-// Tile t of a value region through global windows, for the rare tile whose
-// source span does not fit the stage (kept out of line: its registers would
-// otherwise size the whole kernel).
-__device__ __attribute__((noinline)) void gather_value_tile_global(const uint8_t* seg,
-                                                                   uint64_t seg_bytes,
-                                                                   uint64_t off,
-                                                                   const GatherSmem* sm, int rows,
-                                                                   uint8_t* arena, uint64_t dbase,
-                                                                   uint32_t t) {
-  const GlobalWin src{seg, seg_bytes, off};
-  gather_tiles<true, GlobalWin, 1>(src, *sm, rows, arena, dbase, t, t + 1, 1);
-}
-
-template <uint32_t U = kStU>
-__device__ __forceinline__ bool stage_span(const uint32_t* pre, const uint32_t* sb, uint32_t last,
-                                           int64_t off, uint32_t cbeg, uint32_t cend,
-                                           int64_t& A, int64_t& E, uint32_t& np) {
-  const uint32_t rb = row_of(pre, last, cbeg * 16), re = row_of(pre, last, cend * 16 - 1);
-  const int64_t s0 = off + int64_t(sb[rb]) + int64_t(cbeg) * 16;
-  const int64_t s1 = off + int64_t(sb[re]) + int64_t(cend) * 16;
-  A = (s0 & ~int64_t(15)) - 16;
-  E = ((s1 + 15) & ~int64_t(15)) + 16;
-  np = uint32_t((E - A + 1023) >> 10);
-  return A >= 0 && E - A <= int64_t(StCfg<U>::cap);
-}
-
-template <uint32_t kStU>
-__device__ __forceinline__ void gather_values_staged(const GlobalWin& src, const GatherSmem& sm,
-                                                     int rows, uint8_t* __restrict__ arena,
-                                                     uint64_t dbase, uint32_t t0, uint32_t t1,
-                                                     uint4* stage) {
-  const uint32_t* pre = sm.vpre;
-  const uint32_t* sb = sm.vsb;
-  const uint32_t N = (pre[rows] + 15) >> 4;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t last = uint32_t(rows) - 1;
-  const uint32_t climit = N < t1 * 64 ? N : t1 * 64;  // one past the wave's last chunk
-  const int64_t off = int64_t(src.off);
-  const uint64_t lim = round16(src.seg_bytes);
-  uint32_t r = 0;
-  bool searched = false;
-  for (uint32_t t = t0; t * 64 < climit;) {
-    // kStU tiles per iteration; a span too wide for the stage retries one
-    // tile, and a single tile too wide goes through global windows
-    uint32_t n = min(kStU, t1 - t);
-    uint32_t cbeg = t * 64, cend = min(climit, (t + n) * 64);
-    int64_t A, E;
-    uint32_t np;
-    bool ok = stage_span<kStU>(pre, sb, last, off, cbeg, cend, A, E, np);
-    if (!ok && n > 1) {
-      n = 1;
-      cend = min(climit, (t + 1) * 64);
-      ok = stage_span<kStU>(pre, sb, last, off, cbeg, cend, A, E, np);
-    }
-    if (!ok) {
-      gather_value_tile_global(src.seg, src.seg_bytes, src.off, &sm, rows, arena, dbase, t);
-      searched = false;
-      t += 1;
-      continue;
-    }
-    const uint64_t Eu = uint64_t(E) < lim ? uint64_t(E) : lim;
-    for (uint32_t p = 0; p < np; ++p) {
-      uint64_t a = uint64_t(A) + (uint64_t(p) << 10) + (lane << 4);
-      if (a + 16 > Eu) a = uint64_t(A);  // past the span or the segment: bytes never used
-      __builtin_amdgcn_global_load_lds(src.seg + a, OKV_LDS_PTR(stage + p * 64), 16, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (uint32_t u = 0; u < kStU; ++u) {
-      if (u >= n) break;
-      const uint32_t c = cbeg + u * 64 + lane;
-      const bool okc = c < cend;
-      const uint32_t x = (okc ? c : cend - 1) << 4, xe = x + 16;
-      if (!searched) {
-        r = row_of(pre, last, x);
-        searched = true;
-      } else {
-        while (r < last && pre[r + 1] <= x) ++r;
-      }
-      uint4 out = load16_lds_b128(stage, uint32_t(off + int64_t(sb[r]) + int64_t(x) - A));
-      if (okc) {
-        if (xe > pre[r + 1]) {
-          out = merge_bytes(make_uint4(0, 0, 0, 0), out, 0, int32_t(pre[r + 1] - x));
-          for (uint32_t j = r + 1; j <= last && pre[j] < xe; ++j) {
-            const uint32_t q0 = pre[j], q1 = pre[j + 1];
-            if (q1 == q0) continue;
-            const uint4 w =
-                load16_lds_b128(stage, uint32_t(off + int64_t(sb[j]) + int64_t(x) - A));
-            out = merge_bytes(out, w, int32_t(q0 - x), int32_t((q1 < xe ? q1 : xe) - x));
-          }
-        }
-        *reinterpret_cast<uint4*>(arena + dbase + uint64_t(x)) = out;
-      }
-    }
-    t += n;
-  }
-}
-
-template <int NT, uint32_t U = kStU>
-__global__ __launch_bounds__(NT) void okv_gather_staged_kernel(CopyParams P) {
-  __shared__ GatherSmem sm;
-  __shared__ uint4 stage[NT / 64][StCfg<U>::cap / 16 + 2];
-  // after the value sweep (P.vsrc set): only when the sweep was unsafe
-  if (P.vsrc && sweep_safe(*P.tot, *P.big_count, P.row_cap, P.key_cap, P.val_cap)) return;
-  for (uint32_t b = blockIdx.x; b < P.nblk; b += gridDim.x) {
-    const BlockMeta m = block_meta(P, b);
-    if (block_head(P, b, m)) {
-      const int rows = int(m.c.rows);
-      const GlobalWin src{P.seg, P.seg_bytes, m.off};
-      if (threadIdx.x < 64) {
-        const uint32_t t = threadIdx.x;
-        const uint32_t rec = int(t) < rows ? P.rt_pos[rec_index(P.nblk, b, t)] : 0u;
-        build_row_table(src, sm, rows, rec);
-      }
-      __syncthreads();
-      write_row_index(P, sm, m, rows);
-      const uint32_t wave = threadIdx.x >> 6;
-      const uint32_t Tk = (sm.kpre[rows] + 1023) >> 10;
-      gather_tiles<false, GlobalWin, 2>(src, sm, rows, P.key_arena, m.B.kb0,
-                                        uint32_t(uint64_t(Tk) * wave / (NT / 64)),
-                                        uint32_t(uint64_t(Tk) * (wave + 1) / (NT / 64)), 1);
-      const uint32_t T = (sm.vpre[rows] + 1023) >> 10;
-      gather_values_staged<U>(src, sm, rows, P.val_arena, m.B.vb0,
-                              uint32_t(uint64_t(T) * wave / (NT / 64)),
-                              uint32_t(uint64_t(T) * (wave + 1) / (NT / 64)), stage[wave]);
-    }
-    if (b + gridDim.x < P.nblk) __syncthreads();  // row table reused
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Pass 3b, value sweep: the value arena in address order, one short-lived
-// workgroup per kU x 4 KiB of destination (dispatch order = address order, so
-// the chip's loads and stores stay in one compact window of source and
-// destination -- the one-shot copy shape).  Lane l of tile t
-// produces the 16-byte chunk at X = 4096 t + 16 l: the owning row (the last
-// with val_off <= X) comes from the tile's rows [vtile[t], vtile[t + kU]],
-// staged in LDS; its bytes from two aligned 16-byte loads + the funnel; bytes
-// past its value from the following rows (val_off < X + 16); the rest zero.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kSwRows = 256;  // rows of a sweep workgroup held in LDS
-struct SweepParams {
-  const uint8_t* seg;
-  uint64_t seg_bytes;
-  const uint64_t* val_off;
-  const uint32_t* val_len;
-  const uint64_t* vsrc;
-  const uint32_t* vtile;
-  const uint4* bchunk;
-  uint8_t* val_arena;
-  const Totals* tot;
-  const uint32_t* big_count;
-  uint64_t row_cap, key_cap, val_cap;
-};
-
-// Rows of a sweep workgroup in LDS, relative to its first byte X0: value
-// start and end (clamped to +-2^30: only their order against chunk positions
-// in [0, kU x 4096) matters) and the source bias (segment position of arena
-// byte X = bias + X).
-struct SweepRows {
-  int32_t rel[kSwRows];
-  int32_t end[kSwRows];
-  int64_t bias[kSwRows];
-};
-__device__ __forceinline__ int32_t clamp_rel(int64_t v) {
-  return int32_t(v < -(int64_t(1) << 30) ? -(int64_t(1) << 30)
-                                         : (v > (int64_t(1) << 30) ? (int64_t(1) << 30) : v));
-}
-
-// Workgroups whose rows overflow the LDS window (tiny values): rows past the
-// window come from HBM.
-__device__ __noinline__ uint4 sweep_chunk_any(const uint8_t* seg, uint64_t seg_bytes,
-                                              const uint64_t* val_off, const uint32_t* val_len,
-                                              const uint64_t* vsrc, uint64_t r0, uint64_t r1,
-                                              uint64_t rows, uint64_t X) {
-  uint64_t lo = r0, hi = r1;  // invariant: val_off[lo] <= X
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi + 1) >> 1;
-    if (val_off[mid] <= X) lo = mid; else hi = mid - 1;
-  }
-  uint64_t k = lo;
-  uint64_t ko = val_off[k];
-  uint32_t kl = val_len[k];
-  const uint4 w = window16(seg, seg_bytes, int64_t(vsrc[k] + (X - ko)));
-  uint4 out = merge_bytes(make_uint4(0, 0, 0, 0), w, 0, int32_t(min<uint64_t>(16, ko + kl - X)));
-  for (++k; k < rows; ++k) {
-    ko = val_off[k];
-    if (ko >= X + 16) break;
-    kl = val_len[k];
-    if (kl == 0) continue;
-    const uint4 v = window16(seg, seg_bytes, int64_t(vsrc[k]) - int64_t(ko - X));
-    out = merge_bytes(out, v, int32_t(ko - X), int32_t(min<uint64_t>(16, ko + kl - X)));
-  }
-  return out;
-}
-
-template <uint32_t kU, bool kAl = false>
-__global__ __launch_bounds__(256) void okv_value_sweep_kernel(SweepParams S) {
-  __shared__ SweepRows R;
-  const uint64_t tile0 = uint64_t(blockIdx.x) * kU;
-  // one trip for every scalar: the totals, the big-block count and the two
-  // tile entries (tile0 + kU <= tiles launched + 1: inside the table)
-  const Totals T = *S.tot;
-  const uint32_t nbig = *S.big_count;
-  const uint32_t e0 = S.vtile[tile0], e1 = S.vtile[tile0 + kU];
-  if (!sweep_safe(T, nbig, S.row_cap, S.key_cap, S.val_cap)) return;
-  const uint64_t X0 = tile0 * kSwTile;
-  if (X0 >= T.vb) return;
-  const uint64_t ntile = (T.vb + kSwTile - 1) / kSwTile;
-  // rows [r0, r1] cover the workgroup's bytes; r1 + 1 ends the last spill
-  // check.  (Clamped into [0, rows): every index stays inside the row arrays
-  // whatever the table holds.)
-  const uint64_t r0 = min<uint64_t>(e0, T.rows - 1);
-  const uint64_t r1 =
-      tile0 + kU < ntile ? min<uint64_t>(max<uint64_t>(e1, r0), T.rows - 1) : T.rows - 1;
-  const uint64_t rend = min<uint64_t>(r1 + 1, T.rows - 1);
-  const bool full = rend - r0 + 1 <= kSwRows;  // uniform
-  const uint32_t nw = uint32_t(min<uint64_t>(rend - r0 + 1, kSwRows));
-  const uint32_t tid = threadIdx.x;
-  if (tid < nw) {
-    const int64_t off = int64_t(S.val_off[r0 + tid]);
-    const uint32_t len = S.val_len[r0 + tid];
-    const int64_t src = int64_t(S.vsrc[r0 + tid]);
-    R.rel[tid] = clamp_rel(off - int64_t(X0));
-    R.end[tid] = clamp_rel(off + int64_t(len) - int64_t(X0));
-    R.bias[tid] = src - off;
-  }
-  __syncthreads();
-  uint4 out[kU];
-  bool put[kU];
-  uint4 nxt[kU];        // kAl: the next aligned line, where this lane loads it
-  uint32_t sft[kU];     // kAl: byte offset of the chunk in its line (0: no funnel)
-  bool own[kU];
-#pragma unroll
-  for (uint32_t u = 0; u < kU; ++u) {
-    sft[u] = 0;
-    own[u] = false;
-    nxt[u] = make_uint4(0, 0, 0, 0);
-  }
-  // every load issued before any is used
-#pragma unroll
-  for (uint32_t u = 0; u < kU; ++u) {
-    const int32_t xr = int32_t(u * kSwTile + 16u * tid);
-    const uint64_t X = X0 + uint32_t(xr);
-    out[u] = make_uint4(0, 0, 0, 0);
-    put[u] = X < T.vb;
-    if (!full || !put[u]) continue;
-    // owner: last local row with rel <= xr (rel is non-decreasing)
-    uint32_t o = 0;
-    if (nw <= 8) {
-      for (uint32_t j = 1; j < nw; ++j) o = R.rel[j] <= xr ? j : o;
-    } else {
-      uint32_t hi = nw - 1;
-      while (o < hi) {
-        const uint32_t mid = (o + hi + 1) >> 1;
-        if (R.rel[mid] <= xr) o = mid; else hi = mid - 1;
-      }
-    }
-    // one unaligned 16-byte load inside the owner's value, or the owner's
-    // boundary chunk (okv_rows_kernel).  kAl: the aligned line holding the
-    // chunk's first byte; the next line comes from lane + 1 (the next chunk of
-    // the same row) by a shuffle, or is loaded here when that lane holds no
-    // such chunk (lane 63, the row's last whole chunk)
-    const bool whole = xr + 16 <= R.end[o];
-    if constexpr (kAl) {
-      const int64_t src = R.bias[o] + int64_t(X);
-      sft[u] = whole ? uint32_t(src & 15) : 0u;
-      own[u] = whole && sft[u] && ((tid & 63) == 63 || xr + 32 > R.end[o]);
-      if (whole) {
-        const uint4* line = reinterpret_cast<const uint4*>(S.seg + (src & ~int64_t(15)));
-        out[u] = line[0];
-        if (own[u]) nxt[u] = line[1];
-      } else {
-        out[u] = S.bchunk[r0 + o];
-      }
-    } else {
-      if (whole)
-        out[u] = *reinterpret_cast<const uint4*>(S.seg + (R.bias[o] + int64_t(X)));
-      else
-        out[u] = S.bchunk[r0 + o];
-    }
-  }
-  if constexpr (kAl) {
-#pragma unroll
-    for (uint32_t u = 0; u < kU; ++u) {
-      const uint4 nb = make_uint4(__shfl_down(out[u].x, 1, 64), __shfl_down(out[u].y, 1, 64),
-                                  __shfl_down(out[u].z, 1, 64), __shfl_down(out[u].w, 1, 64));
-      if (sft[u]) out[u] = funnel32(out[u], own[u] ? nxt[u] : nb, sft[u]);
-    }
-  }
-  if (!full) {
-#pragma unroll
-    for (uint32_t u = 0; u < kU; ++u) {
-      const uint64_t X = X0 + uint64_t(u) * kSwTile + 16u * tid;
-      if (put[u])
-        out[u] = sweep_chunk_any(S.seg, S.seg_bytes, S.val_off, S.val_len, S.vsrc, r0, r1, T.rows,
-                                 X);
-    }
-  }
-#pragma unroll
-  for (uint32_t u = 0; u < kU; ++u) {
-    const uint64_t X = X0 + uint64_t(u) * kSwTile + 16u * tid;
-    if (put[u]) *reinterpret_cast<uint4*>(S.val_arena + X) = out[u];
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Pass 3, source tiles (large blocks).  Block b is cut into
 // tiles of kT source bytes, tile t = block bytes [t kT, (t + 1) kT), one
@@ -1060,26 +668,18 @@ __device__ __noinline__ uint4 tile_chunk_pieces(const uint8_t* seg, uint64_t seg
   return out;
 }
 
-template <uint32_t kT, uint32_t kNT, bool kXcd, int kDiag>
+// (The measured alternatives -- other tile sizes and widths, phase probes,
+// per-chunk lookups, direct global loads -- are tile_pass_diag in
+// okv_decode_ablate.inc, ablation build only.)
+template <uint32_t kT, uint32_t kNT, bool kXcd>
 __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uint32_t ntile) {
-  // kDiag: 0 the product form (value runs); ablation arms: 1 no chunk pass,
-  // 2 no DMA, 3 phase probe of the per-chunk form, 4 (+ no stores), 5 (+ no
-  // data reads), 6 direct unaligned global loads, 7 phase probe of the product
-  // form, 8 the per-chunk form (every chunk looked up per lane); 9 (a launch
-  // choice) the product form without the 8-waves register cap
-  constexpr bool kDirect = kDiag == 6;  // no LDS stage: one unaligned global load per chunk
-  constexpr bool kChunk = (kDiag >= 3 && kDiag <= 5) || kDiag == 8;
-  constexpr bool kRuns = !kChunk && !kDirect;
-  constexpr bool kProbe = (kDiag >= 3 && kDiag <= 5) || kDiag == 7;
-  constexpr uint32_t kG = kT / 64 + 8;  // 64-byte destination granules per region table
+  constexpr uint32_t kG = kT / 64 + 8;  // 64-byte destination granules of the key range
   __shared__ TileRows R;
-  __shared__ uint8_t gt[2][kG];         // row holding byte max(64 g, range start)
+  __shared__ uint8_t gt[1][kG];         // row holding key byte max(64 g, range start)
   __shared__ uint4 stage[kT / 16 + 4];
   uint32_t L = blockIdx.x;
   if constexpr (kXcd) L = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
   if (L >= ntile) return;
-  uint64_t T[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // kProbe: phase timestamps (sampled workgroups)
-  if constexpr (kProbe) T[0] = __builtin_amdgcn_s_memrealtime();
   // uniform block index (an SGPR: the loads below are scalar, all in one trip)
   const uint32_t b = __builtin_amdgcn_readfirstlane(L / tpb);
   const uint32_t t = L - b * tpb;
@@ -1098,7 +698,6 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
   asm volatile("" ::"s"(off), "s"(c.rows), "s"(c.kbytes), "s"(c.vbytes), "s"(c.pend),
                "s"(c.status), "s"(lpre.rows), "s"(lpre.kb), "s"(lpre.vb), "s"(tpre.rows),
                "s"(tpre.kb), "s"(tpre.vb));
-  if constexpr (kProbe) T[1] = __builtin_amdgcn_s_memrealtime();
   const uint64_t row0 = tpre.rows + lpre.rows, kb0 = tpre.kb + lpre.kb, vb0 = tpre.vb + lpre.vb;
   const bool fits = row0 + c.rows <= P.row_cap &&
                     (P.index_only ||
@@ -1136,7 +735,7 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
   // Waves 1.. issue the DMA; wave 0 builds the row table meanwhile.  (With a
   // share of the DMA in flight, wave 0's LDS row-table writes would wait for
   // it: the compiler cannot tell them apart from the DMA's LDS target.)
-  if (!P.index_only && kDiag != 2 && !kDirect && tid >= 64) {
+  if (!P.index_only && tid >= 64) {
     const int64_t lim = int64_t(round16(P.seg_bytes));
     const uint32_t u = tid - 64;
     for (uint32_t k0 = 0; k0 < np; k0 += kNT - 64) {
@@ -1149,7 +748,6 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
       }
     }
   }
-  if constexpr (kProbe) T[2] = __builtin_amdgcn_s_memrealtime();
   // row table (wave 0, lane r = row r) while the tile is in flight
   if (tid < 64) {
     const bool live = lane < rows;
@@ -1196,12 +794,11 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
         R.x[2] = X[2];
         R.x[3] = X[3];
       }
-      // granule tables: gt[reg][g - (X0 >> 6)] = row holding byte max(64 g, X0);
-      // granules past the last row's bytes (padding) keep the preset lastr.
-      // The value-run form needs the key table only (its boundary chunks carry
-      // their row): a 4 KiB value is 64 granules, a serial per-lane loop.
+      // granule table of the key range: gt[0][g - (X0 >> 6)] = row holding byte
+      // max(64 g, X0); granules past the last row's bytes (padding) keep the
+      // preset lastr.  Values need none: their boundary chunks carry their row.
 #pragma unroll
-      for (uint32_t reg = 0; reg < (kRuns ? 1u : 2u); ++reg) {
+      for (uint32_t reg = 0; reg < 1u; ++reg) {
         const uint32_t X0 = X[2 * reg], X1 = X[2 * reg + 1];
         if (X1 <= X0) continue;
         const uint32_t g0 = X0 >> 6, gl = (X1 - 1) >> 6;
@@ -1214,7 +811,7 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
           for (uint32_t g = gs; g <= ge; ++g) gt[reg][g - g0] = uint8_t(lane);
         }
       }
-      if constexpr (kRuns) {
+      {
         // row pieces of the owned value range: [a, e) = row r's bytes in [X2, X3)
         const uint32_t X2 = X[2], X3 = X[3];
         const uint32_t a = max(vp, X2), e = min(vp + v, X3);
@@ -1260,7 +857,6 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
       P.val_off[g] = off + vs;
     }
   }
-  if constexpr (kProbe) T[3] = __builtin_amdgcn_s_memrealtime();
   if (P.index_only) {
     block_outputs();
     return;
@@ -1269,7 +865,6 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
   // on their own)
   if (tid >= 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (kProbe) T[4] = __builtin_amdgcn_s_memrealtime();
   if (t == 0 && tid < 64) {  // the block outputs and SoA row index (from the LDS tables)
     block_outputs();
     if (lane < rows) {
@@ -1283,10 +878,8 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
   }
   const uint32_t kx0 = R.x[0], kx1 = R.x[1], vx0 = R.x[2], vx1 = R.x[3];
   const uint32_t nk = kx1 > kx0 ? ((kx1 + 15) >> 4) - (kx0 >> 4) : 0u;
-  const uint32_t nv = vx1 > vx0 ? ((vx1 + 15) >> 4) - (vx0 >> 4) : 0u;
   const uint32_t sbias = uint32_t(int64_t(off) - A);  // stage byte of block position s: s + sbias
-  if (kDiag == 1) return;  // diagnostic: metadata + DMA + row table only
-  if constexpr (kRuns) {
+  {
     // value runs: one unit of <= 64 whole chunks of one row per wave iteration
     const uint32_t nunit = R.nunit, nbnd = R.nbnd;
     uint8_t* const varena = P.val_arena + vb0;
@@ -1328,114 +921,21 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
       else
         store_partial(dst, out, lo - x, hi - x);
     }
-  } else if constexpr (kDirect) {
-    constexpr uint32_t kU = (kT / 16 + 8 + kNT - 1) / kNT;  // chunk slots per lane
-    uint4 v[kU];
-    uint32_t xs[kU], los[kU], his[kU], regs[kU];
-    bool slow[kU];
-#pragma unroll
-    for (uint32_t u = 0; u < kU; ++u) {  // every load issued before any store
-      const uint32_t j = tid + u * kNT;
-      his[u] = 0;
-      los[u] = 0;
-      slow[u] = false;
-      v[u] = make_uint4(0, 0, 0, 0);
-      if (j >= nk + nv) continue;
-      const uint32_t reg = j >= nk;
-      const uint32_t X0 = reg ? vx0 : kx0, X1 = reg ? vx1 : kx1;
-      const uint32_t x = ((X0 >> 4) + (reg ? j - nk : j)) << 4;
-      const uint32_t lo = max(x, X0), hi = min(x + 16, X1);
-      const uint32_t* pre = R.pre[reg];
-      uint32_t r = gt[reg][(lo >> 6) - (X0 >> 6)];
-      while (r < lastr && pre[r + 1] <= lo) ++r;
-      xs[u] = x;
-      los[u] = lo;
-      his[u] = hi;
-      regs[u] = reg | (r << 1);
-      if (lo == x && hi == x + 16 && pre[r + 1] >= x + 16)
-        v[u] = *reinterpret_cast<const uint4*>(P.seg + off + R.sb[reg][r] + x);
-      else
-        slow[u] = true;
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kU; ++u)
-      if (slow[u])
-        v[u] = tile_chunk_pieces(P.seg, P.seg_bytes, off, R.pre[regs[u] & 1], R.sb[regs[u] & 1],
-                                 rows, regs[u] >> 1, xs[u], los[u], his[u]);
-#pragma unroll
-    for (uint32_t u = 0; u < kU; ++u) {
-      if (his[u] <= los[u]) continue;
-      uint8_t* dst = ((regs[u] & 1) ? P.val_arena + vb0 : P.key_arena + kb0) + xs[u];
-      if (los[u] == xs[u] && his[u] == xs[u] + 16)
-        *reinterpret_cast<uint4*>(dst) = v[u];
-      else
-        store_partial(dst, v[u], los[u] - xs[u], his[u] - xs[u]);
-    }
-  } else
-  for (uint32_t j = tid; j < nk + nv; j += kNT) {
-    const uint32_t reg = j >= nk;
-    const uint32_t X0 = reg ? vx0 : kx0, X1 = reg ? vx1 : kx1;
-    const uint32_t x = ((X0 >> 4) + (reg ? j - nk : j)) << 4;
-    const uint32_t lo = max(x, X0), hi = min(x + 16, X1);
-    const uint32_t* pre = R.pre[reg];
-    const uint32_t* sb = R.sb[reg];
-    uint32_t r = gt[reg][(lo >> 6) - (X0 >> 6)];
-    while (r < lastr && pre[r + 1] <= lo) ++r;
-    uint8_t* dst = (reg ? P.val_arena + vb0 : P.key_arena + kb0) + x;
-    if (lo == x && hi == x + 16 && pre[r + 1] >= x + 16) {  // the common chunk: inside row r
-      if constexpr (kDiag == 5) {  // diagnostic: the lookup, no data read
-        *reinterpret_cast<uint4*>(dst) = make_uint4(r, x, 0, 0);
-        continue;
-      }
-      const uint4 w = load16_lds_b128(stage, sb[r] + x + sbias);
-      if constexpr (kDiag == 4) {  // diagnostic: no stores
-        asm volatile("" ::"v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));
-        continue;
-      }
-      *reinterpret_cast<uint4*>(dst) = w;
-      continue;
-    }
-    const uint32_t dend = min(hi, pre[rows]);
-    uint4 out = make_uint4(0, 0, 0, 0);
-    for (uint32_t d = lo; d < dend; ++r) {
-      const uint32_t e = min(dend, pre[r + 1]);
-      if (e > d) {  // bytes [d, e) of the chunk from row r
-        out = merge_bytes(out, load16_lds_b128(stage, sb[r] + x + sbias), int32_t(d - x),
-                          int32_t(e - x));
-        d = e;
-      }
-    }
-    if (lo == x && hi == x + 16)
-      *reinterpret_cast<uint4*>(dst) = out;
-    else
-      store_partial(dst, out, lo - x, hi - x);
-  }
-  if constexpr (kProbe) {
-    T[5] = __builtin_amdgcn_s_memrealtime();
-    __syncthreads();
-    T[6] = __builtin_amdgcn_s_memrealtime();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    T[7] = __builtin_amdgcn_s_memrealtime();
-    if ((L & 255) == 0 && tid == 0)
-      for (int k = 0; k < 8; ++k) P.vsrc[(L >> 8) * 8 + k] = T[k];
   }
 }
 
-// The product form runs 8 waves per SIMD (8 workgroups per CU: the LDS
-// bound; registers capped at 64 per lane, no spills); the ablation build also
-// has the uncapped form (70 registers, 7 waves per SIMD) as arm d9.
-template <uint32_t kT, uint32_t kNT, bool kXcd, int kDiag = 0>
+// 8 waves per SIMD (8 workgroups per CU: the LDS bound; registers capped at
+// 64 per lane, no spills; the uncapped form measured equal).
+template <uint32_t kT, uint32_t kNT, bool kXcd>
 __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kT <= 16384 ? 8 : 4))) void okv_tile_kernel(
     CopyParams P, uint32_t tpb, uint32_t ntile) {
-  tile_pass<kT, kNT, kXcd, kDiag>(P, tpb, ntile);
+  tile_pass<kT, kNT, kXcd>(P, tpb, ntile);
 }
-#ifdef OKV_ABLATE
-template <uint32_t kT, uint32_t kNT, bool kXcd>
-__global__ __launch_bounds__(kNT) void okv_tile_kernel_w7(CopyParams P, uint32_t tpb,
-                                                          uint32_t ntile) {
-  tile_pass<kT, kNT, kXcd, 0>(P, tpb, ntile);
-}
+
+#ifdef OKV_ABLATE  // the measured alternative pass-3 forms (ablation build only)
+#include "okv_decode_ablate.inc"
 #endif
+
 
 // Pass 3, small-block staged form (blocks averaging <= 16 KiB, e.g. 4 KiB
 // blocks): one wave per block DMAs the whole block into its LDS stage right
@@ -2255,9 +1755,12 @@ void launch_tile_t(hipStream_t s, const CopyParams& P, uint32_t tpb, uint32_t nt
                        ntile);
     return;
   }
+  hipLaunchKernelGGL((okv_tile_kernel_diag<kT, kNT, kXcd, kDiag>), dim3(grid), dim3(kNT), 0, s, P,
+                     tpb, ntile);
+#else
+  static_assert(kDiag == 0, "the product library has no diagnostic arms");
+  hipLaunchKernelGGL((okv_tile_kernel<kT, kNT, kXcd>), dim3(grid), dim3(kNT), 0, s, P, tpb, ntile);
 #endif
-  hipLaunchKernelGGL((okv_tile_kernel<kT, kNT, kXcd, kDiag>), dim3(grid), dim3(kNT), 0, s, P, tpb,
-                     ntile);
 }
 typedef void (*TileLaunch)(hipStream_t, const CopyParams&, uint32_t, uint32_t);
 struct TileForm {
@@ -2715,6 +2218,13 @@ void okv_close(okv_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  // unchain: contexts that wait on this one, and the one this one waits on
+  for (okv_ctx* c : ctx->chained_by)
+    if (c->chain == ctx) c->chain = nullptr;
+  if (ctx->chain) {
+    auto& v = ctx->chain->chained_by;
+    v.erase(std::remove(v.begin(), v.end(), ctx), v.end());
+  }
   (void)hipFree(ctx->d_cnt);
   (void)hipFree(ctx->d_lp);
   (void)hipFree(ctx->d_tile_tot);
@@ -2758,16 +2268,31 @@ void okv_close(okv_ctx* ctx) {
 const char* okv_last_error(const okv_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
 void* okv_stream(const okv_ctx* ctx) { return ctx ? ctx->stream : nullptr; }
 
+// Chained contexts are driven from one host thread (as every okv_ctx: not
+// thread safe); okv_close unchains both directions, so neither context keeps
+// a pointer to a closed one.
 int okv_decode_chain(okv_ctx* ctx, okv_ctx* after) {
   if (!ctx || after == ctx || (after && after->device != ctx->device))
     return set_err(ctx, OKV_E_ARG, "okv_decode_chain: contexts");
+  int prev = -1;
+  OKV_HIP(hipGetDevice(&prev));
   for (okv_ctx* c : {ctx, after}) {
     if (c && !c->p3_done) {
       OKV_HIP(hipSetDevice(c->device));
-      OKV_HIP(hipEventCreateWithFlags(&c->p3_done, hipEventDisableTiming));
+      const hipError_t e = hipEventCreateWithFlags(&c->p3_done, hipEventDisableTiming);
+      if (e != hipSuccess) {
+        (void)hipSetDevice(prev);
+        return set_err(ctx, OKV_E_HIP, "okv_decode_chain: event", e);
+      }
     }
   }
+  OKV_HIP(hipSetDevice(prev));  // the caller's current device is left as it was
+  if (ctx->chain) {
+    auto& v = ctx->chain->chained_by;
+    v.erase(std::remove(v.begin(), v.end(), ctx), v.end());
+  }
   ctx->chain = after;
+  if (after) after->chained_by.push_back(ctx);
   return OKV_OK;
 }
 

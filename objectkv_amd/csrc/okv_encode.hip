@@ -2078,6 +2078,7 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   const bool lds = aligned && GL >= 1 && pl.avg_rec <= 512;
   int rc;
 #ifdef OKV_ABLATE
+  (void)lds;
   if ((rc = enc_row_prefix(ctx, e, R, o.threshold_bytes))) return rc;  // any arm may read it
 #else
   if (!lds && (rc = enc_row_prefix(ctx, e, R, o.threshold_bytes))) return rc;

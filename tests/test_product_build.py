@@ -17,7 +17,8 @@ ABLATE = os.path.join(ROOT, "objectkv_amd", "libokv_sst_ablate.so")
 
 # kernels of the measured alternative forms: ablation build only
 ABLATION_ONLY = [b"okv_value_sweep_kernel", b"okv_rows_kernel", b"okv_gather_staged_kernel",
-                 b"okv_gather_kernel", b"okv_tile_kernel_w7", b"okv_scan_kernel"]
+                 b"okv_gather_kernel", b"okv_tile_kernel_w7", b"okv_scan_kernel",
+                 b"okv_tile_kernel_diag"]
 KNOBS = [b"OKV_GATHER_THREADS", b"OKV_GATHER_GRID", b"OKV_DECODE_FUSED", b"OKV_GATHER_STAGED",
          b"OKV_VALUE_SWEEP", b"OKV_TILE", b"OKV_ZSTD_GENERAL", b"OKV_ZSTD_PROF",
          b"OKV_ENC_VARIANT", b"OKV_ENC_IMAGE"]
@@ -33,7 +34,7 @@ def _bytes(path):
 def test_product_ships_one_tile_pass_form():
     data = _bytes(PRODUCT)
     forms = set(re.findall(rb"_ZN3okv15okv_tile_kernelI[A-Za-z0-9_]+", data))
-    assert forms == {b"_ZN3okv15okv_tile_kernelILj16384ELj256ELb1ELi0EEEvNS_10CopyParamsEjj"}, forms
+    assert forms == {b"_ZN3okv15okv_tile_kernelILj16384ELj256ELb1EEEvNS_10CopyParamsEjj"}, forms
     for name in ABLATION_ONLY:
         assert name not in data, name
     # the shipping kernels are all there
@@ -42,6 +43,20 @@ def test_product_ships_one_tile_pass_form():
                  b"okv_enc_pack_lds_kernel", b"okv_zstd_seq_kernel", b"okv_zstd_exec_kernel",
                  b"okv_merge_rank"):
         assert name in data, name
+
+
+def test_product_source_holds_only_product_kernels():
+    """The shipped source is the shipped code: the measured alternatives and
+    the tile pass's diagnostic arms live in okv_decode_ablate.inc, which
+    okv_decode.hip includes only under -DOKV_ABLATE."""
+    src = open(os.path.join(ROOT, "objectkv_amd", "csrc", "okv_decode.hip")).read()
+    for name in ("okv_value_sweep_kernel", "okv_rows_kernel", "okv_gather_staged_kernel",
+                 "okv_gather_kernel", "tile_pass_diag", "okv_tile_kernel_diag"):
+        assert not re.search(r"void\s+" + name + r"\s*\(", src), name
+    for arm in ("kProbe", "kDirect", "kChunk", "kDiag == 1", "kDiag == 4", "kDiag == 5"):
+        assert arm not in src, arm
+    inc = src.index('#include "okv_decode_ablate.inc"')
+    assert src.rfind("#ifdef OKV_ABLATE", 0, inc) > src.rfind("#endif", 0, inc)
 
 
 def test_product_reads_no_environment():

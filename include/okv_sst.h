@@ -136,6 +136,9 @@ okv_ctx *okv_open_on_stream(int device, void *stream);
 #define OKV_OPEN_ZSTD_ONE_PASS 2u /* zstd blocks: the one-wave-per-block decoder for every block
                                      (one launch, no host synchronisation between stages: lower
                                      latency for a few blocks); outputs identical */
+#define OKV_OPEN_NO_PIECES 4u     /* large-block decodes (>= 8192 blocks) as one header walk and
+                                     one tile pass, instead of two pieces whose second walk runs on
+                                     a second stream under the first tile pass; outputs identical */
 typedef struct okv_open_opts {
   uint32_t size;  /* sizeof(okv_open_opts) */
   uint32_t flags; /* OKV_OPEN_* */

@@ -77,7 +77,8 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count,
     const int32_t* __restrict__ pre_status, int prefetch, uint64_t span_cap,
     Prefix* __restrict__ tile_pre, Totals* __restrict__ tot, uint64_t* __restrict__ row_start,
-    uint32_t* __restrict__ arrive, uint32_t* __restrict__ big_zero) {
+    uint32_t* __restrict__ arrive, uint32_t* __restrict__ big_zero,
+    const Totals* __restrict__ base, uint32_t bidx0) {
   // slots of the current chunk: positions [lane][kRecChunk + 1] (odd stride:
   // the walking lanes' stores hit distinct banks), key lengths [lane][kRecChunk]
   __shared__ uint32_t s_pos[kThreads * (kRecChunk + 1)];
@@ -89,7 +90,7 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
   int32_t st = OKV_BLK_OK;
   // the other big-block counter slot, for the next launch (its readers, the
   // previous decode's kernels, have completed: stream order)
-  if (blockIdx.x == 0 && tid == 0) *big_zero = 0;
+  if (blockIdx.x == 0 && tid == 0 && big_zero) *big_zero = 0;
   uint64_t len = 0, orig = 0, off = 0;
   bool walking = false;
   if (b < nblk) {
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
   if (b < nblk) {
     if (st != OKV_BLK_OK) rows = kb = vb = 0;
     if (st == OKV_BLK_OK && (rows > kRCap || p >= (uint64_t(1) << 32) || p > span_cap))
-      big_list[atomicAdd(big_count, 1u)] = b;  // staged path (okv_copy_kernel)
+      big_list[atomicAdd(big_count, 1u)] = bidx0 + b;  // staged path (okv_copy_kernel)
     BlockCount c;
     c.rows = rows;
     c.kbytes = kb;
@@ -236,9 +237,10 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
   if (tid == kThreads - 1) {
     const Prefix t{inc[0] + v[0], inc[1] + v[1], inc[2] + v[2], inc[3] + v[3]};
     if (gridDim.x == 1) {
-      *tile_pre = Prefix{0, 0, 0, 0};
-      *tot = Totals{t.rows, t.kb, t.vb, t.bad};
-      if (row_start) row_start[nblk] = t.rows;
+      const Totals b0 = base ? *base : Totals{0, 0, 0, 0};
+      *tile_pre = Prefix{b0.rows, b0.kb, b0.vb, b0.bad};
+      *tot = Totals{b0.rows + t.rows, b0.kb + t.kb, b0.vb + t.vb, b0.bad + t.bad};
+      if (row_start) row_start[nblk] = b0.rows + t.rows;
       s_last = 0;
     } else {
       Prefix* q = tile_tot + blockIdx.x;
@@ -259,7 +261,14 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
   __syncthreads();
   if (!s_last) return;
   // the last workgroup: exclusive scan of gridDim.x tile totals, 256 at a time
+  // (from the totals of the blocks before this launch's, for a decode in pieces)
   uint64_t carry[4] = {0, 0, 0, 0};
+  if (base) {
+    carry[0] = base->rows;
+    carry[1] = base->kb;
+    carry[2] = base->vb;
+    carry[3] = base->bad;
+  }
   for (uint32_t base = 0; base < gridDim.x; base += kThreads) {
     const uint32_t i = base + tid;
     uint64_t x[4] = {0, 0, 0, 0};
@@ -1717,7 +1726,7 @@ int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_star
                      w.seg_bytes, w.descs, nblk, w.comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
                      ctx->d_rec, rt_kl, ctx->d_big, big_counter(ctx), w.pre, prefetch, span_cap,
                      ctx->d_tile_pre, ctx->d_tot, d_row_start, ctx->d_ctr + kCtrArrive,
-                     big_counter(ctx, 1));
+                     big_counter(ctx, 1), nullptr, 0u);
   OKV_HIP(hipGetLastError());
   ctx->big_slot ^= 1u;  // the launch zeroes the other slot: the next launch's counter
   if (timed) {
@@ -1829,6 +1838,80 @@ int ensure_fused(okv_ctx* ctx, uint32_t nblk) {
   return OKV_OK;
 }
 
+// Large-block decodes run in two pieces: the header walk of the first
+// kPieceDiv-th of the blocks, then the tile pass over them on the context's
+// stream while the second piece's walk runs on a second stream; the second
+// tile pass waits for that walk.  The walk is latency-bound (a dependent
+// chain per block, ~0.09 ms at C3 whatever the block count), so only the
+// first piece's shorter walk stays in front of the bandwidth-bound pass 3.
+constexpr uint32_t kPieceDiv = 8;
+constexpr uint32_t kPieceMinBlocks = 8192;
+uint32_t piece_split(uint32_t nblk) {
+  if (nblk < kPieceMinBlocks) return 0;
+  return (nblk / kPieceDiv) & ~uint32_t(kTile - 1);  // a multiple of the count kernel's tile
+}
+
+int ensure_pieces(okv_ctx* ctx) {
+  if (ctx->stream2) return OKV_OK;
+  OKV_HIP(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
+  OKV_HIP(hipEventCreateWithFlags(&ctx->ev_piece[0], hipEventDisableTiming));
+  OKV_HIP(hipEventCreateWithFlags(&ctx->ev_piece[1], hipEventDisableTiming));
+  OKV_HIP(hipMalloc(&ctx->d_tot2, sizeof(Totals)));
+  return OKV_OK;
+}
+
+// Passes 1-2 as two launches: blocks [0, b0) on the context stream (totals
+// into d_tot2), then -- once they are done -- blocks [b0, nblk) on stream2,
+// their prefixes continuing from d_tot2 (final totals into d_tot).
+int launch_plan_pieces(okv_ctx* ctx, const Work& w, uint32_t nblk, uint32_t b0,
+                       uint64_t* d_row_start, uint16_t* rt_kl, uint64_t span_cap) {
+  int rc = ensure_blocks(ctx, nblk);
+  if (rc) return rc;
+  if ((rc = ensure_pieces(ctx))) return rc;
+  uint32_t* const big = big_counter(ctx);
+  const uint32_t nA = b0, nB = nblk - b0;
+  hipLaunchKernelGGL(okv_count_kernel, dim3((nA + kTile - 1) / kTile), dim3(kThreads), 0,
+                     ctx->stream, w.seg, w.seg_bytes, w.descs, nA, w.comp, ctx->d_cnt, ctx->d_lp,
+                     ctx->d_tile_tot, ctx->d_rec, rt_kl, ctx->d_big, big, w.pre, 0, span_cap,
+                     ctx->d_tile_pre, ctx->d_tot2, nullptr, ctx->d_ctr + kCtrArrive,
+                     big_counter(ctx, 1), nullptr, 0u);
+  OKV_HIP(hipGetLastError());
+  OKV_HIP(hipEventRecord(ctx->ev_piece[0], ctx->stream));
+  OKV_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_piece[0], 0));
+  const uint64_t t0 = b0 / kTile;
+  hipLaunchKernelGGL(okv_count_kernel, dim3((nB + kTile - 1) / kTile), dim3(kThreads), 0,
+                     ctx->stream2, w.seg, w.seg_bytes, w.descs + b0, nB, w.comp, ctx->d_cnt + b0,
+                     ctx->d_lp + b0, ctx->d_tile_tot + t0, ctx->d_rec + uint64_t(b0) * kRCap,
+                     rt_kl ? rt_kl + uint64_t(b0) * kRCap : nullptr, ctx->d_big, big,
+                     w.pre ? w.pre + b0 : nullptr, 0, span_cap, ctx->d_tile_pre + t0, ctx->d_tot,
+                     d_row_start ? d_row_start + b0 : nullptr, ctx->d_ctr + kCtrArrive, nullptr,
+                     ctx->d_tot2, b0);
+  OKV_HIP(hipGetLastError());
+  OKV_HIP(hipEventRecord(ctx->ev_piece[1], ctx->stream2));
+  ctx->big_slot ^= 1u;  // the first launch zeroed the other slot
+  prof_mark(ctx, 2);
+  prof_mark(ctx, 3);
+  return OKV_OK;
+}
+
+// The CopyParams of blocks [b0, b0 + n) of P (block-indexed arrays advanced;
+// row and arena positions stay global).
+CopyParams piece_params(const CopyParams& P, uint32_t b0, uint32_t n) {
+  CopyParams Q = P;
+  Q.descs = P.descs + b0;
+  Q.nblk = n;
+  Q.cnt = P.cnt + b0;
+  Q.lp = P.lp + b0;
+  Q.tile_pre = P.tile_pre + b0 / kTile;
+  Q.rt_pos = P.rt_pos + uint64_t(b0) * kRCap;
+  Q.rt_kl = P.rt_kl ? P.rt_kl + uint64_t(b0) * kRCap : nullptr;
+  Q.row_start = P.row_start + b0;
+  Q.key_base = P.key_base ? P.key_base + b0 : nullptr;
+  Q.val_base = P.val_base ? P.val_base + b0 : nullptr;
+  Q.blk_status = P.blk_status + b0;
+  return Q;
+}
+
 int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
                   uint32_t nblk, int comp, okv_decode_out* o, uint32_t flags) {
   const bool index_only = flags & OKV_F_INDEX_ONLY;
@@ -1865,10 +1948,14 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   }
   if ((rc = ensure_blocks(ctx, nblk))) return rc;
   uint32_t* const big_count = big_counter(ctx);  // this decode's slot (launch_plan flips it)
+  const uint32_t b0 = tile && !ctx->no_pieces ? piece_split(nblk) : 0u;
   if (fused) {
     if ((rc = ensure_fused(ctx, nblk))) return rc;
     prof_mark(ctx, 2);
     prof_mark(ctx, 3);
+  } else if (b0) {
+    rc = launch_plan_pieces(ctx, w, nblk, b0, o->row_start, rt_kl, geo.span_cap);
+    if (rc) return rc;
   } else {
     rc = launch_plan(ctx, w, nblk, o->row_start, true, rt_kl, geo.span_cap);
     if (rc) return rc;
@@ -1964,7 +2051,13 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
         if ((rc = grow(ctx, &ctx->d_vsrc, &ctx->cap_vsrc, n))) return rc;
         P.vsrc = static_cast<uint64_t*>(ctx->d_vsrc);
       }
-      launch_tile(ctx, P, geo);
+      if (b0) {  // the first piece's tile pass, then the second's after its walk
+        launch_tile(ctx, piece_params(P, 0, b0), geo);
+        OKV_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_piece[1], 0));
+        launch_tile(ctx, piece_params(P, b0, nblk - b0), geo);
+      } else {
+        launch_tile(ctx, P, geo);
+      }
     }
 #ifdef OKV_ABLATE
     else if (sweep) {
@@ -2137,6 +2230,7 @@ okv_ctx* okv_open_ex(int device, void* stream, const okv_open_opts* opts) {
   okv_ctx* ctx = okv_open_on_stream(device, stream);
   if (ctx && opts) {
     if (opts->flags & OKV_OPEN_NO_FUSED) ctx->fused = false;
+    if (opts->flags & OKV_OPEN_NO_PIECES) ctx->no_pieces = true;
     ctx->zstd_one_pass = (opts->flags & OKV_OPEN_ZSTD_ONE_PASS) != 0;
   }
   return ctx;
@@ -2259,6 +2353,13 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->z_seqs);
   (void)hipFree(ctx->z_list);
   (void)hipFree(ctx->z_need);
+  if (ctx->stream2) {
+    (void)hipStreamSynchronize(ctx->stream2);
+    (void)hipStreamDestroy(ctx->stream2);
+  }
+  for (hipEvent_t& ev : ctx->ev_piece)
+    if (ev) (void)hipEventDestroy(ev);
+  (void)hipFree(ctx->d_tot2);
   okv::enc_release(ctx);
   okv::merge_release(ctx);
   if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);

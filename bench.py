@@ -573,6 +573,7 @@ def path_kernels(okv, lp):
     """The pass-3 kernels the last decode launched (okv_last_path bits)."""
     L = okv._lib
     names = [(L.PATH_FUSED, "okv_decode_fused_kernel (passes 1-3)"),
+             (L.PATH_STREAM, "okv_decode_stream_kernel (passes 1-3)"),
              (L.PATH_SMALL, "okv_gather_small_kernel"), (L.PATH_TILE, "okv_tile_kernel"),
              (L.PATH_SWEEP, "okv_rows_kernel + okv_value_sweep_kernel"),
              (L.PATH_STAGED, "okv_gather_staged_kernel"), (L.PATH_GATHER, "okv_gather_kernel"),

@@ -24,7 +24,7 @@ OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS, OPEN_NO_PIECES = 1, 2, 4
 # okv_last_path bits (include/okv_sst.h OKV_PATH_*)
 PATH_FUSED, PATH_SMALL, PATH_TILE, PATH_SWEEP = 1, 2, 4, 8
 PATH_STAGED, PATH_GATHER, PATH_BIG, PATH_ZSTD = 16, 32, 64, 128
-PATH_ZSTD_REGROW, PATH_ENC_ONEPASS = 256, 512
+PATH_ZSTD_REGROW, PATH_ENC_ONEPASS, PATH_STREAM = 256, 512, 1024
 # SegmentWriter sentinels (okv_sst.h OKV_W_*)
 W_KEY_TOO_LARGE, W_VALUE_TOO_LARGE, W_CLOSED, W_INVALID_KEY = -101, -102, -103, -104
 W_NIL_WRITER, W_UNSUPPORTED, W_NO_ROWS = -105, -106, -107

@@ -1070,7 +1070,11 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   return v;
 }
 
-__global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, FusedParams F) {
+// kLB: the form for batches of any size (okv_decode_stream_kernel below):
+// the exclusive prefix by a decoupled look-back instead of the last arrival's
+// scan, so no block waits for blocks that may not be resident.
+template <bool kLB>
+__device__ __forceinline__ void fused_pass(const CopyParams& P, const FusedParams& F) {
   __shared__ GatherSmem sm;
   __shared__ uint4 stage[kSmallStage / 16 + 4];
   __shared__ uint32_t s_b;
@@ -1130,10 +1134,53 @@ __global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, Fuse
   kb = __shfl(kb, 0, 64);
   vb = __shfl(vb, 0, 64);
   p = __shfl(p, 0, 64);
+  const Prefix mine{rows, round16(kb), round16(vb), uint64_t(st != OKV_BLK_OK)};
+  Prefix ex{0, 0, 0, 0};
+  if constexpr (kLB) {
+    // ---- pass 2 by decoupled look-back: publish this block's aggregate,
+    // then read the flags of the 64 blocks before it at once (one lane each),
+    // waiting until each has published at least its aggregate; the nearest
+    // inclusive prefix in the window ends the look-back, else the window's
+    // aggregates are added and the next 64 are read.  Blocks take their
+    // index from a counter in start order, so every block waited on is
+    // running: any batch size is safe.
+    if (lane == 0) {
+      publish(&F.flag[b], &F.agg[b], mine, tag | 1u);
+      atomicAdd(F.arr, 1ull);  // (kept in step with F.ctr: the host's base)
+    }
+    int64_t hi = int64_t(b) - 1;
+    for (;;) {
+      const int64_t k = hi - int64_t(lane);
+      uint32_t f = k >= 0 ? flag_peek(&F.flag[k]) : (tag | 2u);
+      while (__any((f & ~3u) != tag)) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((f & ~3u) != tag) f = flag_peek(&F.flag[k]);
+      }
+      const uint64_t inc = __ballot((f & 3u) == 2u);
+      const uint32_t j = inc ? uint32_t(__ffsll(static_cast<unsigned long long>(inc)) - 1) : 64u;
+      // lanes < j: aggregates; lane j: an inclusive prefix (zero before block 0)
+      Prefix v{0, 0, 0, 0};
+      if (lane < j && k >= 0) v = prefix_peek(&F.agg[k]);
+      if (lane == j && k >= 0) v = prefix_peek(&F.incl[k]);
+      ex.rows += wave_sum64(v.rows);
+      ex.kb += wave_sum64(v.kb);
+      ex.vb += wave_sum64(v.vb);
+      ex.bad += wave_sum64(v.bad);
+      if (j < 64) break;
+      hi -= 64;
+    }
+    if (lane == 0) {  // this block's inclusive prefix
+      const Prefix in{ex.rows + mine.rows, ex.kb + mine.kb, ex.vb + mine.vb, ex.bad + mine.bad};
+      publish(&F.flag[b], &F.incl[b], in, tag | 2u);
+      if (b == P.nblk - 1) {
+        *F.tot = Totals{in.rows, in.kb, in.vb, in.bad};
+        P.row_start[P.nblk] = in.rows;
+      }
+    }
+  } else {
   // ---- pass 2: the last block to arrive scans every block's counts ----
   // (every block of the grid is resident: the fused form runs for small
   // batches only, kFusedMaxBlocks << the chip's resident capacity)
-  const Prefix mine{rows, round16(kb), round16(vb), uint64_t(st != OKV_BLK_OK)};
   uint32_t last_arrival = 0;
   if (lane == 0) {
     publish(&F.flag[b], &F.agg[b], mine, tag | 1u);  // sc1 payload, drained, then the flag
@@ -1174,12 +1221,12 @@ __global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, Fuse
   // every block: wait for its exclusive prefix (F.incl holds exclusive values)
   if (lane == 0)
     while (flag_peek(&F.flag[b]) != (tag | 2u)) __builtin_amdgcn_s_sleep(1);
-  Prefix ex{0, 0, 0, 0};
   if (lane == 0) ex = prefix_peek(&F.incl[b]);
   ex.rows = __shfl(ex.rows, 0, 64);
   ex.kb = __shfl(ex.kb, 0, 64);
   ex.vb = __shfl(ex.vb, 0, 64);
   ex.bad = __shfl(ex.bad, 0, 64);
+  }
   // ---- what passes 1-2 leave for okv_copy_kernel, and the totals ----
   if (lane == 0) {
     BlockCount c;
@@ -1219,6 +1266,19 @@ __global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, Fuse
       gather_region<true>(gsrc, sm, nr, P.val_arena, m.B.vb0, 0, 1);
     }
   }
+}
+
+__global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, FusedParams F) {
+  fused_pass<false>(P, F);
+}
+
+// Single pass for batches of small blocks of any size (> kFusedMaxBlocks):
+// the fused kernel's per-block work with the prefix by decoupled look-back.
+// Each block is read once (DMA into LDS, header walk and gather from there);
+// the three-launch form (okv_count_kernel's walk in HBM, then the staged
+// gather) reads it twice.
+__global__ __launch_bounds__(64) void okv_decode_stream_kernel(CopyParams P, FusedParams F) {
+  fused_pass<true>(P, F);
 }
 
 // ---------------------------------------------------------------------------
@@ -1927,9 +1987,13 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   // small blocks: passes 1-3 in one launch (okv_decode_fused_kernel)
   const bool fused =
       ctx->fused && nblk && nblk <= ctx->fused_max && gather_threads(ctx, w, nblk) == 64;
+  // larger batches of small blocks: the same single pass with the prefix by
+  // decoupled look-back (okv_decode_stream_kernel)
+  const bool stream =
+      ctx->fused && nblk > ctx->fused_max && gather_threads(ctx, w, nblk) == 64;
   // large blocks: the source-tile pass (okv_tile_kernel); value_sweep 1-7 are
   // the round-2 forms (row pass + address-ordered value sweep)
-  const bool large = nblk && !fused && gather_threads(ctx, w, nblk) == 256;
+  const bool large = nblk && !fused && !stream && gather_threads(ctx, w, nblk) == 256;
 #ifdef OKV_ABLATE
   const bool tile = large && ctx->value_sweep == 8;
   const bool sweep = large && !tile && ctx->value_sweep && !index_only && ctx->gather_staged &&
@@ -1949,7 +2013,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   if ((rc = ensure_blocks(ctx, nblk))) return rc;
   uint32_t* const big_count = big_counter(ctx);  // this decode's slot (launch_plan flips it)
   const uint32_t b0 = tile && !ctx->no_pieces ? piece_split(nblk) : 0u;
-  if (fused) {
+  if (fused || stream) {
     if ((rc = ensure_fused(ctx, nblk))) return rc;
     prof_mark(ctx, 2);
     prof_mark(ctx, 3);
@@ -2009,6 +2073,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
                    (comp == OKV_COMP_ZSTD && !index_only && ctx->z_retried ? OKV_PATH_ZSTD_REGROW : 0u) |
                    (!nblk ? 0u
                     : fused ? OKV_PATH_FUSED
+                    : stream ? OKV_PATH_STREAM
                     : OKV_PATH_BIG | (tile ? OKV_PATH_TILE
                                       : sweep ? OKV_PATH_SWEEP | OKV_PATH_STAGED
                                       : gt == 256 && ctx->gather_staged && !index_only
@@ -2020,7 +2085,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
     OKV_HIP(hipStreamWaitEvent(ctx->stream, ctx->chain->p3_done, 0));
   if (nblk) {
     const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
-    if (fused) {
+    if (fused || stream) {
       FusedParams F;
       F.pre = w.pre;
       F.cnt = ctx->d_cnt;
@@ -2036,7 +2101,10 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       F.epoch = ctx->f_epoch;
       F.tot = ctx->d_tot;
       F.big_zero = big_counter(ctx, 1);
-      hipLaunchKernelGGL(okv_decode_fused_kernel, dim3(nblk), dim3(64), 0, ctx->stream, P, F);
+      if (fused)
+        hipLaunchKernelGGL(okv_decode_fused_kernel, dim3(nblk), dim3(64), 0, ctx->stream, P, F);
+      else
+        hipLaunchKernelGGL(okv_decode_stream_kernel, dim3(nblk), dim3(64), 0, ctx->stream, P, F);
       const hipError_t le = hipGetLastError();
       if (le != hipSuccess) {
         // nothing ran: the counters keep their value, so f_base must too

@@ -1950,10 +1950,10 @@ __device__ __forceinline__ uint32_t gload_u8(const uint8_t* p) {
 constexpr uint32_t kExecOut = OKV_ZSTD_EXEC_OUT;
 constexpr int kEU = int(kExecOut / 1024);
 #ifndef OKV_ZSTD_GQ
-#define OKV_ZSTD_GQ 2
+#define OKV_ZSTD_GQ 1
 #endif
 #ifndef OKV_ZSTD_GB
-#define OKV_ZSTD_GB 8
+#define OKV_ZSTD_GB 4
 #endif
 #ifndef OKV_ZSTD_SU
 #define OKV_ZSTD_SU 2
@@ -1963,15 +1963,22 @@ constexpr int kEU = int(kExecOut / 1024);
 constexpr int kSU = OKV_ZSTD_SU;
 constexpr uint32_t kSW = 64u * kSU;
 static_assert(kSW <= zst::kSeqChunk, "sequence window (byte map entries are 8-bit)");
-constexpr int kGQ = OKV_ZSTD_GQ;  // gather: output dwords per lane per step (2: 128 registers,
-                                  // 4: 163 -- and slower, profiles/r3/r3v)
+constexpr int kGQ = OKV_ZSTD_GQ;  // gather: output dwords per lane per step (1: 96 registers at the
+                                  // 5-wave cap; 2: 128; 4: 163 -- slower, profiles/r3/r3v, r3z)
 constexpr int kGB = OKV_ZSTD_GB;  // source resolution: 64-byte groups per batch
 static_assert(kExecOut <= zst::kChunkOut && kExecOut % 1024 == 0 && (kExecOut & (kExecOut - 1)) == 0,
               "exec chunk");
 // Executor grid (blocks are strided over it); the profiling slots are sized
 // for the largest grid.
 constexpr uint32_t kExecGridMax = 16384;
-#ifdef OKV_ZSTD_EXEC_WPE  // (build-time occupancy probe: waves per SIMD the registers must allow)
+// Registers capped for 5 waves per SIMD (with one output dword per lane and
+// 4-group batches: 96 registers + 52 B of spills, executor 2.35-2.38 vs
+// 2.43-2.51 ms for 2 dwords / 8 groups uncapped, profiles/r3/r3z).  A build
+// with -DOKV_ZSTD_EXEC_WPE=0 drops the cap (A/B).
+#ifndef OKV_ZSTD_EXEC_WPE
+#define OKV_ZSTD_EXEC_WPE 5
+#endif
+#if OKV_ZSTD_EXEC_WPE > 0
 #define OKV_ZSTD_EXEC_ATTR __attribute__((amdgpu_waves_per_eu(OKV_ZSTD_EXEC_WPE)))
 #else
 #define OKV_ZSTD_EXEC_ATTR

@@ -4,7 +4,7 @@ so that both builds see the same box).
 
 usage: python tools/ab_lib.py <path to libokv_sst*.so> [label]
 env:   ABL_NBLK (65536), ABL_ROUNDS (5), ABL_STEPS (10), ABL_KIND (1), ABL_BS (65536),
-       ABL_TH (57344)
+       ABL_TH (57344), ABL_FLAGS (okv_open_opts.flags, 0; e.g. 4 = OKV_OPEN_NO_PIECES)
 Prints one JSON line: per-pass ms (HIP events, median over rounds), the
 one-at-a-time decode step (host clock, median) and its roofline fraction.
 """
@@ -34,7 +34,8 @@ w = okv.synth_segment(kind, 3, nblocks=nblk, threshold=th, block_size=bs)
 seg = w.data_view()
 d = w.descs()[:nblk]
 dev = torch.device("cuda", 0)
-dec = okv.Decoder(0, stream=torch.cuda.current_stream(dev).cuda_stream)
+dec = okv.Decoder(0, stream=torch.cuda.current_stream(dev).cuda_stream,
+                  flags=int(os.environ.get("ABL_FLAGS", "0")))
 seg_t = torch.empty(seg.nbytes + 64, dtype=torch.uint8, device=dev)
 seg_t[:seg.nbytes].copy_(torch.from_numpy(seg))
 d_t = torch.from_numpy(d.view(np.int64).copy()).to(dev)

@@ -2200,6 +2200,31 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
 }
 
 // Host pointers: stage inputs to device scratch, decode, copy results back.
+// Upper bounds of a host-mode decode's outputs from the host descriptors
+// (uncompressed blocks: a block's records lie in its BlockSize bytes inside
+// the segment, each >= 6 bytes; every block region pads to 16 bytes), or
+// false when they do not exist (zstd: decompressed sizes) or exceed `limit`.
+bool output_bounds(const uint8_t* /*seg*/, uint64_t seg_bytes, const okv_block_desc* descs,
+                   uint32_t nblk, int comp, uint64_t limit, uint64_t* rows, uint64_t* bytes) {
+  if (comp == OKV_COMP_ZSTD) return false;
+  uint64_t r = 0, by = 0;
+  for (uint32_t b = 0; b < nblk; ++b) {
+    const okv_block_desc& d = descs[b];
+    uint64_t span = 0;
+    if (comp != OKV_COMP_LZ4 && int64_t(d.offset) >= 0 && d.offset < seg_bytes)
+      span = std::min<uint64_t>(d.block_size, seg_bytes - d.offset);
+    r += span / 6;
+    by += span + 16;
+    if (by > limit) return false;
+  }
+  *rows = r;
+  *bytes = by;
+  return true;
+}
+
+// Host pointers: stage inputs to device scratch, decode, copy results back.
+// The device outputs are sized from the host descriptors' bounds when those
+// exist (one pass-1 walk per call); otherwise from a pass-1 plan first.
 int decode_host(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv_block_desc* descs,
                 uint32_t nblk, int comp, okv_decode_out* o, uint32_t flags) {
   const bool index_only = flags & OKV_F_INDEX_ONLY;
@@ -2213,43 +2238,50 @@ int decode_host(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv_
   if (nblk)
     OKV_HIP(hipMemcpyAsync(ctx->d_desc, descs, size_t(nblk) * sizeof(Desc),
                            hipMemcpyHostToDevice, ctx->stream));
-  // size the device outputs from the plan
   rc = ensure_blocks(ctx, nblk);
   if (rc) return rc;
   // device output layout inside one scratch allocation
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-  // provisional: row_start needed by the plan launch
   const size_t n1 = size_t(nblk) + 1;
   size_t off_rs = 0, off_kb = al(off_rs + n1 * 8), off_vb = al(off_kb + n1 * 8),
          off_st = al(off_vb + n1 * 8), off_rows = al(off_st + n1 * 4);
-  rc = grow(ctx, &ctx->d_out, &ctx->cap_out, off_rows + 256);
+  uint64_t brows = 0, bbytes = 0;
+  const bool bounded = output_bounds(seg, seg_bytes, descs, nblk, comp, uint64_t(1) << 30, &brows,
+                                     &bbytes);
+  uint64_t R, KB, VB;  // device capacities
+  if (bounded) {
+    R = std::min<uint64_t>(brows, o->row_cap);
+    KB = index_only ? 0 : std::min<uint64_t>(bbytes, o->key_cap);
+    VB = index_only ? 0 : std::min<uint64_t>(bbytes, o->val_cap);
+  } else {
+    rc = grow(ctx, &ctx->d_out, &ctx->cap_out, off_rows + 256);
+    if (rc) return rc;
+    uint8_t* base = static_cast<uint8_t*>(ctx->d_out);
+    Work w;
+    rc = prepare(ctx, ctx->d_seg, seg_bytes, ctx->d_desc, nblk, comp, index_only, &w);
+    if (rc) return rc;
+    rc = launch_plan(ctx, w, nblk, reinterpret_cast<uint64_t*>(base + off_rs));
+    if (rc) return rc;
+    Totals T;
+    rc = read_totals(ctx, &T);
+    if (rc) return rc;
+    o->n_rows = T.rows;
+    o->key_bytes = index_only ? 0 : T.kb;
+    o->val_bytes = index_only ? 0 : T.vb;
+    o->n_bad_blocks = T.bad;
+    if (T.rows > o->row_cap || (!index_only && (T.kb > o->key_cap || T.vb > o->val_cap)))
+      return set_err(ctx, OKV_E_CAPACITY, "output capacity too small (totals set)");
+    R = T.rows;
+    KB = index_only ? 0 : T.kb;
+    VB = index_only ? 0 : T.vb;
+  }
+  size_t off_ko = al(off_rows), off_kl = al(off_ko + R * 8), off_vo = al(off_kl + R * 2),
+         off_vl = al(off_vo + R * 8), off_ka = al(off_vl + R * 4), off_va = al(off_ka + KB),
+         total = al(off_va + VB) + 256;
+  // grow (keeps nothing: plan results live in ctx scratch, row_start[nblk] is rewritten)
+  rc = grow(ctx, &ctx->d_out, &ctx->cap_out, total);
   if (rc) return rc;
   uint8_t* base = static_cast<uint8_t*>(ctx->d_out);
-  Work w;
-  rc = prepare(ctx, ctx->d_seg, seg_bytes, ctx->d_desc, nblk, comp, index_only, &w);
-  if (rc) return rc;
-  rc = launch_plan(ctx, w, nblk, reinterpret_cast<uint64_t*>(base + off_rs));
-  if (rc) return rc;
-  Totals T;
-  rc = read_totals(ctx, &T);
-  if (rc) return rc;
-  o->n_rows = T.rows;
-  o->key_bytes = index_only ? 0 : T.kb;
-  o->val_bytes = index_only ? 0 : T.vb;
-  o->n_bad_blocks = T.bad;
-  if (T.rows > o->row_cap || (!index_only && (T.kb > o->key_cap || T.vb > o->val_cap)))
-    return set_err(ctx, OKV_E_CAPACITY, "output capacity too small (totals set)");
-  const size_t R = T.rows;
-  size_t off_ko = al(off_rows), off_kl = al(off_ko + R * 8), off_vo = al(off_kl + R * 2),
-         off_vl = al(off_vo + R * 8), off_ka = al(off_vl + R * 4),
-         off_va = al(off_ka + (index_only ? 0 : T.kb)),
-         total = al(off_va + (index_only ? 0 : T.vb)) + 256;
-  if (total > ctx->cap_out) {
-    // grow (keeps nothing: plan results live in ctx scratch, row_start[nblk] is rewritten)
-    rc = grow(ctx, &ctx->d_out, &ctx->cap_out, total);
-    if (rc) return rc;
-    base = static_cast<uint8_t*>(ctx->d_out);
-  }
   okv_decode_out d = *o;
   d.row_start = reinterpret_cast<uint64_t*>(base + off_rs);
   d.key_base = reinterpret_cast<uint64_t*>(base + off_kb);
@@ -2262,11 +2294,19 @@ int decode_host(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv_
   d.key_arena = index_only ? nullptr : base + off_ka;
   d.val_arena = index_only ? nullptr : base + off_va;
   d.row_cap = R;
-  d.key_cap = T.kb;
-  d.val_cap = T.vb;
+  d.key_cap = KB;
+  d.val_cap = VB;
   rc = decode_device(ctx, ctx->d_seg, seg_bytes, ctx->d_desc, nblk, comp, &d,
                      (flags & ~OKV_F_ASYNC) | OKV_F_DEVICE_PTRS);
+  o->n_rows = d.n_rows;
+  o->key_bytes = d.key_bytes;
+  o->val_bytes = d.val_bytes;
+  o->n_bad_blocks = d.n_bad_blocks;
+  if (rc == OKV_E_CAPACITY) {  // the caller's capacity (a bounded decode: totals are set)
+    return set_err(ctx, OKV_E_CAPACITY, "output capacity too small (totals set)");
+  }
   if (rc) return rc;
+  const uint64_t nR = d.n_rows, nK = index_only ? 0 : d.key_bytes, nV = index_only ? 0 : d.val_bytes;
   auto d2h = [&](void* dst, const void* src, size_t n) -> int {
     if (dst && n) OKV_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, ctx->stream));
     return OKV_OK;
@@ -2276,13 +2316,13 @@ int decode_host(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv_
   if (!index_only) {
     if ((rc = d2h(o->key_base, d.key_base, size_t(nblk) * 8))) return rc;
     if ((rc = d2h(o->val_base, d.val_base, size_t(nblk) * 8))) return rc;
-    if ((rc = d2h(o->key_arena, d.key_arena, T.kb))) return rc;
-    if ((rc = d2h(o->val_arena, d.val_arena, T.vb))) return rc;
+    if ((rc = d2h(o->key_arena, d.key_arena, nK))) return rc;
+    if ((rc = d2h(o->val_arena, d.val_arena, nV))) return rc;
   }
-  if ((rc = d2h(o->key_off, d.key_off, R * 8))) return rc;
-  if ((rc = d2h(o->key_len, d.key_len, R * 2))) return rc;
-  if ((rc = d2h(o->val_off, d.val_off, R * 8))) return rc;
-  if ((rc = d2h(o->val_len, d.val_len, R * 4))) return rc;
+  if ((rc = d2h(o->key_off, d.key_off, nR * 8))) return rc;
+  if ((rc = d2h(o->key_len, d.key_len, nR * 2))) return rc;
+  if ((rc = d2h(o->val_off, d.val_off, nR * 8))) return rc;
+  if ((rc = d2h(o->val_len, d.val_len, nR * 4))) return rc;
   OKV_HIP(hipStreamSynchronize(ctx->stream));
   return OKV_OK;
 }

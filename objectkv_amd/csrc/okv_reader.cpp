@@ -72,13 +72,20 @@ constexpr size_t kIterWindow = 256;
 // One GPU decode of a batch of blocks (okv_decode_blocks), with the rows of
 // each batch entry built lazily.  Shared: the iteration window, an iterator's
 // current block and the last GetRow / GetRange results may all hold it.
+template <class T>
+using Arr = std::unique_ptr<T[]>;  // uninitialised: the decode writes what is read
+template <class T>
+Arr<T> arr(uint64_t n) {
+  return Arr<T>(new T[n ? n : 1]);
+}
 struct Batch {
   std::vector<uint32_t> entries;  // file_entries index of each batch entry
   std::vector<int32_t> status;
-  std::vector<uint64_t> row_start, key_off, val_off;
-  std::vector<uint16_t> key_len;
-  std::vector<uint32_t> val_len;
-  std::vector<uint8_t> key_arena, val_arena;
+  std::vector<uint64_t> row_start;
+  Arr<uint64_t> key_off, val_off;
+  Arr<uint16_t> key_len;
+  Arr<uint32_t> val_len;
+  Arr<uint8_t> key_arena, val_arena;
   std::vector<std::vector<okv_row>> rows;
   std::vector<bool> built;
 };
@@ -207,18 +214,36 @@ int decode_batch(okv_reader* r, const std::vector<uint32_t>& entries, BatchP* ou
   const uint8_t* seg = hi > lo ? r->data.data() + lo : nullptr;
   const uint64_t n = hi - lo;
   uint64_t rows = 0, kb = 0, vb = 0;
-  int rc = okv_decode_plan(r->ctx, seg, n, descs.data(), nb, r->compression, 0, &rows, &kb, &vb);
-  if (rc) return OKV_R_GPU;
+  int rc;
+  // a small batch (GetRow's one block) sizes its outputs from bounds (one GPU
+  // walk); a large one (an iteration window, GetRange) from the plan, so it
+  // allocates what it fills; zstd (decompressed sizes) always plans
+  if (r->compression == OKV_COMP_ZSTD || n > (uint64_t(1) << 20)) {
+    rc = okv_decode_plan(r->ctx, seg, n, descs.data(), nb, r->compression, 0, &rows, &kb, &vb);
+    if (rc) return OKV_R_GPU;
+  } else {
+    // bounds from the descriptors: a block's records lie in its BlockSize
+    // bytes inside the span (>= 6 bytes each), each region pads to 16 bytes;
+    // the decode then sizes its device outputs the same way (one walk)
+    for (const okv_block_desc& d : descs) {
+      uint64_t span = 0;
+      if (r->compression != OKV_COMP_LZ4 && int64_t(d.offset) >= 0 && d.offset < n)
+        span = std::min<uint64_t>(d.block_size, n - d.offset);
+      rows += span / 6;
+      kb += span + 16;
+    }
+    vb = kb;
+  }
   BatchP B = std::make_shared<Batch>();
   B->entries = entries;
   B->row_start.assign(nb + 1, 0);
   B->status.assign(nb, 0);
-  B->key_off.assign(rows + 1, 0);
-  B->val_off.assign(rows + 1, 0);
-  B->key_len.assign(rows + 1, 0);
-  B->val_len.assign(rows + 1, 0);
-  B->key_arena.assign(kb + 16, 0);
-  B->val_arena.assign(vb + 16, 0);
+  B->key_off = arr<uint64_t>(rows + 1);
+  B->val_off = arr<uint64_t>(rows + 1);
+  B->key_len = arr<uint16_t>(rows + 1);
+  B->val_len = arr<uint32_t>(rows + 1);
+  B->key_arena = arr<uint8_t>(kb + 16);
+  B->val_arena = arr<uint8_t>(vb + 16);
   std::vector<uint64_t> kbase(nb + 1), vbase(nb + 1);
   okv_decode_out o;
   std::memset(&o, 0, sizeof(o));
@@ -226,12 +251,12 @@ int decode_batch(okv_reader* r, const std::vector<uint32_t>& entries, BatchP* ou
   o.key_base = kbase.data();
   o.val_base = vbase.data();
   o.blk_status = B->status.data();
-  o.key_off = B->key_off.data();
-  o.key_len = B->key_len.data();
-  o.val_off = B->val_off.data();
-  o.val_len = B->val_len.data();
-  o.key_arena = B->key_arena.data();
-  o.val_arena = B->val_arena.data();
+  o.key_off = B->key_off.get();
+  o.key_len = B->key_len.get();
+  o.val_off = B->val_off.get();
+  o.val_len = B->val_len.get();
+  o.key_arena = B->key_arena.get();
+  o.val_arena = B->val_arena.get();
   o.row_cap = rows;
   o.key_cap = kb;
   o.val_cap = vb;
@@ -264,8 +289,8 @@ int batch_rows(Batch& B, uint32_t slot, const std::vector<okv_row>** rows) {
       okv_row row;
       row.key_len = B.key_len[g];
       row.val_len = B.val_len[g];
-      row.key = row.key_len ? B.key_arena.data() + B.key_off[g] : nullptr;  // nil (Q4)
-      row.val = row.val_len ? B.val_arena.data() + B.val_off[g] : nullptr;
+      row.key = row.key_len ? B.key_arena.get() + B.key_off[g] : nullptr;  // nil (Q4)
+      row.val = row.val_len ? B.val_arena.get() + B.val_off[g] : nullptr;
       out.push_back(row);
     }
     B.built[slot] = true;

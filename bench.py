@@ -151,8 +151,11 @@ def pmc_traffic(config, mode, kernel, sources=DECODE_SOURCES):
     if d.get("source_sha") != source_sha(sources):
         return None, "stale (kernel sources changed since the PMC run)"
     names = (kernel,) if isinstance(kernel, str) else tuple(kernel)
-    hits = [k["hbm_bytes"] for name, k in d.get("kernels", {}).items()
-            if any(n in name for n in names)]
+    # per launch, times the launches one step makes of it (a two-piece decode
+    # launches the tile pass twice; pmc_summary averages over launches)
+    per = d.get("launches_per_step", {})
+    hits = [k["hbm_bytes"] * next((m for p, m in per.items() if p in name), 1)
+            for name, k in d.get("kernels", {}).items() if any(n in name for n in names)]
     if hits:  # per launch, summed over the kernels of the pass
         return sum(hits), os.path.relpath(path, ROOT)
     return None, None
@@ -172,7 +175,8 @@ def trace_roofline(config, alg):
         return {"source": os.path.relpath(path, ROOT),
                 "stale": "kernel sources changed since the trace"}
     ms = d["avg_ns_timed"] / 1e6
-    out = {"kernel": d["kernel"], "avg_ms": round(ms, 4), "launches": d["timed_launches"],
+    out = {"kernel": d["kernel"], "avg_ms": round(ms, 4), "steps": d["timed_launches"],
+           "launches_per_step": d.get("launches_per_step", 1),
            "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "source": os.path.relpath(path, ROOT)}
     if d.get("bench_event_ms_same_process"):

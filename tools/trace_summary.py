@@ -5,6 +5,11 @@ roofline fraction the timed average implies.
 usage: python tools/trace_summary.py <run_kernel_trace.csv> <kernel substring>
            <untimed launches> <algorithmic bytes per launch> <out.json> [note]
            [--sha <decode source sha>] [--bench-log <the traced bench's stdout/stderr>]
+           [--per-step K]
+
+--per-step K: the kernel runs K launches per step (a two-piece decode launches
+the tile pass twice): consecutive launches are summed in groups of K, and
+every count below (launches, untimed launches) is in steps.
 
 --sha lets bench.py attach the trace to its roofline only while the kernel
 sources are the traced ones; --bench-log records the bench's own HIP-event
@@ -17,7 +22,7 @@ import sys
 
 argv = sys.argv[1:]
 opts = {}
-for flag in ("--sha", "--bench-log"):
+for flag in ("--sha", "--bench-log", "--per-step"):
     if flag in argv:
         i = argv.index(flag)
         opts[flag] = argv[i + 1]
@@ -27,6 +32,9 @@ note = argv[5] if len(argv) > 5 else ""
 rows = [r for r in csv.DictReader(open(path)) if kern in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ns = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
+K = int(opts.get("--per-step", "1"))
+if K > 1:  # per step: the K launches of one decode, summed
+    ns = [sum(ns[i:i + K]) for i in range(0, len(ns) - len(ns) % K, K)]
 timed = ns[skip:]
 avg = sum(timed) / len(timed)
 res = {"kernel": rows[0]["Kernel_Name"].split("(")[0] if rows else kern, "source": path,
@@ -35,6 +43,7 @@ res = {"kernel": rows[0]["Kernel_Name"].split("(")[0] if rows else kern, "source
        "avg_ns_all": sum(ns) / len(ns), "per_launch_ns": ns,
        "algorithmic_bytes_per_launch": alg, "achieved_GB_s": alg / avg,
        "frac_of_8TB_s": alg / avg / 8000.0, "note": note}
+res["launches_per_step"] = K
 if "--sha" in opts:
     res["source_sha"] = opts["--sha"]
 if "--bench-log" in opts:

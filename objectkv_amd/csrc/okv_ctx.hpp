@@ -120,7 +120,8 @@ struct okv_ctx {
   uint8_t* z_blit = nullptr;      // per-block literal scratch (prologue -> executor)
   size_t z_cap_blit = 0;
   uint32_t* z_tabs = nullptr;     // per-block FSE tables (prologue -> sequence stage)
-  size_t z_cap_tabs = 0;
+  size_t z_cap_tabs = 0;         // (+ kHufSlot u16 per block: Huffman tables, prologue -> stream stage)
+  hipEvent_t z_ev = nullptr;      // the sequence count's copy (zstd_run)
   void* z_zb = nullptr;           // per-block zst::ZBlk
   size_t z_cap_zb = 0;
   uint64_t* z_seq_off = nullptr;  // [nblk + 1] sequence offsets

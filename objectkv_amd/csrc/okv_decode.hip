@@ -2456,6 +2456,7 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->z_lit);
   (void)hipFree(ctx->z_blit);
   (void)hipFree(ctx->z_tabs);
+  if (ctx->z_ev) (void)hipEventDestroy(ctx->z_ev);
   (void)hipFree(ctx->z_zb);
   (void)hipFree(ctx->z_seq_off);
   (void)hipFree(ctx->z_seqs);

@@ -533,14 +533,15 @@ __device__ int32_t read_huf_tree(SmemCore& sm, const uint8_t* p, int64_t n, uint
 // dwords prefetched below it, so a refill rarely waits on memory (a literal
 // takes <= 11 bits; a fresh load per container refill made the decode a chain
 // of memory round trips).  Bits below the stream read as 0 (RFC 8878 4.2.1.2).
-__device__ bool huf_stream(const SmemCore& sm, uint32_t mb, const uint8_t* p, int64_t n, uint8_t* out,
-                           uint32_t cnt) {
+__device__ __forceinline__ bool huf_stream(const uint16_t* huf, uint32_t mb, const uint8_t* p, int64_t n,
+                                           uint8_t* out, uint32_t cnt) {
   if (n <= 0) return cnt == 0 && n == 0;
   const uint32_t last = p[n - 1];
   if (last == 0) return false;  // the final byte holds the end marker
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t* ab = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-  const int32_t s0 = int32_t(a & 3), B0 = 8 * s0;  // the stream's bit 0, relative to ab
+  // (pointer arithmetic, not an integer round trip: the address space of p
+  // -- global -- then reaches the loads)
+  const int32_t s0 = int32_t(reinterpret_cast<uintptr_t>(p) & 3), B0 = 8 * s0;  // bit 0, relative to ab
+  const uint32_t* ab = reinterpret_cast<const uint32_t*>(p - s0);
   int32_t P = B0 + int32_t(n - 1) * 8 + (31 - __builtin_clz(last));
   int32_t cd = (P >> 5) - 1;  // the container holds dwords cd + 1 : cd
   auto raw = [&](int32_t d) { return ab[d < 0 ? 0 : d]; };
@@ -564,7 +565,7 @@ __device__ bool huf_stream(const SmemCore& sm, uint32_t mb, const uint8_t* p, in
   auto literal = [&](uint32_t i) {
     const int32_t p0 = P - int32_t(mb);
     const uint32_t idx = uint32_t(c >> uint32_t(p0 - 32 * cd)) & ((1u << mb) - 1u);
-    const uint32_t e = sm.huf[idx];
+    const uint32_t e = huf[idx];
     out[i] = uint8_t(e & 0xff);
     P -= int32_t(e >> 8);
   };
@@ -607,7 +608,7 @@ struct Out {
 // Per segment block, written by the prologue (okv_zstd_pro_kernel) for the
 // sequence stage and the executor.
 enum : int32_t { kKindDone = 0, kKindSeq = 1, kKindSlow = 2 };
-enum : uint32_t { kFlagFcs = 1, kFlagCsum = 2, kFlagRle = 4 };
+enum : uint32_t { kFlagFcs = 1, kFlagCsum = 2, kFlagRle = 4, kFlagHuf = 8 };
 // Sequence-stage tables, 16 bits per state: symbol (6 bits) | the state's
 // FSE "next state" value x (10 bits; x in [count, 2 count), so < 2^(AL+1)).
 // nbBits = AL - floor(log2 x) and baseline = (x << nbBits) - 2^AL follow, so
@@ -629,7 +630,13 @@ struct ZBlk {
   int32_t st;             // kOK / kErr / kCap of the stage that owns the block
   uint32_t nseq_ok;       // sequences the sequence stage decoded (all unless the stream overflowed)
   uint32_t bmax;          // Block_Maximum_Size of the block's frame (<= 128 KiB)
+  // kFlagHuf: the Huffman literal streams are left to okv_zstd_huf_kernel
+  uint64_t hq_off;        // the first stream (after the jump table), from the segment's start
+  uint32_t hlen[4];       // stream sizes (one stream: hlen[0], the rest 0)
+  uint32_t hmb;           // the table's Max_Number_of_Bits
+  uint32_t hns;           // streams: 1 or 4
 };
+constexpr uint32_t kHufSlot = 1u << kHufMaxBits;  // u16 decoding-table entries per deferred block
 
 // Prologue context of one block: per-block literal scratch and table slots.
 struct Pro {
@@ -640,6 +647,10 @@ struct Pro {
   bool deferrable;    // the compressed block being decoded may be deferred
   uint64_t fcs;
   uint32_t fcs_on, csum_on;
+  const uint8_t* seg;
+  uint16_t* htab;     // kHufSlot entries: this block's Huffman decoding table for the stream stage
+  const uint8_t* hq;  // deferred literal streams (huf_on)
+  uint32_t hlen[4], hmb, hns, huf_on;
 };
 
 __device__ __forceinline__ void prof_add(const Out& o, int k, unsigned long long v) {
@@ -880,9 +891,45 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       return kErr;
     }
     const int lane = threadIdx.x & 63;
+    if constexpr (PRO) {
+      // A block whose sequences go to the later stages leaves its streams too:
+      // the table to HBM, the streams' places to zb, and okv_zstd_huf_kernel
+      // decodes 16 blocks' streams per wave, one lane each (here 4 of the
+      // wave's 64 lanes would).  nseq == 0 (the byte after the literals is 0)
+      // emits the literals in this stage and decodes them here.
+      if (pro->deferrable && at + int64_t(csize) < n && p[at + csize] != 0) {
+        const uint32_t mb = fs.huf_bits;
+        if (nstreams == 4) {
+          if (qn < 6) return kErr;
+          const uint32_t s1 = q[0] | (uint32_t(q[1]) << 8), s2 = q[2] | (uint32_t(q[3]) << 8),
+                         s3 = q[4] | (uint32_t(q[5]) << 8);
+          const int64_t s4 = qn - 6 - int64_t(s1) - s2 - s3;
+          if (s4 < 0) return kErr;
+          if (3 * ((regen + 3) / 4) > regen) return kErr;
+          pro->hq = q + 6;
+          pro->hlen[0] = s1;
+          pro->hlen[1] = s2;
+          pro->hlen[2] = s3;
+          pro->hlen[3] = uint32_t(s4);
+        } else {
+          pro->hq = q;
+          pro->hlen[0] = uint32_t(qn);
+          pro->hlen[1] = pro->hlen[2] = pro->hlen[3] = 0;
+        }
+        pro->hmb = mb;
+        pro->hns = nstreams;
+        pro->huf_on = 1;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(sm.huf);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(pro->htab);
+        for (uint32_t u = lane; u < max(1u, (1u << mb) / 2); u += 64) dst[u] = src[u];
+        lits = lit_buf;
+        at += csize;
+        goto sequences;
+      }
+    }
     bool good = true;
     if (nstreams == 1) {
-      if (lane == 0) good = huf_stream(sm, fs.huf_bits, q, qn, lit_buf, regen);
+      if (lane == 0) good = huf_stream(sm.huf, fs.huf_bits, q, qn, lit_buf, regen);
     } else {
       if (qn < 6) return kErr;
       const uint32_t s1 = q[0] | (uint32_t(q[1]) << 8), s2 = q[2] | (uint32_t(q[3]) << 8),
@@ -895,7 +942,7 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
         const int64_t off = 6 + (lane > 0 ? s1 : 0) + (lane > 1 ? s2 : 0) + (lane > 2 ? s3 : 0);
         const int64_t len = lane == 0 ? s1 : lane == 1 ? s2 : lane == 2 ? s3 : s4;
         const uint32_t cnt = lane < 3 ? seg : regen - 3 * seg;
-        good = huf_stream(sm, fs.huf_bits, q + off, len, lit_buf + lane * seg, cnt);
+        good = huf_stream(sm.huf, fs.huf_bits, q + off, len, lit_buf + lane * seg, cnt);
       }
     }
     // every lane must agree the streams decoded cleanly
@@ -905,6 +952,7 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
     lits = lit_buf;
     at += csize;
   }
+sequences:
   const long long t1 = o.prof ? clock64() : 0;
   prof_add(o, 0, t1 - t0);
   // ---- sequences section (3.1.1.3.2)
@@ -990,6 +1038,13 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       z.ml_al = fs.ml_al;
       z.rle_byte = rle_byte;
       z.bmax = o.bmax;
+      if (pro->huf_on) {
+        z.flags |= kFlagHuf;
+        z.hq_off = uint64_t(pro->hq - pro->seg);
+        for (int k = 0; k < 4; ++k) z.hlen[k] = pro->hlen[k];
+        z.hmb = pro->hmb;
+        z.hns = pro->hns;
+      }
     }
     return kDefer;
   } else {
@@ -1526,7 +1581,8 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
     const uint8_t* __restrict__ seg, uint64_t seg_bytes, const Desc* __restrict__ descs,
     uint32_t nblk, const uint64_t* __restrict__ cap_off, uint8_t* __restrict__ dec,
     uint64_t* __restrict__ dec_len, int32_t* __restrict__ zstatus, uint8_t* __restrict__ lits,
-    uint16_t* __restrict__ tabs, zst::ZBlk* __restrict__ zb, unsigned long long* __restrict__ prof) {
+    uint16_t* __restrict__ tabs, uint16_t* __restrict__ htab, zst::ZBlk* __restrict__ zb,
+    unsigned long long* __restrict__ prof) {
   __shared__ zst::SmemCore sm;
   const int lane = threadIdx.x & 63;
   for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
@@ -1552,6 +1608,9 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
       pro.deferrable = false;
       pro.fcs = 0;
       pro.fcs_on = pro.csum_on = 0;
+      pro.htab = htab + uint64_t(b) * zst::kHufSlot;
+      pro.seg = seg;
+      pro.huf_on = 0;
       const int32_t r = zst::decode_frames<true>(sm, seg + d.offset, int64_t(d.compressed_size), o,
                                                  nullptr, &pro);
       __syncthreads();
@@ -1577,6 +1636,62 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
       atomicAdd(prof + 13, 1ull);
     }
   }
+}
+
+// ---- stage 1b: Huffman literal streams, 16 blocks per wave -----------------------
+// One lane per stream (4 per block), each block's decoding table in LDS: the
+// streams of a deferred block (kFlagHuf) decode here into its literal scratch,
+// where the executor reads them.  A stream that fails its checks (no end
+// marker, bits left over; RFC 8878 4.2.2) fails the block: zb.st = kErr,
+// which the sequence stage keeps and the executor reports (the literals come
+// before the sequences, as in the general kernel).
+// (The streams and the scratch are addressed from the kernel's arguments, not
+// through zb's pointers: a pointer read from memory is flat, and a flat load
+// counts against the LDS counter too, so every table lookup's wait would also
+// wait for the stream prefetch.)
+__global__ __launch_bounds__(64) void okv_zstd_huf_kernel(zst::ZBlk* __restrict__ zb, uint32_t nblk,
+                                                          const uint16_t* __restrict__ htab,
+                                                          const uint8_t* __restrict__ seg,
+                                                          uint8_t* __restrict__ blit,
+                                                          const uint64_t* __restrict__ cap_off) {
+  __shared__ uint16_t ht[16 * zst::kHufSlot];  // 64 KiB
+  const int lane = threadIdx.x & 63;
+  const uint32_t j = uint32_t(lane) >> 2, sidx = uint32_t(lane) & 3;
+  const uint32_t b0 = blockIdx.x * 16, b = b0 + j;
+  bool mine = false;
+  uint32_t mb = 0;
+  if (b < nblk) {
+    mine = zb[b].kind == zst::kKindSeq && (zb[b].flags & zst::kFlagHuf);
+    mb = mine ? zb[b].hmb : 0u;
+  }
+  // the tables: 2^(mb+1) bytes each (at least one 1 KiB piece), LDS DMA
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(htab);
+  for (uint32_t jj = 0; jj < 16; ++jj) {
+    const uint32_t mj = __builtin_amdgcn_readlane(mine ? mb + 1 : 0u, int(4 * jj));
+    if (!mj) continue;
+    const uint32_t pieces = mj > 10 ? 1u << (mj - 10) : 1u;
+    for (uint32_t k = 0; k < pieces; ++k)
+      __builtin_amdgcn_global_load_lds(src + (uint64_t(b0 + jj) * zst::kHufSlot * 2 + k * 1024 + 16 * lane),
+                                       OKV_LDS_PTR(reinterpret_cast<uint4*>(ht) + jj * (zst::kHufSlot / 8) + k * 64),
+                                       16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  bool good = true;
+  if (mine) {
+    const uint32_t regen = zb[b].lit_total, ns = zb[b].hns;
+    if (sidx < ns) {
+      const uint32_t sl = (regen + 3) / 4;  // (4 streams: 3 sl <= regen, checked by the prologue)
+      const uint32_t cnt = ns == 1 ? regen : sidx < 3 ? sl : regen - 3 * sl;
+      uint32_t off = 0;
+      for (uint32_t k = 0; k < sidx; ++k) off += zb[b].hlen[k];
+      uint8_t* lits = blit + cap_off[b] + sidx * sl;  // == zb[b].lits + sidx * seg
+      good = zst::huf_stream(ht + j * zst::kHufSlot, mb, seg + zb[b].hq_off + off,
+                             int64_t(zb[b].hlen[sidx]), lits, cnt);
+    }
+  }
+  const uint64_t bad = __ballot(!good);
+  if (mine && sidx == 0 && ((bad >> (4 * j)) & 0xfull)) zb[b].st = zst::kErr;
 }
 
 // Exclusive scan of the deferred blocks' sequence counts -> seq_off[nblk + 1].
@@ -1820,6 +1935,10 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
   const uint32_t b = b0 + lane;
   if (b >= nblk || zb[b].kind != zst::kKindSeq) return;
   const zst::ZBlk z = zb[b];
+  if (z.st != zst::kOK) {  // the literal streams failed (okv_zstd_huf_kernel): nothing to decode
+    zb[b].nseq_ok = 0;
+    return;
+  }
   const uint16_t* T = tl + lane * zst::kTabEnt;
   uint64_t* S = seqs + seq_off[b];
   int32_t st = zst::kOK;
@@ -2526,7 +2645,7 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
                    size_t(nblk) * sizeof(zst::ZBlk))))
       return rc;
     if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_tabs), &ctx->z_cap_tabs,
-                   size_t(nblk) * zst::kTabEnt * 2 + 16)))
+                   size_t(nblk) * (zst::kTabEnt + zst::kHufSlot) * 2 + 16)))
       return rc;
     if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_blit), &ctx->z_cap_blit, total + 64)))
       return rc;
@@ -2534,18 +2653,24 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
                    (size_t(nblk) + 1) * 8)))
       return rc;
     zb = reinterpret_cast<zst::ZBlk*>(ctx->z_zb);
+    uint16_t* htab = reinterpret_cast<uint16_t*>(ctx->z_tabs) + size_t(nblk) * zst::kTabEnt;
     // one workgroup per block (no per-workgroup scratch; OKV_ZSTD_PRO_GRID: A/B)
     const uint32_t pgrid = okv::knob("OKV_ZSTD_PRO_GRID") ? uint32_t(atoi(okv::knob("OKV_ZSTD_PRO_GRID")))
                                                        : nblk;
     hipLaunchKernelGGL(okv_zstd_pro_kernel, dim3(std::max(1u, std::min(nblk, pgrid))), dim3(64), 0, s,
                        seg, seg_bytes, descs, nblk, ctx->z_cap_off, ctx->z_dec, ctx->z_dec_len,
-                       ctx->z_status, ctx->z_blit, reinterpret_cast<uint16_t*>(ctx->z_tabs), zb,
+                       ctx->z_status, ctx->z_blit, reinterpret_cast<uint16_t*>(ctx->z_tabs), htab, zb,
                        pprof);
     hipLaunchKernelGGL(okv_zstd_seqoff_kernel, dim3(1), dim3(1024), 0, s, zb, nblk,
                        ctx->z_seq_off);
     uint64_t nseq_total = 0;
     OKV_HIP(hipMemcpyAsync(&nseq_total, ctx->z_seq_off + nblk, 8, hipMemcpyDeviceToHost, s));
-    OKV_HIP(hipStreamSynchronize(s));
+    if (!ctx->z_ev) OKV_HIP(hipEventCreateWithFlags(&ctx->z_ev, hipEventDisableTiming));
+    OKV_HIP(hipEventRecord(ctx->z_ev, s));
+    // the literal streams decode while the host reads the sequence count
+    hipLaunchKernelGGL(okv_zstd_huf_kernel, dim3((nblk + 15) / 16), dim3(64), 0, s, zb, nblk, htab, seg,
+                       ctx->z_blit, ctx->z_cap_off);
+    OKV_HIP(hipEventSynchronize(ctx->z_ev));
     if (prof) (void)hipEventRecord(ev[1], s);
     if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_seqs), &ctx->z_cap_seqs,
                    nseq_total * 8 + 64)))

@@ -37,6 +37,30 @@ constexpr uint32_t kChunkOut = 4096;     // output bytes per chunk covered by th
 constexpr uint32_t kChunkClose = 3072;   // a chunk takes no more sequences past this output
 
 enum : int32_t { kOK = 0, kErr = 1, kCap = 2, kSlow = 3, kDefer = 4 };
+#ifdef OKV_ABLATE
+// ablation build: every corrupt-input exit records its source line
+// (okv_debug_zstd_err; diagnostics only)
+__device__ int g_zerr[4];  // last line, count
+__device__ __forceinline__ int32_t zerr_at(int line) {
+  if ((threadIdx.x & 63) == 0) {
+    g_zerr[0] = line;
+    atomicAdd(&g_zerr[1], 1);
+  }
+  return kErr;
+}
+#define ZERR zerr_at(__LINE__)
+__device__ __forceinline__ int32_t zfail_at(int line, int32_t v) {
+  if ((threadIdx.x & 63) == 0) {
+    if (g_zerr[2] == 0) g_zerr[2] = line;  // the innermost failure (first recorded)
+    g_zerr[3] = line;
+  }
+  return v;
+}
+#define ZFAIL(v) zfail_at(__LINE__, (v))
+#else
+#define ZERR kErr
+#define ZFAIL(v) (v)
+#endif
 // kSlow: the prologue stage hands the block to the general kernel; kDefer: its
 // sequences are decoded by the lane-per-block stage and executed by the
 // parallel executor (okv_zstd_seq_kernel, okv_zstd_exec_kernel).
@@ -234,13 +258,13 @@ __device__ int32_t read_ncount(const uint8_t* p, int64_t n, int16_t* norm, uint3
   };
   const uint32_t al = peek(4) + 5;
   bit += 4;
-  if (al > max_al) return -1;
+  if (al > max_al) return ZFAIL(-1);
   int32_t remaining = (1 << al) + 1;
   int32_t threshold = 1 << al;
   uint32_t nbits = al + 1;
   uint32_t s = 0;
   while (remaining > 1) {
-    if (s > max_sym) return -1;
+    if (s > max_sym) return ZFAIL(-1);
     const int32_t max = 2 * threshold - 1 - remaining;
     int32_t count;
     const uint32_t v = peek(nbits);
@@ -260,7 +284,7 @@ __device__ int32_t read_ncount(const uint8_t* p, int64_t n, int16_t* norm, uint3
         const uint32_t r = peek(2);
         bit += 2;
         for (uint32_t k = 0; k < r; ++k) {
-          if (s > max_sym) return -1;
+          if (s > max_sym) return ZFAIL(-1);
           norm[s++] = 0;
         }
         if (r != 3) break;
@@ -270,9 +294,9 @@ __device__ int32_t read_ncount(const uint8_t* p, int64_t n, int16_t* norm, uint3
       --nbits;
       threshold >>= 1;
     }
-    if ((bit >> 3) > n) return -1;
+    if ((bit >> 3) > n) return ZFAIL(-1);
   }
-  if (remaining != 1) return -1;
+  if (remaining != 1) return ZFAIL(-1);
   al_out = al;
   nsym_out = s;
   return int32_t((bit + 7) >> 3);
@@ -315,7 +339,7 @@ __device__ bool build_fse(uint32_t* table, const int16_t* norm, uint32_t nsym, u
   const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
   s_cum[lane] = uint16_t(inc - c);
   __syncthreads();
-  if (int32_t(total) != high + 1) return false;
+  if (int32_t(total) != high + 1) return ZFAIL(false);
   const uint32_t step = (size >> 1) + (size >> 3) + 3;
   uint32_t carry = 0;
   for (uint32_t j0 = 0; j0 < size; j0 += 64) {
@@ -774,13 +798,13 @@ __device__ int32_t seq_table(SmemCore& sm, uint32_t* table, uint32_t mode, const
     case 0: {  // Predefined_Mode
       for (uint32_t s = threadIdx.x & 63; s < def_n; s += 64) sm.norm[s] = def[s];
       __syncthreads();
-      if (!build_fse(table, sm.norm, def_n, def_al, sm.next)) return -1;
+      if (!build_fse(table, sm.norm, def_n, def_al, sm.next)) return ZFAIL(-1);
       ok = true;
       al = def_al;
       return 0;
     }
     case 1: {  // RLE_Mode
-      if (n < 1 || p[0] > max_sym) return -1;
+      if (n < 1 || p[0] > max_sym) return ZFAIL(-1);
       build_rle(table, p[0]);
       ok = true;
       al = 0;
@@ -789,15 +813,31 @@ __device__ int32_t seq_table(SmemCore& sm, uint32_t* table, uint32_t mode, const
     case 2: {  // FSE_Compressed_Mode
       uint32_t nsym;
       const int32_t used = read_ncount(p, n, sm.norm, max_sym, max_al, al, nsym);
-      if (used < 0) return -1;
+      if (used < 0) return ZFAIL(-1);
       __syncthreads();
-      if (!build_fse(table, sm.norm, nsym, al, sm.next)) return -1;
+      if (!build_fse(table, sm.norm, nsym, al, sm.next)) return ZFAIL(-1);
       ok = true;
       return used;
     }
     default:  // Repeat_Mode
-      return ok ? 0 : -1;
+      return ok ? 0 : ZFAIL(-1);
   }
+}
+
+// seq_table as a real call, for the one-wave-per-block kernel: inlined into
+// okv_zstd_kernel (ROCm 7.2 clang, gfx950, -O3) the offset table came out
+// wrong for every block of the zstd test cases (OKV_BLK_ZSTD_ERROR at the OF
+// table) while the same source inlined into the prologue kernel decodes them;
+// any change of the inlined code's shape (a diagnostic store, -O2 elsewhere)
+// moved the failure, a call removes it.  tests/test_zstd_gpu.py::test_zstd_cases
+// [one_pass-*] is the check.
+__device__ __attribute__((noinline)) int32_t seq_table_call(SmemCore& sm, uint32_t* table,
+                                                           uint32_t mode, const int16_t* def,
+                                                           uint32_t def_al, uint32_t def_n,
+                                                           uint32_t max_sym, uint32_t max_al,
+                                                           const uint8_t* p, int64_t n, bool& ok,
+                                                           uint32_t& al) {
+  return seq_table(sm, table, mode, def, def_al, def_n, max_sym, max_al, p, n, ok, al);
 }
 
 // Decompress one compressed zstd block (RFC 8878 3.1.1.3) into the output.
@@ -809,7 +849,7 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
   o.pos = rfl64(o.pos);
   o.cap = rfl64(o.cap);
   o.frame0 = rfl64(o.frame0);
-  if (n < 1) return kErr;
+  if (n < 1) return ZERR;
   // the block's output may not exceed Block_Maximum_Size (RFC 8878 3.1.1.2.4)
   const uint64_t blk_end = o.pos + rfl(o.bmax);
   const long long t0 = o.prof ? clock64() : 0;
@@ -822,31 +862,31 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       regen = b0 >> 3;
       hdr = 1;
     } else if (sf == 1) {
-      if (n < 2) return kErr;
+      if (n < 2) return ZERR;
       regen = (b0 >> 4) + (uint32_t(p[1]) << 4);
       hdr = 2;
     } else {
-      if (n < 3) return kErr;
+      if (n < 3) return ZERR;
       regen = (b0 >> 4) + (uint32_t(p[1]) << 4) + (uint32_t(p[2]) << 12);
       hdr = 3;
     }
   } else {
     if (sf <= 1) {
-      if (n < 3) return kErr;
+      if (n < 3) return ZERR;
       const uint32_t h = b0 | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16);
       regen = (h >> 4) & 0x3ff;
       csize = (h >> 14) & 0x3ff;
       hdr = 3;
       nstreams = sf == 0 ? 1 : 4;
     } else if (sf == 2) {
-      if (n < 4) return kErr;
+      if (n < 4) return ZERR;
       const uint32_t h = b0 | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
       regen = (h >> 4) & 0x3fff;
       csize = h >> 18;
       hdr = 4;
       nstreams = 4;
     } else {
-      if (n < 5) return kErr;
+      if (n < 5) return ZERR;
       const uint64_t h = uint64_t(b0) | (uint64_t(p[1]) << 8) | (uint64_t(p[2]) << 16) |
                          (uint64_t(p[3]) << 24) | (uint64_t(p[4]) << 32);
       regen = uint32_t((h >> 4) & 0x3ffff);
@@ -855,22 +895,22 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       nstreams = 4;
     }
   }
-  if (regen > kBlockMax) return kErr;
+  if (regen > kBlockMax) return ZERR;
   const uint8_t* lits = nullptr;  // literal source for the sequences
   uint8_t rle_byte = 0;
   bool rle = false;
   int64_t at = hdr;
   if (ltype == 0) {  // Raw_Literals_Block
-    if (at + regen > n) return kErr;
+    if (at + regen > n) return ZERR;
     lits = p + at;
     at += regen;
   } else if (ltype == 1) {  // RLE_Literals_Block
-    if (at + 1 > n) return kErr;
+    if (at + 1 > n) return ZERR;
     rle_byte = p[at];
     rle = true;
     at += 1;
   } else {  // Compressed / Treeless
-    if (at + csize > n) return kErr;
+    if (at + csize > n) return ZERR;
     if constexpr (PRO) {
       if (regen > pro->lit_cap) return kSlow;  // per-block scratch too small: general kernel
       lit_buf = pro->lit_blk;
@@ -882,13 +922,13 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       const long long th = o.prof ? clock64() : 0;
       const int32_t used = read_huf_tree(sm, q, qn, mb);
       if (o.prof) prof_add(o, 12, clock64() - th);
-      if (used < 0) return kErr;
+      if (used < 0) return ZERR;
       fs.huf_ok = true;
       fs.huf_bits = mb;
       q += used;
       qn -= used;
     } else if (!fs.huf_ok) {
-      return kErr;
+      return ZERR;
     }
     const int lane = threadIdx.x & 63;
     if constexpr (PRO) {
@@ -900,12 +940,12 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       if (pro->deferrable && at + int64_t(csize) < n && p[at + csize] != 0) {
         const uint32_t mb = fs.huf_bits;
         if (nstreams == 4) {
-          if (qn < 6) return kErr;
+          if (qn < 6) return ZERR;
           const uint32_t s1 = q[0] | (uint32_t(q[1]) << 8), s2 = q[2] | (uint32_t(q[3]) << 8),
                          s3 = q[4] | (uint32_t(q[5]) << 8);
           const int64_t s4 = qn - 6 - int64_t(s1) - s2 - s3;
-          if (s4 < 0) return kErr;
-          if (3 * ((regen + 3) / 4) > regen) return kErr;
+          if (s4 < 0) return ZERR;
+          if (3 * ((regen + 3) / 4) > regen) return ZERR;
           pro->hq = q + 6;
           pro->hlen[0] = s1;
           pro->hlen[1] = s2;
@@ -931,13 +971,13 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
     if (nstreams == 1) {
       if (lane == 0) good = huf_stream(sm.huf, fs.huf_bits, q, qn, lit_buf, regen);
     } else {
-      if (qn < 6) return kErr;
+      if (qn < 6) return ZERR;
       const uint32_t s1 = q[0] | (uint32_t(q[1]) << 8), s2 = q[2] | (uint32_t(q[3]) << 8),
                      s3 = q[4] | (uint32_t(q[5]) << 8);
       const int64_t s4 = qn - 6 - int64_t(s1) - s2 - s3;
-      if (s4 < 0) return kErr;
+      if (s4 < 0) return ZERR;
       const uint32_t seg = (regen + 3) / 4;
-      if (3 * seg > regen) return kErr;
+      if (3 * seg > regen) return ZERR;
       if (lane < 4) {
         const int64_t off = 6 + (lane > 0 ? s1 : 0) + (lane > 1 ? s2 : 0) + (lane > 2 ? s3 : 0);
         const int64_t len = lane == 0 ? s1 : lane == 1 ? s2 : lane == 2 ? s3 : s4;
@@ -946,7 +986,7 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       }
     }
     // every lane must agree the streams decoded cleanly
-    if (__any(!good)) return kErr;
+    if (__any(!good)) return ZERR;
     __builtin_amdgcn_s_waitcnt(0);
     __threadfence_block();
     lits = lit_buf;
@@ -956,16 +996,16 @@ sequences:
   const long long t1 = o.prof ? clock64() : 0;
   prof_add(o, 0, t1 - t0);
   // ---- sequences section (3.1.1.3.2)
-  if (at >= n) return kErr;
+  if (at >= n) return ZERR;
   uint32_t nseq = p[at];
   if (nseq < 128) {
     at += 1;
   } else if (nseq < 255) {
-    if (at + 2 > n) return kErr;
+    if (at + 2 > n) return ZERR;
     nseq = ((nseq - 128) << 8) + p[at + 1];
     at += 2;
   } else {
-    if (at + 3 > n) return kErr;
+    if (at + 3 > n) return ZERR;
     nseq = p[at + 1] + (uint32_t(p[at + 2]) << 8) + 0x7f00;
     at += 3;
   }
@@ -987,7 +1027,7 @@ sequences:
     return true;
   };
   if (nseq == 0) {  // literals only (bytes after the header are not read, as libzstd)
-    if (o.pos + lit_left > blk_end) return kErr;
+    if (o.pos + lit_left > blk_end) return ZERR;
     if (o.pos + lit_left > o.cap) return kCap;
     emit_lits(lit_left);
     return kOK;
@@ -995,23 +1035,24 @@ sequences:
   if constexpr (PRO) {
     if (!pro->deferrable) return kSlow;
   }
-  if (at >= n) return kErr;
+  if (at >= n) return ZERR;
   const uint32_t modes = p[at++];
-  if (modes & 3) return kErr;  // reserved bits
+  if (modes & 3) return ZERR;  // reserved bits
   int32_t used;
-  used = seq_table(sm, sm.ll, modes >> 6, LL_DEF, 6, 36, 35, kLLMaxAL, p + at, n - at, fs.ll_ok,
-                   fs.ll_al);
-  if (used < 0) return kErr;
+  // (the one-pass kernel calls the table builds, see seq_table_call)
+  auto table = [&](auto&&... a) { return PRO ? seq_table(sm, a...) : seq_table_call(sm, a...); };
+  used = table(sm.ll, modes >> 6, LL_DEF, 6, 36, 35, kLLMaxAL, p + at, n - at, fs.ll_ok, fs.ll_al);
+  if (used < 0) return ZERR;
   at += used;
   if ((modes >> 6) != 3) seq_xbits(sm.ll, fs.ll_al, 0);
-  used = seq_table(sm, sm.of, (modes >> 4) & 3, OF_DEF, 5, 29, 31, kOFMaxAL, p + at, n - at,
-                   fs.of_ok, fs.of_al);
-  if (used < 0) return kErr;
+  used = table(sm.of, (modes >> 4) & 3, OF_DEF, 5, 29, 31, kOFMaxAL, p + at, n - at, fs.of_ok,
+               fs.of_al);
+  if (used < 0) return ZERR;
   at += used;
   if (((modes >> 4) & 3) != 3) seq_xbits(sm.of, fs.of_al, 1);
-  used = seq_table(sm, sm.ml, (modes >> 2) & 3, ML_DEF, 6, 53, 52, kMLMaxAL, p + at, n - at,
-                   fs.ml_ok, fs.ml_al);
-  if (used < 0) return kErr;
+  used = table(sm.ml, (modes >> 2) & 3, ML_DEF, 6, 53, 52, kMLMaxAL, p + at, n - at, fs.ml_ok,
+               fs.ml_al);
+  if (used < 0) return ZERR;
   at += used;
   if (((modes >> 2) & 3) != 3) seq_xbits(sm.ml, fs.ml_al, 2);
   if (o.prof) prof_add(o, 10, clock64() - t1);
@@ -1059,7 +1100,7 @@ sequences:
   fs.rep1 = rfl(fs.rep1);
   fs.rep2 = rfl(fs.rep2);
   SeqBits br;
-  if (!seqbits_init(br, p + at, n - at)) return kErr;
+  if (!seqbits_init(br, p + at, n - at)) return ZERR;
   uint32_t sll = seqbits_read(br, fs.ll_al);
   uint32_t sof = seqbits_read(br, fs.of_al);
   uint32_t sml = seqbits_read(br, fs.ml_al);
@@ -1090,7 +1131,7 @@ sequences:
     const uint32_t lit_done = uint32_t(lit_pos);
     uint32_t cnt = 0, lsum = 0, osum = 0;
     for (; cnt < kSeqChunk && i < nseq && osum < kChunkClose; ++cnt, ++i) {
-      if (br.pos < 0) return kErr;  // libzstd: the stream overflowed before this sequence
+      if (br.pos < 0) return ZERR;  // libzstd: the stream overflowed before this sequence
       const uint32_t ell = rfl(sm.ll[sll]), eof = rfl(sm.of[sof]), eml = rfl(sm.ml[sml]);
       // extra bits: offset, then match length, then literals length
       seqbits_reload(br, 47);  // offset (<= 31) + match length (<= 16) extra bits
@@ -1119,10 +1160,10 @@ sequences:
         sof = fse_base(eof) + seqbits_take(br, fse_nb(eof));
       }
       // execution checks (3.1.1.4): literals available, match inside the frame
-      if (lsum + ll > lit_lim - lit_done) return kErr;
+      if (lsum + ll > lit_lim - lit_done) return ZERR;
       const uint32_t mstart = osum + ll;  // relative to o.pos
-      if (mstart + ml > bm_lim) return kErr;  // the block outgrows Block_Maximum_Size
-      if (off > back + mstart) return kErr;  // before the frame start (no dictionary)
+      if (mstart + ml > bm_lim) return ZERR;  // the block outgrows Block_Maximum_Size
+      if (off > back + mstart) return ZERR;  // before the frame start (no dictionary)
       if (mstart + ml > cap_lim) return kCap;  // (the retry pass sizes the output exactly)
       if (w0) sm.rec[cnt] = make_uint4(ll, ml, uint32_t(off), 0);
       lsum += ll;
@@ -1262,10 +1303,10 @@ sequences:
   fs.rep0 = rep0;
   fs.rep1 = rep1;
   fs.rep2 = rep2;
-  if (br.pos > 0) return kErr;  // unread bits: corrupt (an over-read on the last one passes)
+  if (br.pos > 0) return ZERR;  // unread bits: corrupt (an over-read on the last one passes)
   if (o.prof) prof_add(o, 1, clock64() - t1);
   prof_add(o, 4, nseq);
-  if (o.pos + lit_left > blk_end) return kErr;
+  if (o.pos + lit_left > blk_end) return ZERR;
   if (o.pos + lit_left > o.cap) return kCap;
   emit_lits(lit_left);
   return kOK;
@@ -1333,40 +1374,40 @@ __device__ int32_t decode_frames(SM& sm, const uint8_t* src, int64_t n, Out& o, 
   int64_t at = 0;
   bool first_frame = true;
   while (at < n) {
-    if (n - at < 4) return kErr;
+    if (n - at < 4) return ZERR;
     const uint32_t magic = ld32z(src, at, n);
     if ((magic & 0xfffffff0u) == 0x184d2a50u) {  // skippable frame (3.1.2)
-      if (n - at < 8) return kErr;
+      if (n - at < 8) return ZERR;
       const uint64_t sz = ld32z(src, at + 4, n);
-      if (uint64_t(n - at - 8) < sz) return kErr;
+      if (uint64_t(n - at - 8) < sz) return ZERR;
       at += 8 + int64_t(sz);
       continue;
     }
-    if (magic != 0xfd2fb528u) return kErr;
+    if (magic != 0xfd2fb528u) return ZERR;
     at += 4;
-    if (at >= n) return kErr;
+    if (at >= n) return ZERR;
     const uint32_t fhd = src[at++];
     const uint32_t fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, reserved = (fhd >> 3) & 1;
     const uint32_t has_csum = (fhd >> 2) & 1, did_flag = fhd & 3;
-    if (reserved) return kErr;
+    if (reserved) return ZERR;
     uint64_t window = 0;
     if (!single) {  // Window_Descriptor (3.1.1.1.2)
-      if (at >= n) return kErr;
+      if (at >= n) return ZERR;
       const uint32_t wd = src[at++];
       const uint32_t wlog = 10 + (wd >> 3);
       // libzstd: windowLog above ZSTD_WINDOWLOG_MAX (31 on 64-bit hosts) is
       // frameParameter_windowTooLarge
-      if (wlog > 31) return kErr;
+      if (wlog > 31) return ZERR;
       window = (uint64_t(1) << wlog) + ((uint64_t(1) << wlog) / 8) * (wd & 7);
     }
     const uint32_t did_size = did_flag == 0 ? 0 : did_flag == 1 ? 1 : did_flag == 2 ? 2 : 4;
-    if (at + did_size > n) return kErr;
+    if (at + did_size > n) return ZERR;
     uint32_t did = 0;
     for (uint32_t k = 0; k < did_size; ++k) did |= uint32_t(src[at + k]) << (8 * k);
     at += did_size;
-    if (did != 0) return kErr;  // no dictionaries are registered with the reader
+    if (did != 0) return ZERR;  // no dictionaries are registered with the reader
     const uint32_t fcs_size = fcs_flag == 0 ? (single ? 1 : 0) : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8;
-    if (at + fcs_size > n) return kErr;
+    if (at + fcs_size > n) return ZERR;
     uint64_t fcs = 0;
     for (uint32_t k = 0; k < fcs_size; ++k) fcs |= uint64_t(src[at + k]) << (8 * k);
     if (fcs_size == 2) fcs += 256;
@@ -1383,19 +1424,19 @@ __device__ int32_t decode_frames(SM& sm, const uint8_t* src, int64_t n, Out& o, 
     o.frame0 = o.pos;
     bool first_block = true;
     for (;;) {  // blocks (3.1.1.2)
-      if (n - at < 3) return kErr;
+      if (n - at < 3) return ZERR;
       const uint32_t bh = src[at] | (uint32_t(src[at + 1]) << 8) | (uint32_t(src[at + 2]) << 16);
       at += 3;
       const uint32_t last = bh & 1, btype = (bh >> 1) & 3, bsize = bh >> 3;
       if (btype == 0) {  // Raw_Block
-        if (int64_t(bsize) > n - at) return kErr;
-        if (bsize > o.bmax) return kErr;  // Block_Size > Block_Maximum_Size (3.1.1.2.3)
+        if (int64_t(bsize) > n - at) return ZERR;
+        if (bsize > o.bmax) return ZERR;  // Block_Size > Block_Maximum_Size (3.1.1.2.3)
         if (o.pos + bsize > o.cap) return kCap;
         out_copy(o, src + at, bsize);
         at += bsize;
       } else if (btype == 1) {  // RLE_Block
-        if (at >= n) return kErr;
-        if (bsize > o.bmax) return kErr;
+        if (at >= n) return ZERR;
+        if (bsize > o.bmax) return ZERR;
         if (o.pos + bsize > o.cap) return kCap;
         const uint8_t v = src[at];
         const int lane = threadIdx.x & 63;
@@ -1404,7 +1445,7 @@ __device__ int32_t decode_frames(SM& sm, const uint8_t* src, int64_t n, Out& o, 
         o.pos += bsize;
         at += 1;
       } else if (btype == 2) {  // Compressed_Block (libzstd: < 128 KiB)
-        if (int64_t(bsize) > n - at || bsize >= kBlockMax) return kErr;
+        if (int64_t(bsize) > n - at || bsize >= kBlockMax) return ZERR;
         if constexpr (PRO) {
           // deferrable: the input is exactly one frame holding this one block
           pro->deferrable = first_frame && first_block && last &&
@@ -1419,20 +1460,20 @@ __device__ int32_t decode_frames(SM& sm, const uint8_t* src, int64_t n, Out& o, 
         if (r != kOK) return r;
         at += bsize;
       } else {
-        return kErr;  // reserved block type
+        return ZERR;  // reserved block type
       }
       first_block = false;
       if (last) break;
     }
     first_frame = false;
-    if (fcs_size && o.pos - o.frame0 != fcs) return kErr;  // Frame_Content_Size check
+    if (fcs_size && o.pos - o.frame0 != fcs) return ZERR;  // Frame_Content_Size check
     if (has_csum) {
-      if (n - at < 4) return kErr;
+      if (n - at < 4) return ZERR;
       if (!o.dry) {  // (content-dependent: checked by the retry's producing pass)
         commit(o);
         const uint32_t want = ld32z(src, at, n);
         const uint64_t h = xxh64_out(o.base + o.frame0, o.pos - o.frame0);
-        if (uint32_t(h) != want) return kErr;
+        if (uint32_t(h) != want) return ZERR;
       }
       at += 4;
     }
@@ -2740,3 +2781,19 @@ void launch_zstd_desc(hipStream_t s, const Desc* descs, uint32_t nblk, const uin
 }
 
 }  // namespace okv
+
+#ifdef OKV_ABLATE
+// Diagnostic: the last corrupt-input exit's source line and the exit count
+// since the previous call (then reset).
+extern "C" int okv_debug_zstd_err(int* out2) {
+  int h[4] = {};
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(okv::zst::g_zerr), sizeof(h)) != hipSuccess) return -1;
+  out2[0] = h[0];
+  out2[1] = h[1];
+  out2[2] = h[2];
+  out2[3] = h[3];
+  int z[4] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(okv::zst::g_zerr), z, sizeof(z));
+  return 0;
+}
+#endif

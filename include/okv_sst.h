@@ -136,9 +136,6 @@ okv_ctx *okv_open_on_stream(int device, void *stream);
 #define OKV_OPEN_ZSTD_ONE_PASS 2u /* zstd blocks: the one-wave-per-block decoder for every block
                                      (one launch, no host synchronisation between stages: lower
                                      latency for a few blocks); outputs identical */
-#define OKV_OPEN_NO_PIECES 4u     /* large-block decodes (>= 8192 blocks) as one header walk and
-                                     one tile pass, instead of two pieces whose second walk runs on
-                                     a second stream under the first tile pass; outputs identical */
 typedef struct okv_open_opts {
   uint32_t size;  /* sizeof(okv_open_opts) */
   uint32_t flags; /* OKV_OPEN_* */
@@ -387,8 +384,8 @@ int okv_profile_read(okv_ctx *ctx, double *ms, uint64_t *calls);
 #define OKV_PATH_ZSTD 128u  /* the zstd stage ran first */
 #define OKV_PATH_STREAM 1024u   /* okv_decode_stream_kernel: passes 1-3 in one launch for any
                                      batch of small blocks (prefix by decoupled look-back) */
-#define OKV_PATH_ENC_ONEPASS 512u /* okv_encode_rows: the single-pass plan (okv_enc_plan_kernel);
-                                     clear: the general E1-E9 kernels (a block > 256 rows) */
+#define OKV_PATH_ENC_ONEPASS 512u /* okv_encode_rows used the single-pass plan kernel: ablation
+                                     builds only (OKV_ENC_ONEPASS=1); the product runs E1-E9 */
 #define OKV_PATH_ZSTD_REGROW 256u /* zstd frames outgrew their first output region and were
                                      measured and decoded again (io.Copy inflates them all) */
 uint32_t okv_last_path(const okv_ctx *ctx);

@@ -66,9 +66,9 @@ struct okv_ctx {
   size_t f_cap = 0;
   okv::Totals* d_tot = nullptr;
   okv::Totals* h_tot = nullptr;  // pinned
-  // large-block decodes in two pieces (decode_device): the second piece's
-  // header walk on stream2 under the first piece's tile pass
-  bool no_pieces = false;          // OKV_OPEN_NO_PIECES: one walk, one tile pass
+  // ablation build (OKV_DECODE_PIECES=1): large-block decodes in two pieces,
+  // the second piece's header walk on stream2 under the first's tile pass
+  bool pieces = false;
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_piece[2] = {nullptr, nullptr};
   okv::Totals* d_tot2 = nullptr;   // totals of the first piece

@@ -1898,7 +1898,13 @@ int ensure_fused(okv_ctx* ctx, uint32_t nblk) {
   return OKV_OK;
 }
 
-// Large-block decodes run in two pieces: the header walk of the first
+#ifdef OKV_ABLATE
+// Ablation build only (OKV_DECODE_PIECES=1): large-block decodes in two
+// pieces.  Measured at C3 (r4b, 3 alternating runs): count+scan 0.061 vs
+// 0.105 ms but the two tile launches 1.487 vs 1.384 ms, step 1.55 vs 1.48 ms:
+// the first piece's walk costs what the whole walk does (latency-bound), and
+// the second launch adds a tail.  The product decodes in one piece.
+// The header walk of the first
 // kPieceDiv-th of the blocks, then the tile pass over them on the context's
 // stream while the second piece's walk runs on a second stream; the second
 // tile pass waits for that walk.  The walk is latency-bound (a dependent
@@ -1971,6 +1977,7 @@ CopyParams piece_params(const CopyParams& P, uint32_t b0, uint32_t n) {
   Q.blk_status = P.blk_status + b0;
   return Q;
 }
+#endif  // OKV_ABLATE
 
 int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
                   uint32_t nblk, int comp, okv_decode_out* o, uint32_t flags) {
@@ -2012,14 +2019,18 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   }
   if ((rc = ensure_blocks(ctx, nblk))) return rc;
   uint32_t* const big_count = big_counter(ctx);  // this decode's slot (launch_plan flips it)
-  const uint32_t b0 = tile && !ctx->no_pieces ? piece_split(nblk) : 0u;
+#ifdef OKV_ABLATE
+  const uint32_t b0 = tile && ctx->pieces ? piece_split(nblk) : 0u;
+#endif
   if (fused || stream) {
     if ((rc = ensure_fused(ctx, nblk))) return rc;
     prof_mark(ctx, 2);
     prof_mark(ctx, 3);
+#ifdef OKV_ABLATE
   } else if (b0) {
     rc = launch_plan_pieces(ctx, w, nblk, b0, o->row_start, rt_kl, geo.span_cap);
     if (rc) return rc;
+#endif
   } else {
     rc = launch_plan(ctx, w, nblk, o->row_start, true, rt_kl, geo.span_cap);
     if (rc) return rc;
@@ -2119,13 +2130,14 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
         if ((rc = grow(ctx, &ctx->d_vsrc, &ctx->cap_vsrc, n))) return rc;
         P.vsrc = static_cast<uint64_t*>(ctx->d_vsrc);
       }
+#ifdef OKV_ABLATE
       if (b0) {  // the first piece's tile pass, then the second's after its walk
         launch_tile(ctx, piece_params(P, 0, b0), geo);
         OKV_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_piece[1], 0));
         launch_tile(ctx, piece_params(P, b0, nblk - b0), geo);
-      } else {
+      } else
+#endif
         launch_tile(ctx, P, geo);
-      }
     }
 #ifdef OKV_ABLATE
     else if (sweep) {
@@ -2338,7 +2350,6 @@ okv_ctx* okv_open_ex(int device, void* stream, const okv_open_opts* opts) {
   okv_ctx* ctx = okv_open_on_stream(device, stream);
   if (ctx && opts) {
     if (opts->flags & OKV_OPEN_NO_FUSED) ctx->fused = false;
-    if (opts->flags & OKV_OPEN_NO_PIECES) ctx->no_pieces = true;
     ctx->zstd_one_pass = (opts->flags & OKV_OPEN_ZSTD_ONE_PASS) != 0;
   }
   return ctx;
@@ -2376,6 +2387,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   }
   if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
   if (const char* v = getenv("OKV_DECODE_FUSED")) ctx->fused = atoi(v) != 0;
+  if (const char* v = getenv("OKV_DECODE_PIECES")) ctx->pieces = atoi(v) != 0;
   if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
   if (const char* v = getenv("OKV_VALUE_SWEEP")) {
     ctx->value_sweep = uint32_t(atoi(v));

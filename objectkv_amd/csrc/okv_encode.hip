@@ -653,6 +653,11 @@ __device__ __forceinline__ void put_bytes(uint8_t* p, const uint8_t* s, uint64_t
   for (uint64_t i = 0; i < n; ++i) p[i] = s[i];
 }
 
+#ifdef OKV_ABLATE
+// Ablation build only (OKV_ENC_ONEPASS=1).  Measured at C4 (100 M rows, 48 828
+// chunks): 17.5 ms for the plan vs 1.27 ms for E1-E9 -- the inclusive state
+// crosses one chunk per cross-XCD hand-off (~360 ns), a serial frontier; the
+// product keeps E1-E9's pointer doubling (profiles/r4/c4_arms.log).
 // ---------------------------------------------------------------------------
 // EP: E1-E9 in one launch, for the common shape (no block longer than
 // kFuseLook rows).  One workgroup per chunk of kETile rows, chunks claimed in
@@ -989,6 +994,7 @@ __global__ __launch_bounds__(kThreads) void okv_enc_plan_kernel(PlanParams P) {
     }
   }
 }
+#endif  // OKV_ABLATE
 
 // ---------------------------------------------------------------------------
 // E10: pack.  One workgroup per block; lane l of a pass owns destination
@@ -1317,10 +1323,13 @@ __device__ __forceinline__ void lds_copy_field(uint32_t* img, uint32_t d, const 
   }
 }
 
-template <uint32_t IMG, int V = 0>  // V: diagnostic ablation (OKV_ENC_VARIANT 4: no hash,
+template <uint32_t IMG, int V = 0, bool kMeta = false>  // V: diagnostic ablation (OKV_ENC_VARIANT 4: no hash,
                                    // 5: headers only, 6: loads without LDS writes;
                                    // 7: row positions by a workgroup scan, no pl reads (the product);
                                    // 8: 7 with registers capped for 8 waves)
+                                   // kMeta (ablation, OKV_ENC_META_FUSED=1): the meta index
+                                   // entries written here too (measured slower: 5.16-5.30
+                                   // vs 4.31-4.39 ms pack, + 0.23 ms meta kernel saved)
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(V == 8 ? 8 : 1)))
 void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
   // V == 7, the product form (70 registers, 7 waves per SIMD); V == 8
@@ -1352,9 +1361,11 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
       blen[t] = uint32_t(dt.block_size);
       slim[t] = uint32_t(dt.offset - O0 + (dt.block_size & ~uint64_t(31)));
       orig = dt.original_size;
-      borig[t] = orig;
-      bcsz[t] = dt.compressed_size;
-      if (P.meta) bmoff[t] = P.moff[k0 + t];
+      if constexpr (kMeta) {
+        borig[t] = orig;
+        bcsz[t] = dt.compressed_size;
+        bmoff[t] = P.moff[k0 + t];
+      }
     }
     // each block's start in the region's row stream: the OriginalSizes before it
     const uint64_t incl = wave_incl_scan(orig, int(t));
@@ -1402,7 +1413,7 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
       else
         hi = m;
     }
-    if (r == bfirst[lo]) bfkl[lo] = kl;
+    if (kMeta && r == bfirst[lo]) bfkl[lo] = kl;
     const uint32_t d = VL == 7 ? uint32_t(brel[lo] + srel - (bbase[lo] - bbase[0]))
                               : uint32_t(brel[lo] + Pg(P.pl, P.tp, int64_t(r) - 1) - bbase[lo]);
     if (VL == 5) {
@@ -1451,7 +1462,7 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
       else
         hi = m;
     }
-    if (P.meta) {  // FirstKey bytes of the block's meta entry (block_stat.go:31-33)
+    if constexpr (kMeta) {  // FirstKey bytes of the block's meta entry (block_stat.go:31-33)
       const uint32_t ks = uint32_t(brel[lo]) + 6, ke = ks + bfkl[lo];
       const uint32_t a0 = max(p, ks), a1 = min(p + 16, ke);
       uint8_t* m = P.meta + bmoff[lo] + 2 - ks;
@@ -1526,7 +1537,7 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
       h *= XP3;
       h ^= h >> 32;
       P.hash[k0 + b] = h;
-      if (P.meta) {  // the rest of the entry: u16 len(FirstKey), then 5 x u64 (:27-42)
+      if constexpr (kMeta) {  // the rest of the entry: u16 len(FirstKey), then 5 x u64 (:27-42)
         uint8_t* m = P.meta + bmoff[b];
         const uint32_t kl = bfkl[b];
         put_le(m, kl, 2);
@@ -1882,6 +1893,7 @@ int enc_row_prefix(okv_ctx* ctx, EncScratch* e, const DevRows& R, uint64_t T) {
   return OKV_OK;
 }
 
+#ifdef OKV_ABLATE  // A/B arm OKV_ENC_ONEPASS=1 (the single-pass plan, measured slower)
 // E1-E9 in one launch (okv_enc_plan_kernel).  *general = true when the shape
 // needs the general kernels (a block longer than kFuseLook rows): the caller
 // then runs enc_plan.
@@ -1969,6 +1981,7 @@ int enc_plan_fast(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encod
   }
   return set_err(ctx, OKV_E_HIP, "encode: plan capacity");
 }
+#endif  // OKV_ABLATE
 
 // Block boundaries, BlockStat sizes/offsets and meta layout (E1-E9).
 int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opts& o, Plan* pl,
@@ -2078,8 +2091,12 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   const bool lds = aligned && GL >= 1 && pl.avg_rec <= 512;
   int rc;
 #ifdef OKV_ABLATE
-  (void)lds;
-  if ((rc = enc_row_prefix(ctx, e, R, o.threshold_bytes))) return rc;  // any arm may read it
+  // OKV_ENC_META_FUSED=1: the product arm (meta entries written by the pack kernel)
+  const bool meta_fused = okv::knob("OKV_ENC_META_FUSED") && atoi(okv::knob("OKV_ENC_META_FUSED"));
+  const char* evar0 = okv::knob("OKV_ENC_VARIANT");
+  if (!(lds && (evar0 ? atoi(evar0) : 7) == 7 && !okv::knob("OKV_ENC_IMAGE")) &&
+      (rc = enc_row_prefix(ctx, e, R, o.threshold_bytes)))
+    return rc;  // the arms that read it
 #else
   if (!lds && (rc = enc_row_prefix(ctx, e, R, o.threshold_bytes))) return rc;
 #endif
@@ -2122,12 +2139,17 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
       hipLaunchKernelGGL(okv_enc_pack_lds_kernel<12288>, dim3(ceil_div(pl.nb, GLa)),
                          dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GLa));
     else if (EV >= 4 && EV <= 9) {
-      auto* kern = EV == 4   ? okv_enc_pack_lds_kernel<kImage, 4>
+      void (*kern)(PackParams, uint64_t, uint32_t) = EV == 4   ? okv_enc_pack_lds_kernel<kImage, 4>
                    : EV == 5 ? okv_enc_pack_lds_kernel<kImage, 5>
                    : EV == 6 ? okv_enc_pack_lds_kernel<kImage, 6>
                    : EV == 8 ? okv_enc_pack_lds_kernel<kImage, 8>
                    : EV == 9 ? okv_enc_pack_lds_kernel<kImage, 9>
                              : okv_enc_pack_lds_kernel<kImage, 7>;
+      if (EV == 7 && meta_fused) {
+        pp.meta = seg + pl.data_bytes;
+        meta_done = true;
+        kern = okv_enc_pack_lds_kernel<kImage, 7, true>;
+      }
       hipLaunchKernelGGL(kern, dim3(ceil_div(pl.nb, GLa)), dim3(kThreads), 0, ctx->stream, pp,
                          pl.nb, uint32_t(GLa));
     } else
@@ -2148,11 +2170,10 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
                          uint32_t(G));
 #else
   if (lds) {
-    // small records: record-major LDS assembly, hashes and meta index entries fused
-    pp.meta = seg + pl.data_bytes;
+    // small records: record-major LDS assembly and the block hashes
     hipLaunchKernelGGL((okv_enc_pack_lds_kernel<kImage, 7>), dim3(ceil_div(pl.nb, GL)),
                        dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
-    hashed = meta_done = true;
+    hashed = true;
   } else if (aligned && G >= 1) {
     // large records: chunk-major regions
     hipLaunchKernelGGL(okv_enc_pack_region_kernel<0>, dim3(ceil_div(pl.nb, G)), dim3(kThreads), 0,
@@ -2385,8 +2406,15 @@ int okv_encode_rows(okv_ctx* ctx, const okv_rows* rows, const okv_encode_opts* o
   }
   Plan pl;
   uint64_t bad = kNone;
-  bool general = false;
-  rc = enc_plan_fast(ctx, e, R, *opts, &pl, &bad, &general);
+  // the cut, sizes and offsets: E1-E9 (pointer doubling over chunks)
+  bool general = true;
+#ifdef OKV_ABLATE
+  // A/B (OKV_ENC_ONEPASS=1): the single-pass plan kernel, falling back to E1-E9
+  if (okv::knob("OKV_ENC_ONEPASS") && atoi(okv::knob("OKV_ENC_ONEPASS")))
+    rc = enc_plan_fast(ctx, e, R, *opts, &pl, &bad, &general);
+  else
+#endif
+    rc = OKV_OK, enc_mark(ctx, e, 0);
   if (!rc && general) rc = enc_plan(ctx, e, R, *opts, &pl, &bad);
   ctx->last_path = general ? 0u : OKV_PATH_ENC_ONEPASS;
   if (rc == OKV_W_INVALID_KEY) out->bad_row = bad;

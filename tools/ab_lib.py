@@ -4,7 +4,7 @@ so that both builds see the same box).
 
 usage: python tools/ab_lib.py <path to libokv_sst*.so> [label]
 env:   ABL_NBLK (65536), ABL_ROUNDS (5), ABL_STEPS (10), ABL_KIND (1), ABL_BS (65536),
-       ABL_TH (57344), ABL_FLAGS (okv_open_opts.flags, 0; e.g. 4 = OKV_OPEN_NO_PIECES)
+       ABL_TH (57344), ABL_FLAGS (okv_open_opts.flags, 0)
 Prints one JSON line: per-pass ms (HIP events, median over rounds), the
 one-at-a-time decode step (host clock, median) and its roofline fraction.
 """

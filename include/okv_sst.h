@@ -382,8 +382,9 @@ int okv_profile_read(okv_ctx *ctx, double *ms, uint64_t *calls);
 #define OKV_PATH_BIG 64u    /* okv_copy_kernel / okv_index_kernel for big blocks (always
                                launched after a non-fused pass; exits when none) */
 #define OKV_PATH_ZSTD 128u  /* the zstd stage ran first */
-#define OKV_PATH_STREAM 1024u   /* okv_decode_stream_kernel: passes 1-3 in one launch for any
-                                     batch of small blocks (prefix by decoupled look-back) */
+#define OKV_PATH_STREAM 1024u   /* okv_decode_stream_kernel (ablation builds only,
+                                     OKV_DECODE_STREAM=1): passes 1-3 in one launch for any batch
+                                     of small blocks, prefix by decoupled look-back */
 #define OKV_PATH_ENC_ONEPASS 512u /* okv_encode_rows used the single-pass plan kernel: ablation
                                      builds only (OKV_ENC_ONEPASS=1); the product runs E1-E9 */
 #define OKV_PATH_ZSTD_REGROW 256u /* zstd frames outgrew their first output region and were

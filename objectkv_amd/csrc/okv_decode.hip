@@ -1073,7 +1073,7 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 // kLB: the form for batches of any size (okv_decode_stream_kernel below):
 // the exclusive prefix by a decoupled look-back instead of the last arrival's
 // scan, so no block waits for blocks that may not be resident.
-template <bool kLB>
+template <bool kLB>  // (kLB: the ablation build's stream kernel only)
 __device__ __forceinline__ void fused_pass(const CopyParams& P, const FusedParams& F) {
   __shared__ GatherSmem sm;
   __shared__ uint4 stage[kSmallStage / 16 + 4];
@@ -1272,14 +1272,16 @@ __global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, Fuse
   fused_pass<false>(P, F);
 }
 
-// Single pass for batches of small blocks of any size (> kFusedMaxBlocks):
-// the fused kernel's per-block work with the prefix by decoupled look-back.
-// Each block is read once (DMA into LDS, header walk and gather from there);
-// the three-launch form (okv_count_kernel's walk in HBM, then the staged
-// gather) reads it twice.
+#ifdef OKV_ABLATE
+// Ablation build (OKV_DECODE_STREAM=1): single pass for batches of small
+// blocks of any size (> kFusedMaxBlocks), the fused kernel's per-block work
+// with the prefix by decoupled look-back.  Each block is read once, but one
+// block per workgroup makes the look-back chase a frontier that lags by the
+// workgroups in flight (CM: 9.2 vs 1.38 ms for passes 1-3, profiles/r4).
 __global__ __launch_bounds__(64) void okv_decode_stream_kernel(CopyParams P, FusedParams F) {
   fused_pass<true>(P, F);
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // Pass 4 (big blocks only): LDS-staged decode with a serial header chase.
@@ -1994,10 +1996,17 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   // small blocks: passes 1-3 in one launch (okv_decode_fused_kernel)
   const bool fused =
       ctx->fused && nblk && nblk <= ctx->fused_max && gather_threads(ctx, w, nblk) == 64;
-  // larger batches of small blocks: the same single pass with the prefix by
-  // decoupled look-back (okv_decode_stream_kernel)
-  const bool stream =
-      ctx->fused && nblk > ctx->fused_max && gather_threads(ctx, w, nblk) == 64;
+  // (ablation build, OKV_DECODE_STREAM=1: larger batches of small blocks in
+  // the same single pass with the prefix by decoupled look-back,
+  // okv_decode_stream_kernel -- measured 9.2 vs 1.38 ms per CM segment of
+  // 386 K blocks: every block's look-back walks back to an inclusive frontier
+  // that lags by the blocks in flight; the product runs passes 1-3)
+#ifdef OKV_ABLATE
+  const bool stream = ctx->stream_lb && ctx->fused && nblk > ctx->fused_max &&
+                      gather_threads(ctx, w, nblk) == 64;
+#else
+  constexpr bool stream = false;
+#endif
   // large blocks: the source-tile pass (okv_tile_kernel); value_sweep 1-7 are
   // the round-2 forms (row pass + address-ordered value sweep)
   const bool large = nblk && !fused && !stream && gather_threads(ctx, w, nblk) == 256;
@@ -2112,10 +2121,12 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       F.epoch = ctx->f_epoch;
       F.tot = ctx->d_tot;
       F.big_zero = big_counter(ctx, 1);
-      if (fused)
-        hipLaunchKernelGGL(okv_decode_fused_kernel, dim3(nblk), dim3(64), 0, ctx->stream, P, F);
-      else
+#ifdef OKV_ABLATE
+      if (stream)
         hipLaunchKernelGGL(okv_decode_stream_kernel, dim3(nblk), dim3(64), 0, ctx->stream, P, F);
+      else
+#endif
+        hipLaunchKernelGGL(okv_decode_fused_kernel, dim3(nblk), dim3(64), 0, ctx->stream, P, F);
       const hipError_t le = hipGetLastError();
       if (le != hipSuccess) {
         // nothing ran: the counters keep their value, so f_base must too
@@ -2388,6 +2399,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
   if (const char* v = getenv("OKV_DECODE_FUSED")) ctx->fused = atoi(v) != 0;
   if (const char* v = getenv("OKV_DECODE_PIECES")) ctx->pieces = atoi(v) != 0;
+  if (const char* v = getenv("OKV_DECODE_STREAM")) ctx->stream_lb = atoi(v) != 0;
   if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
   if (const char* v = getenv("OKV_VALUE_SWEEP")) {
     ctx->value_sweep = uint32_t(atoi(v));

@@ -530,17 +530,18 @@ def test_large_batch_with_big_blocks(decoder, index_only):
     _assert_same_as_oracle(a, seg, d, 0, index_only)
 
 
-def test_stream_path_large_batches(decoder, nofused_decoder, golden):
-    """More than 512 small blocks: the single-pass stream kernel (prefix by
-    decoupled look-back) -- 3 000 mixed blocks (4 KiB, over-kRCap blocks for
+def test_large_batches_of_small_blocks(decoder, nofused_decoder, golden):
+    """More than 512 small blocks: passes 1-3 as three launches (count, scan,
+    staged gather) -- 3 000 mixed blocks (4 KiB, over-kRCap blocks for
     okv_copy_kernel), and the crafted edge blocks repeated past 512 -- equal
-    to the oracle and to the three-launch path (OKV_OPEN_NO_FUSED)."""
+    to the oracle and to the OKV_OPEN_NO_FUSED context."""
     rng = np.random.default_rng(5)
     kinds = list(rng.choice(["s"] * 12 + ["M"], size=3000))
     seg, d = _mixed_segment(kinds, 8)
     for index_only in (False, True):
         got = decoder.decode(seg, d, index_only=index_only)
-        assert decoder.last_path() & _lib.PATH_STREAM
+        assert decoder.last_path() & (_lib.PATH_SMALL | _lib.PATH_GATHER)
+        assert not decoder.last_path() & (_lib.PATH_STREAM | _lib.PATH_FUSED)
         _assert_same_as_oracle(got, seg, d, 0, index_only)
         ref = nofused_decoder.decode(seg, d, index_only=index_only)
         for k in ("status", "row_start", "key_off", "key_len", "val_off", "val_len"):
@@ -552,7 +553,7 @@ def test_stream_path_large_batches(decoder, nofused_decoder, golden):
     cd = np.tile(descs_of(case), (60, 1))
     for comp in (_lib.COMP_NONE, _lib.COMP_LZ4):
         got = decoder.decode(cseg, cd, comp)
-        assert decoder.last_path() & _lib.PATH_STREAM
+        assert not decoder.last_path() & (_lib.PATH_STREAM | _lib.PATH_FUSED)
         want = [b["status"] if comp == _lib.COMP_NONE else b["status_lz4"] for b in case["blocks"]]
         assert [int(x) for x in got.status] == want * 60
         _assert_same_as_oracle(got, cseg, cd, comp, False)

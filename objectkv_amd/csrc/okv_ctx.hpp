@@ -66,6 +66,11 @@ struct okv_ctx {
   size_t f_cap = 0;
   okv::Totals* d_tot = nullptr;
   okv::Totals* h_tot = nullptr;  // pinned
+  // the longest block walk of the last okv_decode_plan, for that batch's tile
+  // pass (tile_geo); keyed by the batch's device inputs
+  unsigned long long* d_span = nullptr;
+  unsigned long long* h_span = nullptr;  // pinned
+  okv::SpanHint span_hint;
   // ablation build (OKV_DECODE_PIECES=1): large-block decodes in two pieces,
   // the second piece's header walk on stream2 under the first's tile pass
   bool pieces = false;

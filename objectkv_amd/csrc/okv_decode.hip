@@ -78,7 +78,7 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     const int32_t* __restrict__ pre_status, int prefetch, uint64_t span_cap,
     Prefix* __restrict__ tile_pre, Totals* __restrict__ tot, uint64_t* __restrict__ row_start,
     uint32_t* __restrict__ arrive, uint32_t* __restrict__ big_zero,
-    const Totals* __restrict__ base, uint32_t bidx0) {
+    const Totals* __restrict__ base, uint32_t bidx0, unsigned long long* __restrict__ span_max) {
   // slots of the current chunk: positions [lane][kRecChunk + 1] (odd stride:
   // the walking lanes' stores hit distinct banks), key lengths [lane][kRecChunk]
   __shared__ uint32_t s_pos[kThreads * (kRecChunk + 1)];
@@ -199,6 +199,15 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     c.status = st;
     c.pad = 0;
     cnt[b] = c;
+  }
+  if (span_max) {  // the longest walk (okv_decode_plan: the tile pass's span hint)
+    unsigned long long m = b < nblk && st == OKV_BLK_OK ? p : 0ull;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const unsigned long long o = __shfl_xor(m, d, 64);
+      m = o > m ? o : m;
+    }
+    if ((tid & 63) == 0 && m) atomicMax(span_max, m);
   }
   // workgroup exclusive scan of (rows, padded kb, padded vb, bad)
   __shared__ uint64_t s_w[4][kThreads / 64];
@@ -1775,7 +1784,8 @@ uint32_t gather_threads(const okv_ctx* ctx, const Work& w, uint32_t nblk) {
 // tile pass (null: positions only); span_cap: blocks whose walk ends past it
 // go to the big-block list.
 int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_start,
-                bool timed = false, uint16_t* rt_kl = nullptr, uint64_t span_cap = ~0ull) {
+                bool timed = false, uint16_t* rt_kl = nullptr, uint64_t span_cap = ~0ull,
+                unsigned long long* span_max = nullptr) {
   int rc = ensure_blocks(ctx, nblk);
   if (rc) return rc;
   // one launch: the count walk, and the tile-total scan by its last workgroup
@@ -1788,7 +1798,7 @@ int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_star
                      w.seg_bytes, w.descs, nblk, w.comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
                      ctx->d_rec, rt_kl, ctx->d_big, big_counter(ctx), w.pre, prefetch, span_cap,
                      ctx->d_tile_pre, ctx->d_tot, d_row_start, ctx->d_ctr + kCtrArrive,
-                     big_counter(ctx, 1), nullptr, 0u);
+                     big_counter(ctx, 1), nullptr, 0u, span_max);
   OKV_HIP(hipGetLastError());
   ctx->big_slot ^= 1u;  // the launch zeroes the other slot: the next launch's counter
   if (timed) {
@@ -1807,11 +1817,17 @@ struct TileGeo {
   uint32_t tpb;
   uint64_t span_cap;
 };
-TileGeo tile_geo(const okv_ctx* ctx, uint64_t seg_bytes, uint32_t nblk, bool index_only) {
+// Tiles per block from the average block span, or from the longest walk the
+// last okv_decode_plan of the same batch measured (blocks longer than the span
+// go to okv_copy_kernel: with bimodal block sizes most bytes would).
+TileGeo tile_geo(const okv_ctx* ctx, const Work& w, uint32_t nblk, bool index_only) {
   if (index_only || !nblk) return {1, ~0ull};
   const uint64_t kT = uint64_t(ctx->tile_kib) << 10;
-  uint64_t span = (seg_bytes / nblk) & ~uint64_t(4095);
+  uint64_t span = (w.seg_bytes / nblk) & ~uint64_t(4095);
   if (span < 4096) span = 4096;
+  const SpanHint& h = ctx->span_hint;
+  if (h.nblk == nblk && h.seg == w.seg && h.descs == w.descs && h.seg_bytes == w.seg_bytes)
+    span = std::max<uint64_t>(span, (h.span + 4095) & ~uint64_t(4095));
   uint64_t tpb = std::min<uint64_t>(64, (span + kT - 1) / kT);
   while (tpb > 1 && uint64_t(nblk) * tpb >= (uint64_t(1) << 31)) tpb >>= 1;
   return {uint32_t(tpb), tpb * kT};
@@ -1942,7 +1958,7 @@ int launch_plan_pieces(okv_ctx* ctx, const Work& w, uint32_t nblk, uint32_t b0,
                      ctx->stream, w.seg, w.seg_bytes, w.descs, nA, w.comp, ctx->d_cnt, ctx->d_lp,
                      ctx->d_tile_tot, ctx->d_rec, rt_kl, ctx->d_big, big, w.pre, 0, span_cap,
                      ctx->d_tile_pre, ctx->d_tot2, nullptr, ctx->d_ctr + kCtrArrive,
-                     big_counter(ctx, 1), nullptr, 0u);
+                     big_counter(ctx, 1), nullptr, 0u, nullptr);
   OKV_HIP(hipGetLastError());
   OKV_HIP(hipEventRecord(ctx->ev_piece[0], ctx->stream));
   OKV_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_piece[0], 0));
@@ -1953,7 +1969,7 @@ int launch_plan_pieces(okv_ctx* ctx, const Work& w, uint32_t nblk, uint32_t b0,
                      rt_kl ? rt_kl + uint64_t(b0) * kRCap : nullptr, ctx->d_big, big,
                      w.pre ? w.pre + b0 : nullptr, 0, span_cap, ctx->d_tile_pre + t0, ctx->d_tot,
                      d_row_start ? d_row_start + b0 : nullptr, ctx->d_ctr + kCtrArrive, nullptr,
-                     ctx->d_tot2, b0);
+                     ctx->d_tot2, b0, nullptr);
   OKV_HIP(hipGetLastError());
   OKV_HIP(hipEventRecord(ctx->ev_piece[1], ctx->stream2));
   ctx->big_slot ^= 1u;  // the first launch zeroed the other slot
@@ -2018,7 +2034,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   const bool tile = large;  // the product: okv_tile_kernel for every large-block decode
   constexpr bool sweep = false;
 #endif
-  const TileGeo geo = tile ? tile_geo(ctx, w.seg_bytes, nblk, index_only) : TileGeo{1, ~0ull};
+  const TileGeo geo = tile ? tile_geo(ctx, w, nblk, index_only) : TileGeo{1, ~0ull};
   uint16_t* rt_kl = nullptr;
   if (tile || sweep) {
     if ((rc = ensure_blocks(ctx, nblk)) ||
@@ -2431,7 +2447,10 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
     ctx->own_stream = true;
   }
   if (hipMalloc(&ctx->d_tot, sizeof(Totals)) != hipSuccess ||
-      hipHostMalloc(reinterpret_cast<void**>(&ctx->h_tot), sizeof(Totals), 0) != hipSuccess) {
+      hipHostMalloc(reinterpret_cast<void**>(&ctx->h_tot), sizeof(Totals), 0) != hipSuccess ||
+      hipMalloc(&ctx->d_span, sizeof(unsigned long long)) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&ctx->h_span), sizeof(unsigned long long), 0) !=
+          hipSuccess) {
     okv_close(ctx);
     return nullptr;
   }
@@ -2465,6 +2484,8 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->f_ctr);
   (void)hipFree(ctx->d_tot);
   if (ctx->h_tot) (void)hipHostFree(ctx->h_tot);
+  if (ctx->h_span) (void)hipHostFree(ctx->h_span);
+  (void)hipFree(ctx->d_span);
   (void)hipFree(ctx->d_seg);
   (void)hipFree(ctx->d_desc);
   (void)hipFree(ctx->d_out);
@@ -2564,9 +2585,13 @@ int okv_decode_plan(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes,
   if ((rc = prepare(ctx, d_seg, seg_bytes, d_desc, nblk, compression,
                     (flags & OKV_F_INDEX_ONLY) != 0, &w)))
     return rc;
-  if ((rc = launch_plan(ctx, w, nblk, nullptr))) return rc;
+  OKV_HIP(hipMemsetAsync(ctx->d_span, 0, sizeof(unsigned long long), ctx->stream));
+  if ((rc = launch_plan(ctx, w, nblk, nullptr, false, nullptr, ~0ull, ctx->d_span))) return rc;
+  OKV_HIP(hipMemcpyAsync(ctx->h_span, ctx->d_span, sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost, ctx->stream));
   Totals T;
-  if ((rc = read_totals(ctx, &T))) return rc;
+  if ((rc = read_totals(ctx, &T))) return rc;  // (synchronises: h_span is valid too)
+  ctx->span_hint = SpanHint{w.seg, w.descs, w.seg_bytes, nblk, *ctx->h_span};
   if (n_rows) *n_rows = T.rows;
   if (key_bytes) *key_bytes = (flags & OKV_F_INDEX_ONLY) ? 0 : T.kb;
   if (val_bytes) *val_bytes = (flags & OKV_F_INDEX_ONLY) ? 0 : T.vb;

@@ -43,6 +43,14 @@ struct Desc {         // == okv_block_desc
   uint64_t offset, block_size, original_size, compressed_size;
 };
 
+struct SpanHint {  // okv_decode_plan's longest walk (host side)
+  const uint8_t* seg = nullptr;
+  const Desc* descs = nullptr;
+  uint64_t seg_bytes = 0;
+  uint32_t nblk = 0;
+  uint64_t span = 0;
+};
+
 __device__ __forceinline__ uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
 // Go's int() conversions at the block boundary (segment_reader.go:303-340),

@@ -188,6 +188,48 @@ def test_device_pointer_api_torch(decoder):
     assert out["key_arena"].cpu().numpy().tobytes() == host.key_arena.tobytes()
 
 
+def test_bimodal_blocks_with_plan_span(decoder):
+    """Alternating 4 KiB / 60 KiB blocks (average 32 KiB): okv_decode_plan
+    measures the longest walk and the tile pass of the same batch sizes its
+    tiles per block from it (no block left to okv_copy_kernel).  Device-pointer
+    decode after the plan == host-mode decode == oracle."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(77)
+    parts, descs, off = [], [], 0
+    for i in range(1200):
+        target = 4096 if i % 2 == 0 else 61440
+        body = bytearray()
+        while len(body) < target - 3100:
+            vl = int(rng.integers(1000, 3000))
+            body += (16).to_bytes(2, "little") + vl.to_bytes(4, "little")
+            body += rng.integers(0, 256, 16 + vl, dtype=np.uint8).tobytes()
+        bsize = (len(body) // 4096 + 1) * 4096
+        parts.append(bytes(body) + bytes(bsize - len(body)))
+        descs.append((off, bsize, len(body), 0))
+        off += bsize
+    seg = np.frombuffer(b"".join(parts) + bytes(4096), np.uint8)
+    d = np.array(descs, np.uint64)
+    n = d.shape[0]
+    dev = torch.device("cuda", 0)
+    seg_t = torch.from_numpy(seg.copy()).to(dev)
+    d_t = torch.from_numpy(d.view(np.int64).copy()).to(dev)
+    rows, kb, vb = decoder.plan_device(seg_t, seg.size, d_t, n)
+    out = {k: torch.zeros(m, dtype=t, device=dev) for k, m, t in [
+        ("row_start", n + 1, torch.int64), ("key_base", n, torch.int64),
+        ("val_base", n, torch.int64), ("status", n, torch.int32),
+        ("key_off", rows, torch.int64), ("key_len", rows, torch.int16),
+        ("val_off", rows, torch.int64), ("val_len", rows, torch.int32),
+        ("key_arena", kb, torch.uint8), ("val_arena", vb, torch.uint8)]}
+    decoder.decode_device(seg_t, seg.size, d_t, n, out, sync=True)
+    assert decoder.last_path() & _lib.PATH_TILE
+    host = decoder.decode(seg.tobytes(), d)
+    _assert_same_as_oracle(host, seg.tobytes(), d, 0, False)
+    assert np.array_equal(out["row_start"].cpu().numpy().view(np.uint64), host.row_start)
+    assert np.array_equal(out["val_off"].cpu().numpy().view(np.uint64), host.val_off)
+    assert out["val_arena"].cpu().numpy().tobytes() == host.val_arena.tobytes()
+    assert out["key_arena"].cpu().numpy().tobytes() == host.key_arena.tobytes()
+
+
 def test_random_fuzz_against_c_oracle(decoder):
     """Random record streams with truncation/corruption/odd offsets."""
     rng = np.random.default_rng(2024)

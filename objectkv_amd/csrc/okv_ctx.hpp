@@ -74,7 +74,9 @@ struct okv_ctx {
   // ablation build (OKV_DECODE_PIECES=1): large-block decodes in two pieces,
   // the second piece's header walk on stream2 under the first's tile pass
   bool pieces = false;
-  bool stream_lb = false;  // ablation build (OKV_DECODE_STREAM=1): okv_decode_stream_kernel
+  bool stream_lb = false;
+  uint64_t small_piece = 0;   // ablation build (OKV_SMALL_PIECE_MB): small-block decodes in pieces
+  void* d_ptot = nullptr;     // two Totals: the running prefix between pieces  // ablation build (OKV_DECODE_STREAM=1): okv_decode_stream_kernel
   hipStream_t stream2 = nullptr;
   hipEvent_t ev_piece[2] = {nullptr, nullptr};
   okv::Totals* d_tot2 = nullptr;   // totals of the first piece

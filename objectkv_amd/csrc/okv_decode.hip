@@ -1793,7 +1793,10 @@ int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_star
   const uint32_t ntiles = std::max<uint32_t>(1, (nblk + kTile - 1) / kTile);
   // prefetch block lines before the chase when the segment fits in the caches
   // and blocks are small (dense headers); 64 KiB blocks touch ~5 % of their lines
-  const int prefetch = nblk && w.seg_bytes <= (64ull << 20) && w.seg_bytes / nblk <= 16384;
+  int prefetch = nblk && w.seg_bytes <= (64ull << 20) && w.seg_bytes / nblk <= 16384;
+#ifdef OKV_ABLATE
+  if (const char* v = getenv("OKV_COUNT_PREFETCH")) prefetch = atoi(v) && nblk;  // A/B
+#endif
   hipLaunchKernelGGL(okv_count_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, w.seg,
                      w.seg_bytes, w.descs, nblk, w.comp, ctx->d_cnt, ctx->d_lp, ctx->d_tile_tot,
                      ctx->d_rec, rt_kl, ctx->d_big, big_counter(ctx), w.pre, prefetch, span_cap,
@@ -1995,6 +1998,21 @@ CopyParams piece_params(const CopyParams& P, uint32_t b0, uint32_t n) {
   Q.blk_status = P.blk_status + b0;
   return Q;
 }
+
+// Pass 1-2 of blocks [b0, b0 + n) (b0 a multiple of kTile) continuing the
+// prefixes of the blocks before them (base: their totals, or null), totals
+// into tot; the piece's record table at d_rec + b0 * kRCap (its own layout).
+void launch_count_piece(okv_ctx* ctx, const Work& w, uint32_t b0, uint32_t n, uint64_t* d_row_start,
+                        const Totals* base, Totals* tot, bool first) {
+  const uint64_t t0 = b0 / kTile;
+  hipLaunchKernelGGL(okv_count_kernel, dim3((n + kTile - 1) / kTile), dim3(kThreads), 0,
+                     ctx->stream, w.seg, w.seg_bytes, w.descs + b0, n, w.comp, ctx->d_cnt + b0,
+                     ctx->d_lp + b0, ctx->d_tile_tot + t0, ctx->d_rec + uint64_t(b0) * kRCap,
+                     nullptr, ctx->d_big, big_counter(ctx), w.pre ? w.pre + b0 : nullptr, 0,
+                     ~0ull, ctx->d_tile_pre + t0, tot, d_row_start ? d_row_start + b0 : nullptr,
+                     ctx->d_ctr + kCtrArrive, first ? big_counter(ctx, 1) : nullptr, base, b0,
+                     nullptr);
+}
 #endif  // OKV_ABLATE
 
 int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
@@ -2046,6 +2064,13 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   uint32_t* const big_count = big_counter(ctx);  // this decode's slot (launch_plan flips it)
 #ifdef OKV_ABLATE
   const uint32_t b0 = tile && ctx->pieces ? piece_split(nblk) : 0u;
+  // small blocks in pieces of ~small_piece bytes (OKV_SMALL_PIECE_MB): count
+  // then gather per piece, the gather reading what the count just read
+  uint32_t spn = 0;
+  if (!fused && !stream && !large && nblk && ctx->small_piece && w.seg_bytes > ctx->small_piece)
+    spn = std::max<uint32_t>(kTile, uint32_t(uint64_t(nblk) * ctx->small_piece / w.seg_bytes) &
+                                        ~uint32_t(kTile - 1));
+  if (spn >= nblk) spn = 0;
 #endif
   if (fused || stream) {
     if ((rc = ensure_fused(ctx, nblk))) return rc;
@@ -2055,6 +2080,10 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   } else if (b0) {
     rc = launch_plan_pieces(ctx, w, nblk, b0, o->row_start, rt_kl, geo.span_cap);
     if (rc) return rc;
+  } else if (spn) {  // the counts run piece by piece with the gathers below
+    if (!ctx->d_ptot) OKV_HIP(hipMalloc(&ctx->d_ptot, 2 * sizeof(Totals)));
+    prof_mark(ctx, 2);
+    prof_mark(ctx, 3);
 #endif
   } else {
     rc = launch_plan(ctx, w, nblk, o->row_start, true, rt_kl, geo.span_cap);
@@ -2199,6 +2228,18 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
                          dim3(kThreads), 0, ctx->stream, P);
     } else if (gather_threads(ctx, w, nblk) == 256 && ctx->gather_staged && !index_only) {
       hipLaunchKernelGGL((okv_gather_staged_kernel<kThreads>), g, dim3(kThreads), 0, ctx->stream, P);
+    } else if (spn && ctx->gather_staged) {
+      Totals* pt = static_cast<Totals*>(ctx->d_ptot);
+      const Totals* base = nullptr;
+      for (uint32_t p0 = 0, k = 0; p0 < nblk; p0 += spn, ++k) {
+        const uint32_t n = std::min(spn, nblk - p0);
+        Totals* tot = p0 + n == nblk ? ctx->d_tot : pt + (k & 1);
+        launch_count_piece(ctx, w, p0, n, o->row_start, base, tot, k == 0);
+        hipLaunchKernelGGL(okv_gather_small_kernel, dim3(n), dim3(64), 0, ctx->stream,
+                           piece_params(P, p0, n));
+        base = tot;
+      }
+      ctx->big_slot ^= 1u;  // the first count launch zeroed the other slot
     } else if (gather_threads(ctx, w, nblk) == 64 && ctx->gather_staged)
       hipLaunchKernelGGL(okv_gather_small_kernel, g, dim3(64), 0, ctx->stream, P);
     else if (gather_threads(ctx, w, nblk) == 64)
@@ -2416,6 +2457,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   if (const char* v = getenv("OKV_DECODE_FUSED")) ctx->fused = atoi(v) != 0;
   if (const char* v = getenv("OKV_DECODE_PIECES")) ctx->pieces = atoi(v) != 0;
   if (const char* v = getenv("OKV_DECODE_STREAM")) ctx->stream_lb = atoi(v) != 0;
+  if (const char* v = getenv("OKV_SMALL_PIECE_MB")) ctx->small_piece = uint64_t(atoi(v)) << 20;
   if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
   if (const char* v = getenv("OKV_VALUE_SWEEP")) {
     ctx->value_sweep = uint32_t(atoi(v));
@@ -2501,6 +2543,7 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->z_lit);
   (void)hipFree(ctx->z_blit);
   (void)hipFree(ctx->z_tabs);
+  (void)hipFree(ctx->d_ptot);
   if (ctx->z_ev) (void)hipEventDestroy(ctx->z_ev);
   (void)hipFree(ctx->z_zb);
   (void)hipFree(ctx->z_seq_off);

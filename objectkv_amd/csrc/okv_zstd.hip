@@ -37,9 +37,10 @@ constexpr uint32_t kChunkOut = 4096;     // output bytes per chunk covered by th
 constexpr uint32_t kChunkClose = 3072;   // a chunk takes no more sequences past this output
 
 enum : int32_t { kOK = 0, kErr = 1, kCap = 2, kSlow = 3, kDefer = 4 };
-#ifdef OKV_ABLATE
-// ablation build: every corrupt-input exit records its source line
-// (okv_debug_zstd_err; diagnostics only)
+#ifdef OKV_ZSTD_TRACE
+// diagnostic build (make ablate ZTRACE=1): every corrupt-input exit records
+// its source line (okv_debug_zstd_err, tools/zdebug.py).  The records change
+// the inlined code's shape, and with them the failures of DESIGN.md 13.2.
 __device__ int g_zerr[4];  // last line, count
 __device__ __forceinline__ int32_t zerr_at(int line) {
   if ((threadIdx.x & 63) == 0) {
@@ -1690,24 +1691,27 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
 // through zb's pointers: a pointer read from memory is flat, and a flat load
 // counts against the LDS counter too, so every table lookup's wait would also
 // wait for the stream prefetch.)
+// kHB blocks per wave (kHB * 4 KiB of LDS): fewer blocks per wave put more
+// waves on each CU's four SIMDs (the stream chains are latency-bound).
+template <uint32_t kHB>
 __global__ __launch_bounds__(64) void okv_zstd_huf_kernel(zst::ZBlk* __restrict__ zb, uint32_t nblk,
                                                           const uint16_t* __restrict__ htab,
                                                           const uint8_t* __restrict__ seg,
                                                           uint8_t* __restrict__ blit,
                                                           const uint64_t* __restrict__ cap_off) {
-  __shared__ uint16_t ht[16 * zst::kHufSlot];  // 64 KiB
+  __shared__ uint16_t ht[kHB * zst::kHufSlot];
   const int lane = threadIdx.x & 63;
   const uint32_t j = uint32_t(lane) >> 2, sidx = uint32_t(lane) & 3;
-  const uint32_t b0 = blockIdx.x * 16, b = b0 + j;
+  const uint32_t b0 = blockIdx.x * kHB, b = b0 + j;
   bool mine = false;
   uint32_t mb = 0;
-  if (b < nblk) {
+  if (j < kHB && b < nblk) {
     mine = zb[b].kind == zst::kKindSeq && (zb[b].flags & zst::kFlagHuf);
     mb = mine ? zb[b].hmb : 0u;
   }
   // the tables: 2^(mb+1) bytes each (at least one 1 KiB piece), LDS DMA
   const uint8_t* src = reinterpret_cast<const uint8_t*>(htab);
-  for (uint32_t jj = 0; jj < 16; ++jj) {
+  for (uint32_t jj = 0; jj < kHB; ++jj) {
     const uint32_t mj = __builtin_amdgcn_readlane(mine ? mb + 1 : 0u, int(4 * jj));
     if (!mj) continue;
     const uint32_t pieces = mj > 10 ? 1u << (mj - 10) : 1u;
@@ -1734,6 +1738,11 @@ __global__ __launch_bounds__(64) void okv_zstd_huf_kernel(zst::ZBlk* __restrict_
   const uint64_t bad = __ballot(!good);
   if (mine && sidx == 0 && ((bad >> (4 * j)) & 0xfull)) zb[b].st = zst::kErr;
 }
+
+#ifndef OKV_ZSTD_HUF_BLOCKS
+#define OKV_ZSTD_HUF_BLOCKS 8  // 0.392 vs 0.439 ms at 16, 0.391 at 4 (CZ, profiles/r4/session)
+#endif
+constexpr uint32_t kHufBlocks = OKV_ZSTD_HUF_BLOCKS;  // blocks per wave of the stream stage
 
 // Exclusive scan of the deferred blocks' sequence counts -> seq_off[nblk + 1].
 __global__ __launch_bounds__(1024) void okv_zstd_seqoff_kernel(const zst::ZBlk* __restrict__ zb,
@@ -2709,8 +2718,22 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
     if (!ctx->z_ev) OKV_HIP(hipEventCreateWithFlags(&ctx->z_ev, hipEventDisableTiming));
     OKV_HIP(hipEventRecord(ctx->z_ev, s));
     // the literal streams decode while the host reads the sequence count
-    hipLaunchKernelGGL(okv_zstd_huf_kernel, dim3((nblk + 15) / 16), dim3(64), 0, s, zb, nblk, htab, seg,
-                       ctx->z_blit, ctx->z_cap_off);
+#ifdef OKV_ABLATE
+    const uint32_t hb = okv::knob("OKV_ZSTD_HUF_BLOCKS") ? uint32_t(atoi(okv::knob("OKV_ZSTD_HUF_BLOCKS")))
+                                                        : kHufBlocks;
+    if (hb == 16)
+      hipLaunchKernelGGL(okv_zstd_huf_kernel<16>, dim3((nblk + 15) / 16), dim3(64), 0, s, zb, nblk,
+                         htab, seg, ctx->z_blit, ctx->z_cap_off);
+    else if (hb == 8)
+      hipLaunchKernelGGL(okv_zstd_huf_kernel<8>, dim3((nblk + 7) / 8), dim3(64), 0, s, zb, nblk,
+                         htab, seg, ctx->z_blit, ctx->z_cap_off);
+    else if (hb == 2)
+      hipLaunchKernelGGL(okv_zstd_huf_kernel<2>, dim3((nblk + 1) / 2), dim3(64), 0, s, zb, nblk,
+                         htab, seg, ctx->z_blit, ctx->z_cap_off);
+    else
+#endif
+    hipLaunchKernelGGL(okv_zstd_huf_kernel<kHufBlocks>, dim3((nblk + kHufBlocks - 1) / kHufBlocks),
+                       dim3(64), 0, s, zb, nblk, htab, seg, ctx->z_blit, ctx->z_cap_off);
     OKV_HIP(hipEventSynchronize(ctx->z_ev));
     if (prof) (void)hipEventRecord(ev[1], s);
     if ((rc = grow(ctx, reinterpret_cast<void**>(&ctx->z_seqs), &ctx->z_cap_seqs,
@@ -2782,7 +2805,7 @@ void launch_zstd_desc(hipStream_t s, const Desc* descs, uint32_t nblk, const uin
 
 }  // namespace okv
 
-#ifdef OKV_ABLATE
+#ifdef OKV_ZSTD_TRACE
 // Diagnostic: the last corrupt-input exit's source line and the exit count
 // since the previous call (then reset).
 extern "C" int okv_debug_zstd_err(int* out2) {

@@ -1,4 +1,4 @@
-"""Diagnostics (ablation build): decode the zstd test cases through the
+"""Diagnostics (ablation build made with `make ablate ZTRACE=1`): decode the zstd test cases through the
 one-pass kernel and print each case's statuses with the last corrupt-input
 exit line the kernel recorded (okv_debug_zstd_err)."""
 import ctypes as C
@@ -16,8 +16,11 @@ from tests import zstd_cases as ZC  # noqa: E402
 
 lib = C.CDLL(_lib.LIB_PATH)
 lib.okv_debug_zstd_err.argtypes = [C.POINTER(C.c_int)]
-dec = okv.Decoder(0, flags=_lib.OPEN_ZSTD_ONE_PASS)
-want = sys.argv[1:] or None
+args = sys.argv[1:]
+staged = "--staged" in args
+args = [a for a in args if a != "--staged"]
+dec = okv.Decoder(0, flags=0 if staged else _lib.OPEN_ZSTD_ONE_PASS)
+want = args or None
 for name, seg, descs, _note in ZC.cases():
     if want and name not in want:
         continue

@@ -155,6 +155,30 @@ def test_zstd_staged_equals_general_under_corruption(decoder, one_pass_decoder):
     assert 0 < int((staged.status != 0).sum()) < len(dl)
 
 
+def test_zstd_literal_stream_corruption(decoder, one_pass_decoder):
+    """Byte flips in the first KiBs of 48 frames -- the Huffman tree and the
+    literal streams, which the staged path decodes in its stream stage
+    (okv_zstd_huf_kernel, 8 blocks per wave) and the one-pass kernel inline.
+    Two-sided against libzstd through the oracle: every block's status equals
+    the checker's (a stream that fails its end-marker or bit-count checks fails
+    the block; a flip that only changes literal values must give the checker's
+    bytes), on both device paths."""
+    import random
+    from tools.zstd_gen import text_zstd_segment
+    seg, descs, _ = text_zstd_segment(48, 17, 3)
+    b = bytearray(seg.tobytes())
+    rng = random.Random(23)
+    for i, d in enumerate(descs):
+        off, csz = int(d[0]), int(d[3])
+        for _ in range(1 + i % 2):
+            b[off + 40 + rng.randrange(min(csz - 60, 4000))] ^= 1 << rng.randrange(8)
+    dl = [tuple(int(x) for x in d) for d in descs]
+    staged = _check(decoder, bytes(b), dl)
+    general = _check(one_pass_decoder, bytes(b), dl)
+    assert np.array_equal(staged.status, general.status)
+    assert 0 < int((staged.status != 0).sum()) < len(dl)
+
+
 @pytest.mark.parametrize("case", ZC.past_original_cases(), ids=lambda c: c[0])
 def test_zstd_past_original_size(zdec, case):
     """Frames that inflate past OriginalSize decode in full on the device (Go's

@@ -561,7 +561,7 @@ def run_decode(args, torch, okv, D):
                      "traffic_source": traffic_src, "decode_source_sha": source_sha(),
                      # the same kernel's rocprofv3 trace average (another process, maybe
                      # another box) and the event time the traced process measured itself
-                     "trace": None if comp else trace_roofline(args.config, alg)},
+                     "trace": trace_roofline(args.config, alg)},
         "cpu_baseline": cpu,
         "verify": ver,
         "dist": D.info(),

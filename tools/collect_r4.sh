@@ -11,7 +11,7 @@ mkdir -p $D
 for f in $S/*.log; do
   [ -f "$f" ] && grep -v "amdgpu.ids" "$f" > $D/$(basename "$f")
 done
-for f in pmc_c3_full.json pmc_c4_encode.json trace_c3.json; do
+for f in pmc_c3_full.json pmc_c4_encode.json trace_c3.json trace_cz.json; do
   [ -f $S/$f ] && cp $S/$f $D/
 done
 for t in trace_c3 trace_cz; do

@@ -53,9 +53,17 @@ if [ "$PART" = a ]; then
   echo "final4 a done"
 else
   step bench_c4 600 python3 bench.py --config c4
-  step bench_cz 600 python3 bench.py --config cz
+  # the zstd stage: its 9 kernels per decode summed (cap, prologue, seq offsets, streams,
+  # sequences, executor, general, regrow list, descriptors); untimed: plan, guard, 2 warmup
   step trace_cz 300 rocprofv3 --kernel-trace --stats -d "$O/trace_cz" -o run --output-format csv \
     -- python3 "$R/bench.py" --config cz --steps 10 --warmup 2 --no-cpu --no-verify --decode-inflight 1
+  CSV=$(find "$O/trace_cz" -name 'run_kernel_trace.csv' | head -1)
+  ALG=$(python3 -c "import json; l=[json.loads(x) for x in open('$O/trace_cz.log') if x.startswith('{')][-1]; print(l['roofline']['algorithmic_bytes_per_launch'])")
+  step trace_cz_sum 60 python3 tools/trace_summary.py "$CSV" okv_zstd_ 4 "$ALG" "$O/trace_cz.json" \
+    "CZ one decode at a time (bench.py --decode-inflight 1, 10 steps + 2 warmup + guard + plan); the zstd stage's 9 kernels summed per decode" \
+    --sha "$DSHA" --bench-log "$O/trace_cz.log" --per-step 9 --event-key zstd
+  mkdir -p profiles/r4 && cp "$O/trace_cz.json" profiles/r4/
+  step bench_cz 600 python3 bench.py --config cz
   step bench_cm 600 python3 bench.py --config cm
   step bench_c5 300 python3 bench.py --config c5 --no-cpu
   step bench_c2 300 python3 bench.py --config c2 --no-cpu

@@ -5,11 +5,14 @@ roofline fraction the timed average implies.
 usage: python tools/trace_summary.py <run_kernel_trace.csv> <kernel substring>
            <untimed launches> <algorithmic bytes per launch> <out.json> [note]
            [--sha <decode source sha>] [--bench-log <the traced bench's stdout/stderr>]
-           [--per-step K]
+           [--per-step K] [--event-key copy|zstd]
 
 --per-step K: the kernel runs K launches per step (a two-piece decode launches
 the tile pass twice): consecutive launches are summed in groups of K, and
 every count below (launches, untimed launches) is in steps.
+
+--event-key: which of the bench line's kernel_ms to compare with (default
+copy, pass 3; zstd: the zstd stage, whose kernels --per-step sums per decode).
 
 --sha lets bench.py attach the trace to its roofline only while the kernel
 sources are the traced ones; --bench-log records the bench's own HIP-event
@@ -22,7 +25,7 @@ import sys
 
 argv = sys.argv[1:]
 opts = {}
-for flag in ("--sha", "--bench-log", "--per-step"):
+for flag in ("--sha", "--bench-log", "--per-step", "--event-key"):
     if flag in argv:
         i = argv.index(flag)
         opts[flag] = argv[i + 1]
@@ -52,7 +55,8 @@ if "--bench-log" in opts:
         if ln.startswith("{") and '"metric"' in ln:
             line = json.loads(ln)
     if line:
-        res["bench_event_ms_same_process"] = line.get("kernel_ms", {}).get("copy")
+        res["bench_event_ms_same_process"] = line.get("kernel_ms", {}).get(
+            opts.get("--event-key", "copy"))
         res["bench_event_vs_trace"] = (res["bench_event_ms_same_process"] * 1e6 / avg
                                        if res["bench_event_ms_same_process"] else None)
 with open(out, "w") as f:

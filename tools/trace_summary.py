@@ -40,7 +40,9 @@ if K > 1:  # per step: the K launches of one decode, summed
     ns = [sum(ns[i:i + K]) for i in range(0, len(ns) - len(ns) % K, K)]
 timed = ns[skip:]
 avg = sum(timed) / len(timed)
-res = {"kernel": rows[0]["Kernel_Name"].split("(")[0] if rows else kern, "source": path,
+names = sorted({r["Kernel_Name"].split("(")[0] for r in rows})
+label = names[0] if len(names) == 1 else f"{kern}* ({len(names)} kernels summed per step)"
+res = {"kernel": label if rows else kern, "kernels": names, "source": path,
        "launches": len(ns), "untimed_launches": skip, "timed_launches": len(timed),
        "avg_ns_timed": avg, "min_ns_timed": min(timed), "max_ns_timed": max(timed),
        "avg_ns_all": sum(ns) / len(ns), "per_launch_ns": ns,

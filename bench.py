@@ -288,10 +288,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--c4-inflight", type=int, default=2,
                     help="c4: segments in flight (Close of one overlaps the next's kernels)")
-    ap.add_argument("--decode-inflight", type=int, default=2,
+    ap.add_argument("--decode-inflight", type=int, default=4,
                     help="decode configs: whole-segment decodes in flight, each on its own "
-                         "context, stream and output buffers (one's pass 1 overlaps another's "
-                         "pass 3); 1 = one at a time")
+                         "context, stream, segment copy and output buffers (later decodes' "
+                         "pass 1 under the current pass 3); 1 = one at a time.  C3, one box: "
+                         "2 / 3 / 4 in flight 2694 / 2765 / 2789 GiB/s (DESIGN.md 13.11)")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the pinned, pipelined host-buffer path (PCIe both ways)")
     ap.add_argument("--dist-backend", default="nccl",

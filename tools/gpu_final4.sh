@@ -9,7 +9,7 @@
 #   b: the other configurations' bench lines (with CPU baselines), the CZ
 #      kernel trace, GetRow latency, bimodal blocks, 2-rank one-GPU rehearsals
 # Every step has its own time limit; the first failure ends the script.
-#   tools/gpu_final4.sh <a|b> <tag>
+#   tools/gpu_final4.sh <a|b|b2> <tag>   (b2: b plus the driver's bench command)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 export TMPDIR=/tmp
@@ -52,6 +52,7 @@ if [ "$PART" = a ]; then
   step bench_driver 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
   echo "final4 a done"
 else
+  [ "$PART" = b2 ] && step bench_driver 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
   step bench_c4 600 python3 bench.py --config c4
   # the zstd stage: its 9 kernels per decode summed (cap, prologue, seq offsets, streams,
   # sequences, executor, general, regrow list, descriptors); untimed: plan, guard, 2 warmup

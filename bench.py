@@ -70,6 +70,7 @@ DECODE_SOURCES = ("objectkv_amd/csrc/okv_decode.hip", "objectkv_amd/csrc/okv_ker
                   "objectkv_amd/csrc/okv_ctx.hpp")
 ENCODE_SOURCES = ("objectkv_amd/csrc/okv_encode.hip", "objectkv_amd/csrc/okv_kernels.hpp",
                   "objectkv_amd/csrc/okv_ctx.hpp")
+ZSTD_SOURCES = DECODE_SOURCES + ("objectkv_amd/csrc/okv_zstd.hip",)
 
 
 def log(*a):
@@ -161,7 +162,7 @@ def pmc_traffic(config, mode, kernel, sources=DECODE_SOURCES):
     return None, None
 
 
-def trace_roofline(config, alg):
+def trace_roofline(config, alg, sources=DECODE_SOURCES):
     """The rocprofv3 kernel-trace average of the roofline kernel from
     profiles/<PMC_ROUND>/trace_<config>.json (tools/trace_summary.py), and the
     roofline fraction it implies for `alg` bytes -- attached only if the trace
@@ -171,7 +172,7 @@ def trace_roofline(config, alg):
         return None
     with open(path) as f:
         d = json.load(f)
-    if d.get("source_sha") != source_sha():
+    if d.get("source_sha") != source_sha(sources):
         return {"source": os.path.relpath(path, ROOT),
                 "stale": "kernel sources changed since the trace"}
     ms = d["avg_ns_timed"] / 1e6
@@ -562,7 +563,8 @@ def run_decode(args, torch, okv, D):
                      "traffic_source": traffic_src, "decode_source_sha": source_sha(),
                      # the same kernel's rocprofv3 trace average (another process, maybe
                      # another box) and the event time the traced process measured itself
-                     "trace": trace_roofline(args.config, alg)},
+                     "trace": trace_roofline(args.config, alg,
+                                             ZSTD_SOURCES if comp else DECODE_SOURCES)},
         "cpu_baseline": cpu,
         "verify": ver,
         "dist": D.info(),

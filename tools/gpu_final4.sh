@@ -29,6 +29,7 @@ step() {
 }
 DSHA=$(python3 -c "import bench; print(bench.source_sha(bench.DECODE_SOURCES))")
 ESHA=$(python3 -c "import bench; print(bench.source_sha(bench.ENCODE_SOURCES))")
+ZSHA=$(python3 -c "import bench; print(bench.source_sha(bench.ZSTD_SOURCES))")
 if [ "$PART" = a ]; then
   step pytest 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
   step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
@@ -62,7 +63,7 @@ else
   ALG=$(python3 -c "import json; l=[json.loads(x) for x in open('$O/trace_cz.log') if x.startswith('{')][-1]; print(l['roofline']['algorithmic_bytes_per_launch'])")
   step trace_cz_sum 60 python3 tools/trace_summary.py "$CSV" okv_zstd_ 4 "$ALG" "$O/trace_cz.json" \
     "CZ one decode at a time (bench.py --decode-inflight 1, 10 steps + 2 warmup + guard + plan); the zstd stage's 9 kernels summed per decode" \
-    --sha "$DSHA" --bench-log "$O/trace_cz.log" --per-step 9 --event-key zstd
+    --sha "$ZSHA" --bench-log "$O/trace_cz.log" --per-step 9 --event-key zstd
   mkdir -p profiles/r4 && cp "$O/trace_cz.json" profiles/r4/
   step bench_cz 600 python3 bench.py --config cz
   step bench_cm 600 python3 bench.py --config cm

@@ -289,11 +289,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--c4-inflight", type=int, default=2,
                     help="c4: segments in flight (Close of one overlaps the next's kernels)")
-    ap.add_argument("--decode-inflight", type=int, default=4,
+    ap.add_argument("--decode-inflight", type=int, default=None,
                     help="decode configs: whole-segment decodes in flight, each on its own "
                          "context, stream, segment copy and output buffers (later decodes' "
-                         "pass 1 under the current pass 3); 1 = one at a time.  C3, one box: "
-                         "2 / 3 / 4 in flight 2694 / 2765 / 2789 GiB/s (DESIGN.md 13.11)")
+                         "pass 1 under the current pass 3); 1 = one at a time.  Default 4 for "
+                         "C3 (one box: 2 / 3 / 4 in flight 2694 / 2765 / 2789 GiB/s), 2 for the "
+                         "others (C2 at 4: 48.3 vs 55.3 GiB/s; DESIGN.md 13.11)")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the pinned, pipelined host-buffer path (PCIe both ways)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -440,7 +441,8 @@ def run_decode(args, torch, okv, D):
     # Each in-flight decode reads its own copy of the segment (consecutive
     # segments of a reader are different bytes: two decodes of one buffer
     # could share its lines in the caches).
-    inflight = max(1, args.decode_inflight)
+    inflight = max(1, args.decode_inflight if args.decode_inflight is not None
+                   else (4 if args.config == "c3" else 2))
     decs, outs, streams, segs = [dec], [out], [], [seg_t]
     for i in range(1, inflight):
         streams.append(torch.cuda.Stream(dev))

@@ -1082,6 +1082,10 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 // kLB: the form for batches of any size (okv_decode_stream_kernel below):
 // the exclusive prefix by a decoupled look-back instead of the last arrival's
 // scan, so no block waits for blocks that may not be resident.
+// The exclusive prefix by a decoupled look-back: the ablation build's stream
+// kernel (okv_decode_ablate_lb.inc); declared here, defined only there.
+__device__ Prefix fused_prefix_lookback(const CopyParams& P, const FusedParams& F, uint32_t b,
+                                        uint32_t lane, uint32_t tag, const Prefix& mine);
 template <bool kLB>  // (kLB: the ablation build's stream kernel only)
 __device__ __forceinline__ void fused_pass(const CopyParams& P, const FusedParams& F) {
   __shared__ GatherSmem sm;
@@ -1146,46 +1150,7 @@ __device__ __forceinline__ void fused_pass(const CopyParams& P, const FusedParam
   const Prefix mine{rows, round16(kb), round16(vb), uint64_t(st != OKV_BLK_OK)};
   Prefix ex{0, 0, 0, 0};
   if constexpr (kLB) {
-    // ---- pass 2 by decoupled look-back: publish this block's aggregate,
-    // then read the flags of the 64 blocks before it at once (one lane each),
-    // waiting until each has published at least its aggregate; the nearest
-    // inclusive prefix in the window ends the look-back, else the window's
-    // aggregates are added and the next 64 are read.  Blocks take their
-    // index from a counter in start order, so every block waited on is
-    // running: any batch size is safe.
-    if (lane == 0) {
-      publish(&F.flag[b], &F.agg[b], mine, tag | 1u);
-      atomicAdd(F.arr, 1ull);  // (kept in step with F.ctr: the host's base)
-    }
-    int64_t hi = int64_t(b) - 1;
-    for (;;) {
-      const int64_t k = hi - int64_t(lane);
-      uint32_t f = k >= 0 ? flag_peek(&F.flag[k]) : (tag | 2u);
-      while (__any((f & ~3u) != tag)) {
-        __builtin_amdgcn_s_sleep(1);
-        if ((f & ~3u) != tag) f = flag_peek(&F.flag[k]);
-      }
-      const uint64_t inc = __ballot((f & 3u) == 2u);
-      const uint32_t j = inc ? uint32_t(__ffsll(static_cast<unsigned long long>(inc)) - 1) : 64u;
-      // lanes < j: aggregates; lane j: an inclusive prefix (zero before block 0)
-      Prefix v{0, 0, 0, 0};
-      if (lane < j && k >= 0) v = prefix_peek(&F.agg[k]);
-      if (lane == j && k >= 0) v = prefix_peek(&F.incl[k]);
-      ex.rows += wave_sum64(v.rows);
-      ex.kb += wave_sum64(v.kb);
-      ex.vb += wave_sum64(v.vb);
-      ex.bad += wave_sum64(v.bad);
-      if (j < 64) break;
-      hi -= 64;
-    }
-    if (lane == 0) {  // this block's inclusive prefix
-      const Prefix in{ex.rows + mine.rows, ex.kb + mine.kb, ex.vb + mine.vb, ex.bad + mine.bad};
-      publish(&F.flag[b], &F.incl[b], in, tag | 2u);
-      if (b == P.nblk - 1) {
-        *F.tot = Totals{in.rows, in.kb, in.vb, in.bad};
-        P.row_start[P.nblk] = in.rows;
-      }
-    }
+    ex = fused_prefix_lookback(P, F, b, lane, tag, mine);  // ablation build only
   } else {
   // ---- pass 2: the last block to arrive scans every block's counts ----
   // (every block of the grid is resident: the fused form runs for small
@@ -1281,16 +1246,6 @@ __global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, Fuse
   fused_pass<false>(P, F);
 }
 
-#ifdef OKV_ABLATE
-// Ablation build (OKV_DECODE_STREAM=1): single pass for batches of small
-// blocks of any size (> kFusedMaxBlocks), the fused kernel's per-block work
-// with the prefix by decoupled look-back.  Each block is read once, but one
-// block per workgroup makes the look-back chase a frontier that lags by the
-// workgroups in flight (CM: 9.2 vs 1.38 ms for passes 1-3, profiles/r4).
-__global__ __launch_bounds__(64) void okv_decode_stream_kernel(CopyParams P, FusedParams F) {
-  fused_pass<true>(P, F);
-}
-#endif
 
 // ---------------------------------------------------------------------------
 // Pass 4 (big blocks only): LDS-staged decode with a serial header chase.
@@ -1659,6 +1614,9 @@ void launch_hash(hipStream_t stream, const uint8_t* seg, uint64_t seg_bytes, con
                      dim3(kThreads), 0, stream, seg, seg_bytes, descs, nblk, out);
 }
 
+#ifdef OKV_ABLATE  // the look-back stream kernel (ablation build only)
+#include "okv_decode_ablate_lb.inc"
+#endif
 }  // namespace okv
 
 // ===========================================================================
@@ -1919,101 +1877,9 @@ int ensure_fused(okv_ctx* ctx, uint32_t nblk) {
   return OKV_OK;
 }
 
-#ifdef OKV_ABLATE
-// Ablation build only (OKV_DECODE_PIECES=1): large-block decodes in two
-// pieces.  Measured at C3 (r4b, 3 alternating runs): count+scan 0.061 vs
-// 0.105 ms but the two tile launches 1.487 vs 1.384 ms, step 1.55 vs 1.48 ms:
-// the first piece's walk costs what the whole walk does (latency-bound), and
-// the second launch adds a tail.  The product decodes in one piece.
-// The header walk of the first
-// kPieceDiv-th of the blocks, then the tile pass over them on the context's
-// stream while the second piece's walk runs on a second stream; the second
-// tile pass waits for that walk.  The walk is latency-bound (a dependent
-// chain per block, ~0.09 ms at C3 whatever the block count), so only the
-// first piece's shorter walk stays in front of the bandwidth-bound pass 3.
-constexpr uint32_t kPieceDiv = 8;
-constexpr uint32_t kPieceMinBlocks = 8192;
-uint32_t piece_split(uint32_t nblk) {
-  if (nblk < kPieceMinBlocks) return 0;
-  return (nblk / kPieceDiv) & ~uint32_t(kTile - 1);  // a multiple of the count kernel's tile
-}
-
-int ensure_pieces(okv_ctx* ctx) {
-  if (ctx->stream2) return OKV_OK;
-  OKV_HIP(hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking));
-  OKV_HIP(hipEventCreateWithFlags(&ctx->ev_piece[0], hipEventDisableTiming));
-  OKV_HIP(hipEventCreateWithFlags(&ctx->ev_piece[1], hipEventDisableTiming));
-  OKV_HIP(hipMalloc(&ctx->d_tot2, sizeof(Totals)));
-  return OKV_OK;
-}
-
-// Passes 1-2 as two launches: blocks [0, b0) on the context stream (totals
-// into d_tot2), then -- once they are done -- blocks [b0, nblk) on stream2,
-// their prefixes continuing from d_tot2 (final totals into d_tot).
-int launch_plan_pieces(okv_ctx* ctx, const Work& w, uint32_t nblk, uint32_t b0,
-                       uint64_t* d_row_start, uint16_t* rt_kl, uint64_t span_cap) {
-  int rc = ensure_blocks(ctx, nblk);
-  if (rc) return rc;
-  if ((rc = ensure_pieces(ctx))) return rc;
-  uint32_t* const big = big_counter(ctx);
-  const uint32_t nA = b0, nB = nblk - b0;
-  hipLaunchKernelGGL(okv_count_kernel, dim3((nA + kTile - 1) / kTile), dim3(kThreads), 0,
-                     ctx->stream, w.seg, w.seg_bytes, w.descs, nA, w.comp, ctx->d_cnt, ctx->d_lp,
-                     ctx->d_tile_tot, ctx->d_rec, rt_kl, ctx->d_big, big, w.pre, 0, span_cap,
-                     ctx->d_tile_pre, ctx->d_tot2, nullptr, ctx->d_ctr + kCtrArrive,
-                     big_counter(ctx, 1), nullptr, 0u, nullptr);
-  OKV_HIP(hipGetLastError());
-  OKV_HIP(hipEventRecord(ctx->ev_piece[0], ctx->stream));
-  OKV_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_piece[0], 0));
-  const uint64_t t0 = b0 / kTile;
-  hipLaunchKernelGGL(okv_count_kernel, dim3((nB + kTile - 1) / kTile), dim3(kThreads), 0,
-                     ctx->stream2, w.seg, w.seg_bytes, w.descs + b0, nB, w.comp, ctx->d_cnt + b0,
-                     ctx->d_lp + b0, ctx->d_tile_tot + t0, ctx->d_rec + uint64_t(b0) * kRCap,
-                     rt_kl ? rt_kl + uint64_t(b0) * kRCap : nullptr, ctx->d_big, big,
-                     w.pre ? w.pre + b0 : nullptr, 0, span_cap, ctx->d_tile_pre + t0, ctx->d_tot,
-                     d_row_start ? d_row_start + b0 : nullptr, ctx->d_ctr + kCtrArrive, nullptr,
-                     ctx->d_tot2, b0, nullptr);
-  OKV_HIP(hipGetLastError());
-  OKV_HIP(hipEventRecord(ctx->ev_piece[1], ctx->stream2));
-  ctx->big_slot ^= 1u;  // the first launch zeroed the other slot
-  prof_mark(ctx, 2);
-  prof_mark(ctx, 3);
-  return OKV_OK;
-}
-
-// The CopyParams of blocks [b0, b0 + n) of P (block-indexed arrays advanced;
-// row and arena positions stay global).
-CopyParams piece_params(const CopyParams& P, uint32_t b0, uint32_t n) {
-  CopyParams Q = P;
-  Q.descs = P.descs + b0;
-  Q.nblk = n;
-  Q.cnt = P.cnt + b0;
-  Q.lp = P.lp + b0;
-  Q.tile_pre = P.tile_pre + b0 / kTile;
-  Q.rt_pos = P.rt_pos + uint64_t(b0) * kRCap;
-  Q.rt_kl = P.rt_kl ? P.rt_kl + uint64_t(b0) * kRCap : nullptr;
-  Q.row_start = P.row_start + b0;
-  Q.key_base = P.key_base ? P.key_base + b0 : nullptr;
-  Q.val_base = P.val_base ? P.val_base + b0 : nullptr;
-  Q.blk_status = P.blk_status + b0;
-  return Q;
-}
-
-// Pass 1-2 of blocks [b0, b0 + n) (b0 a multiple of kTile) continuing the
-// prefixes of the blocks before them (base: their totals, or null), totals
-// into tot; the piece's record table at d_rec + b0 * kRCap (its own layout).
-void launch_count_piece(okv_ctx* ctx, const Work& w, uint32_t b0, uint32_t n, uint64_t* d_row_start,
-                        const Totals* base, Totals* tot, bool first) {
-  const uint64_t t0 = b0 / kTile;
-  hipLaunchKernelGGL(okv_count_kernel, dim3((n + kTile - 1) / kTile), dim3(kThreads), 0,
-                     ctx->stream, w.seg, w.seg_bytes, w.descs + b0, n, w.comp, ctx->d_cnt + b0,
-                     ctx->d_lp + b0, ctx->d_tile_tot + t0, ctx->d_rec + uint64_t(b0) * kRCap,
-                     nullptr, ctx->d_big, big_counter(ctx), w.pre ? w.pre + b0 : nullptr, 0,
-                     ~0ull, ctx->d_tile_pre + t0, tot, d_row_start ? d_row_start + b0 : nullptr,
-                     ctx->d_ctr + kCtrArrive, first ? big_counter(ctx, 1) : nullptr, base, b0,
-                     nullptr);
-}
-#endif  // OKV_ABLATE
+#ifdef OKV_ABLATE  // the measured alternative forms of round 4 (ablation build only)
+#include "okv_decode_ablate_host.inc"
+#endif
 
 int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* descs,
                   uint32_t nblk, int comp, okv_decode_out* o, uint32_t flags) {

@@ -653,348 +653,9 @@ __device__ __forceinline__ void put_bytes(uint8_t* p, const uint8_t* s, uint64_t
   for (uint64_t i = 0; i < n; ++i) p[i] = s[i];
 }
 
-#ifdef OKV_ABLATE
-// Ablation build only (OKV_ENC_ONEPASS=1).  Measured at C4 (100 M rows, 48 828
-// chunks): 17.5 ms for the plan vs 1.27 ms for E1-E9 -- the inclusive state
-// crosses one chunk per cross-XCD hand-off (~360 ns), a serial frontier; the
-// product keeps E1-E9's pointer doubling (profiles/r4/c4_arms.log).
-// ---------------------------------------------------------------------------
-// EP: E1-E9 in one launch, for the common shape (no block longer than
-// kFuseLook rows).  One workgroup per chunk of kETile rows, chunks claimed in
-// order from a counter, so a workgroup only ever waits on chunks already
-// claimed by running workgroups.  Each stages the record sizes of its chunk
-// plus kFuseLook rows on either side, computes next(a) (:138-143) for them,
-// and from the rows behind the chunk the entry offsets the chain can have
-// into it (< jlim).  For every such entry it walks the chain through the
-// chunk in LDS -- (exit offset, blocks, sum of BlockSize (Q2, :171-182), sum
-// of meta entry sizes (block_stat.go:27-42)) -- and publishes that table; then
-// it looks back to the nearest chunk that has published its inclusive state
-// (first block start, blocks, bytes and meta bytes before the next chunk),
-// applies the tables of the chunks in between, publishes its own inclusive
-// state and emits its blocks: first row, BlockStat sizes and Offset, meta
-// entry offset.  No per-row array is written (the round-3 kernels wrote 12 B
-// per row and re-read them).  A block longer than kFuseLook rows, or a
-// chunk's BlockSize sum past 2^32, aborts the launch (every later chunk sees
-// the abort); the host then runs E1-E9.
-// Hand-off: payloads and flags through coherent (sc1) stores, payloads
-// drained before the flag, sc1 loads on the reader (cdna_hip_programming.md
-// G16, valid forms; as okv_decode_fused_kernel).
-// ---------------------------------------------------------------------------
-constexpr uint32_t kPlanWin = kFuseLook + kETile + kFuseLook;  // staged rows (2560)
-constexpr int kPlanItems = kPlanWin / kThreads;                // 10 per thread
-constexpr uint32_t kPlanStates = kFuseLook + kETile;          // rows with next() (2304)
-
-struct PlanChunk {  // state at the start of chunk c + 1, published by chunk c
-  uint64_t entry;   // its first block start, relative to the chunk start
-  uint64_t kb;      // blocks before it
-  uint64_t bytes;   // sum of BlockSize before it (its first block's Offset)
-  uint64_t ment;    // sum of meta index entry sizes before it
-};
-
-struct PlanParams {
-  const uint16_t* key_len;
-  const uint32_t* val_len;
-  uint64_t n, T, D;
-  int lz4;
-  uint64_t bloom_extra;  // 8 + filter bytes, or 0
-  uint64_t nch;
-  uint32_t* flag;        // [nch] (epoch << 2) | 1 table, | 2 inclusive, | 3 abort
-  PlanChunk* inc;        // [nch]
-  uint4* tab;            // [nch][kFuseLook] {exit | blocks << 16, bytes, meta bytes, 0}
-  uint32_t* jlim;        // [nch]
-  unsigned long long* ctr;
-  unsigned long long base;
-  uint32_t epoch;
-  uint64_t cap;          // capacity of first (cap + 1), desc, moff
-  uint64_t* first;
-  Desc* desc;
-  uint64_t* moff;
-  EncTotals* tot;
-};
-
-__device__ __forceinline__ void st_sc1(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ __launch_bounds__(kThreads) void okv_enc_plan_kernel(PlanParams P) {
-  __shared__ uint64_t W[kPlanWin + 1];    // W[m] = bytes of window rows [0, m)
-  __shared__ uint16_t s_nx[kPlanStates];  // next(a) - a of window rows [0, kPlanStates)
-  __shared__ uint16_t s_kl[kPlanStates];  // key lengths of the same rows
-  __shared__ uint16_t s_blk[kETile];      // the chain's block starts (chunk-relative)
-  __shared__ uint4 s_tab[kFuseLook];
-  __shared__ uint64_t sm[kThreads / 64 + 1];
-  __shared__ uint32_t s_c, s_abort, s_jlim, s_wmax, s_nblk;
-  __shared__ PlanChunk s_in;
-  const uint32_t tid = threadIdx.x;
-  if (tid == 0) {
-    s_c = uint32_t(atomicAdd(P.ctr, 1ull) - P.base);
-    s_abort = 0;
-    s_jlim = 0;
-    s_wmax = 0;
-  }
-  __syncthreads();
-  const uint64_t c = s_c;
-  if (c >= P.nch) return;
-  const uint32_t tag = P.epoch << 2;
-  const uint64_t n = P.n, cs = c * kETile;
-  const int64_t w0 = int64_t(cs) - int64_t(kFuseLook);  // window row 0 (< 0 for chunk 0)
-  // valid window rows [jlo, jhi)
-  const uint32_t jlo = c == 0 ? kFuseLook : 0u;
-  const uint32_t jhi = uint32_t(std::min<uint64_t>(kPlanWin, n + kFuseLook - cs));
-  const bool complete = int64_t(jhi) + w0 == int64_t(n);  // the window reaches the last row
-  const uint32_t owned = uint32_t(std::min<uint64_t>(kETile, n - cs));
-  // ---- record sizes (WriteRow frames 6 + len(key) + len(val), :121-125) ----
-  uint64_t bad = kNone, own_bytes = 0;
-  for (int i = 0; i < kPlanItems; ++i) {
-    const uint32_t j = uint32_t(i) * kThreads + tid;
-    uint64_t sz = 0;
-    if (j >= jlo && j < jhi) {
-      const uint64_t r = uint64_t(w0 + int64_t(j));
-      const uint32_t kl = P.key_len[r];
-      sz = 6u + uint64_t(kl) + uint64_t(P.val_len[r]);
-      if (j < kPlanStates) s_kl[j] = uint16_t(kl);
-      if (j >= kFuseLook && j < kFuseLook + owned) {
-        if (kl == 0 && r < bad) bad = r;  // empty key (:89-91)
-        own_bytes += sz;
-      }
-    }
-    W[j + 1] = sz;
-  }
-  __syncthreads();
-  {
-    uint64_t loc[kPlanItems], sum = 0;
-#pragma unroll
-    for (int i = 0; i < kPlanItems; ++i) {
-      sum += W[1 + tid * kPlanItems + i];
-      loc[i] = sum;
-    }
-    uint64_t total;
-    const uint64_t ex = wg_excl_scan(sum, sm, total);
-#pragma unroll
-    for (int i = 0; i < kPlanItems; ++i) W[1 + tid * kPlanItems + i] = ex + loc[i];
-    if (tid == 0) W[0] = 0;
-  }
-  __syncthreads();
-  // ---- next(a) for the rows behind and in the chunk: first m > a with
-  // W[m] >= W[a] + T, or the segment end; anything past kFuseLook rows aborts
-  {
-    uint32_t mb = 0, wm = 0;
-    bool ab = false;
-    for (int i = 0; i < kPlanItems; ++i) {
-      const uint32_t a = tid * kPlanItems + i;
-      if (a >= kPlanStates || a >= jhi) break;
-      if (a < jlo) continue;
-      const uint64_t target = W[a] + P.T;
-      if (mb <= a) {
-        uint32_t L = a + 1, H = jhi;
-        while (L < H) {
-          const uint32_t m = (L + H) >> 1;
-          if (W[m] >= target)
-            H = m;
-          else
-            L = m + 1;
-        }
-        mb = L;
-      } else {
-        while (mb < jhi && W[mb] < target) ++mb;
-      }
-      uint32_t d;
-      if (mb < jhi || (W[jhi] >= target && mb == jhi))
-        d = mb - a;  // the block's last row is window row mb - 1
-      else if (complete)
-        d = jhi - a;  // the segment ends first: next = n
-      else
-        d = 0xffffu;
-      if (d > kFuseLook) ab = true;
-      s_nx[a] = uint16_t(d > kFuseLook ? 1u : d);
-      if (a >= kFuseLook) wm = d > wm ? d : wm;
-    }
-    if (__any(ab) && (tid & 63) == 0) s_abort = 1;
-    const uint32_t wmw = uint32_t(wave_max64(wm));
-    if ((tid & 63) == 0) atomicMax(&s_wmax, wmw);
-  }
-  __syncthreads();
-  // ---- entry offsets the chain can have into this chunk: exits of the rows
-  // behind it (every block holds <= kFuseLook rows)
-  if (c == 0) {
-    if (tid == 0) s_jlim = 1;
-  } else if (tid < kFuseLook && !s_abort) {
-    const uint32_t e = tid + s_nx[tid];  // the next block start after row tid
-    if (e >= kFuseLook) atomicMax(&s_jlim, e - kFuseLook + 1);
-  }
-  __syncthreads();
-  const bool abort0 = s_abort != 0;
-  const uint32_t jlim = s_jlim;
-  // ---- the chunk's table: one chain per entry offset ----
-  if (!abort0 && tid < jlim) {
-    uint32_t pos = tid, cnt = 0;
-    uint64_t by = 0, me = 0;
-    while (pos < owned) {
-      const uint32_t a = kFuseLook + pos, d = s_nx[a];
-      const uint64_t raw = W[a + d] - W[a];
-      by += (raw / P.D + 1) * P.D;
-      me += 42u + s_kl[a];
-      ++cnt;
-      pos += d;
-    }
-    const uint4 t = make_uint4((pos - owned) | (cnt << 16), uint32_t(by), uint32_t(me),
-                               uint32_t(by >> 32));
-    s_tab[tid] = t;
-    if (c > 0) {
-      uint64_t* q = reinterpret_cast<uint64_t*>(P.tab + c * kFuseLook + tid);
-      st_sc1(q, uint64_t(t.x) | (uint64_t(t.y) << 32));
-      st_sc1(q + 1, uint64_t(t.z) | (uint64_t(t.w) << 32));
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // ---- look-back (one lane) ----
-  if (tid == 0) {
-    bool abort = abort0;
-    for (uint32_t j = 0; j < jlim && !abort; ++j)
-      if (s_tab[j].w) abort = true;  // a BlockSize sum past 2^32: the general path
-    PlanChunk in{0, 0, 0, 0};
-    if (c > 0 && !abort) {
-      __hip_atomic_store(P.jlim + c, jlim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(P.flag + c, tag | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // walk back to the nearest chunk with an inclusive state
-      uint64_t q = c - 1;
-      for (;;) {
-        uint32_t f = ld_sc1(P.flag + q);
-        while ((f & ~3u) != tag) {
-          __builtin_amdgcn_s_sleep(2);
-          f = ld_sc1(P.flag + q);
-        }
-        if ((f & 3u) == 3u) {
-          abort = true;
-          break;
-        }
-        if ((f & 3u) == 2u) {
-          const uint64_t* s = reinterpret_cast<const uint64_t*>(P.inc + q);
-          in.entry = ld_sc1(s);
-          in.kb = ld_sc1(s + 1);
-          in.bytes = ld_sc1(s + 2);
-          in.ment = ld_sc1(s + 3);
-          break;
-        }
-        --q;  // a table only (chunk 0 always publishes its inclusive state)
-      }
-      // apply the tables of the chunks in between, in order
-      for (uint64_t u = q + 1; u < c && !abort; ++u) {
-        if (in.entry >= ld_sc1(P.jlim + u)) {  // never expected: the entry sets are exact
-          atomicOr(&P.tot->fault, 1ull);
-          abort = true;
-          break;
-        }
-        const uint64_t* t = reinterpret_cast<const uint64_t*>(P.tab + u * kFuseLook + in.entry);
-        const uint64_t x = ld_sc1(t), y = ld_sc1(t + 1);
-        in.kb += uint32_t(x) >> 16;
-        in.bytes += uint32_t(x >> 32) + ((y >> 32) << 32);
-        in.ment += uint32_t(y);
-        in.entry = uint32_t(x) & 0xffffu;
-      }
-    }
-    if (!abort && in.entry >= jlim) {
-      atomicOr(&P.tot->fault, 1ull);
-      abort = true;
-    }
-    if (abort) {
-      __hip_atomic_store(P.flag + c, tag | 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      atomicOr(&P.tot->far, 1ull);
-      s_abort = 1;
-    } else {
-      const uint4 t = s_tab[in.entry];
-      PlanChunk out;
-      out.entry = t.x & 0xffffu;
-      out.kb = in.kb + (t.x >> 16);
-      out.bytes = in.bytes + t.y;
-      out.ment = in.ment + t.z;
-      uint64_t* s = reinterpret_cast<uint64_t*>(P.inc + c);
-      st_sc1(s, out.entry);
-      st_sc1(s + 1, out.kb);
-      st_sc1(s + 2, out.bytes);
-      st_sc1(s + 3, out.ment);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(P.flag + c, tag | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_in = in;
-      // the chain through this chunk, from its entry
-      uint32_t pos = uint32_t(in.entry), k = 0;
-      while (pos < owned) {
-        s_blk[k++] = uint16_t(pos);
-        pos += s_nx[kFuseLook + pos];
-      }
-      s_nblk = k;
-      if (c == P.nch - 1) {
-        P.tot->nb = out.kb;
-        P.tot->data_bytes = out.bytes;
-        P.tot->meta_ent = out.ment;
-      }
-    }
-  }
-  {  // empty keys (the first one's row: ErrInvalidKey)
-    const uint64_t bw = wave_min64(bad);
-    if ((tid & 63) == 0 && bw != kNone) atomicMin(&P.tot->bad_row, (unsigned long long)bw);
-  }
-  __syncthreads();
-  if (s_abort) return;
-  // ---- this chunk's blocks: first row, BlockStat sizes and Offset, meta
-  // entry offset (head + entries before) ----
-  const PlanChunk in = s_in;
-  const uint32_t nblk = s_nblk;
-  const uint64_t head = 2u + P.key_len[0] + 2u + P.key_len[n - 1] + 3u + 8u + P.bloom_extra;
-  const bool fits = in.kb + nblk <= P.cap;
-  uint64_t cb = 0, ce = 0, bmax = 0;
-  for (uint32_t i0 = 0; i0 < nblk; i0 += kThreads) {
-    const uint32_t i = i0 + tid;
-    uint64_t raw = 0, bs = 0, es = 0;
-    uint32_t a = 0;
-    if (i < nblk) {
-      a = kFuseLook + s_blk[i];
-      raw = W[a + s_nx[a]] - W[a];
-      bs = (raw / P.D + 1) * P.D;
-      es = 42u + s_kl[a];
-      bmax = bs > bmax ? bs : bmax;
-    }
-    uint64_t tb, te;
-    const uint64_t xb = wg_excl_scan(bs, sm, tb);
-    const uint64_t xe = wg_excl_scan(es, sm, te);
-    if (i < nblk && fits) {
-      const uint64_t k = in.kb + i;
-      P.first[k] = cs + s_blk[i];
-      Desc d;
-      d.offset = in.bytes + cb + xb;
-      d.block_size = bs;
-      d.original_size = raw;
-      d.compressed_size = P.lz4 ? raw : 0;  // (:165-167)
-      P.desc[k] = d;
-      P.moff[k] = head + in.ment + ce + xe;
-      if (c == P.nch - 1 && i == nblk - 1) {
-        P.tot->last_raw = raw;
-        P.first[k + 1] = n;
-      }
-    }
-    cb += tb;
-    ce += te;
-  }
-  if (!fits && tid == 0) atomicOr(&P.tot->pad[0], 1ull);  // capacity: the host grows and reruns
-  bmax = wave_max64(bmax);
-  if ((tid & 63) == 0) {
-    if (bmax) atomicMax(&P.tot->bmax, (unsigned long long)bmax);
-    atomicAdd(&P.tot->total_raw, (unsigned long long)wave_sum64_u(own_bytes));
-    if (tid == 0) {
-      atomicMax(&P.tot->wmax, (unsigned long long)s_wmax);
-      if (c == 0) P.tot->head = head;
-    }
-  }
-}
-#endif  // OKV_ABLATE
+#ifdef OKV_ABLATE  // the single-pass plan kernel (ablation build only, OKV_ENC_ONEPASS=1)
+#include "okv_encode_ablate.inc"
+#endif
 
 // ---------------------------------------------------------------------------
 // E10: pack.  One workgroup per block; lane l of a pass owns destination
@@ -1894,94 +1555,8 @@ int enc_row_prefix(okv_ctx* ctx, EncScratch* e, const DevRows& R, uint64_t T) {
 }
 
 #ifdef OKV_ABLATE  // A/B arm OKV_ENC_ONEPASS=1 (the single-pass plan, measured slower)
-// E1-E9 in one launch (okv_enc_plan_kernel).  *general = true when the shape
-// needs the general kernels (a block longer than kFuseLook rows): the caller
-// then runs enc_plan.
-int enc_plan_fast(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opts& o,
-                  Plan* pl, uint64_t* bad_row, bool* general) {
-  const uint64_t n = R.n;
-  const uint64_t nch = (n + kETile - 1) / kETile;
-  int rc;
-  *general = false;
-  e->have_pl = false;
-  if (nch > e->cap_pch || !e->p_flag) {
-    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->p_flag), nch * 4))) return rc;
-    OKV_HIP(hipMemsetAsync(e->p_flag, 0, nch * 4, ctx->stream));
-    if ((rc = dev_realloc(ctx, &e->p_inc, nch * sizeof(PlanChunk)))) return rc;
-    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->p_tab), nch * kFuseLook * 16)))
-      return rc;
-    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->p_jlim), nch * 4))) return rc;
-    e->cap_pch = nch;
-  }
-  if (!e->p_ctr) {
-    OKV_HIP(hipMalloc(&e->p_ctr, sizeof(unsigned long long)));
-    OKV_HIP(hipMemsetAsync(e->p_ctr, 0, sizeof(unsigned long long), ctx->stream));
-    e->p_base = 0;
-  }
-  // per-block outputs: the last capacity, or a guess (a block of 4 KiB holds
-  // tens of small rows); a launch that finds more blocks is rerun once
-  uint64_t cap = std::max<uint64_t>(e->cap_blocks ? e->cap_blocks - 1 : 0, n / 32 + 1024);
-  cap = std::min<uint64_t>(cap, n);
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    if ((rc = ensure_blocks_enc(ctx, e, cap))) return rc;
-    enc_mark(ctx, e, 0);
-    hipLaunchKernelGGL(okv_enc_init_kernel, dim3(1), dim3(1), 0, ctx->stream, e->d_tot);
-    PlanParams P;
-    P.key_len = R.kl;
-    P.val_len = R.vl;
-    P.n = n;
-    P.T = o.threshold_bytes;
-    P.D = o.block_size;
-    P.lz4 = o.compression == OKV_COMP_LZ4;
-    P.bloom_extra = o.bloom ? 8 + o.bloom_len : 0;
-    P.nch = nch;
-    P.flag = e->p_flag;
-    P.inc = static_cast<PlanChunk*>(e->p_inc);
-    P.tab = e->p_tab;
-    P.jlim = e->p_jlim;
-    P.ctr = e->p_ctr;
-    P.base = e->p_base;
-    e->p_epoch = (e->p_epoch % 0x3fffffffu) + 1;  // never 0 (the zeroed flags)
-    P.epoch = e->p_epoch;
-    P.cap = cap;
-    P.first = e->first;
-    P.desc = e->desc;
-    P.moff = e->moff;
-    P.tot = e->d_tot;
-    hipLaunchKernelGGL(okv_enc_plan_kernel, dim3(uint32_t(nch)), dim3(kThreads), 0, ctx->stream,
-                       P);
-    const hipError_t le = hipGetLastError();
-    if (le != hipSuccess) return set_err(ctx, OKV_E_HIP, "okv_enc_plan_kernel launch", le);
-    e->p_base += nch;  // every workgroup claims one chunk
-    if ((rc = read_enc_totals(ctx, e))) return rc;
-    const EncTotals& t = *e->h_tot;
-    if (t.far) {
-      *general = true;
-      return OKV_OK;
-    }
-    if (t.bad_row != kNone) {
-      *bad_row = t.bad_row;
-      return set_err(ctx, OKV_W_INVALID_KEY, "key cannot be empty (ErrInvalidKey)");
-    }
-    if (t.fault || t.nb == 0 || t.nb > n) return set_err(ctx, OKV_E_HIP, "encode: inconsistent plan");
-    if (t.pad[0]) {  // more blocks than the guess: grow and rerun
-      cap = t.nb;
-      continue;
-    }
-    pl->nb = t.nb;
-    pl->data_bytes = t.data_bytes;
-    pl->head = t.head;
-    pl->meta_bytes = t.head + t.meta_ent;
-    pl->file_bytes = pl->data_bytes + pl->meta_bytes + 25;
-    pl->last_raw = t.last_raw;
-    pl->w = std::max<uint64_t>(1, t.wmax);
-    pl->bmax = t.bmax;
-    pl->avg_rec = t.total_raw / n;
-    return OKV_OK;
-  }
-  return set_err(ctx, OKV_E_HIP, "encode: plan capacity");
-}
-#endif  // OKV_ABLATE
+#include "okv_encode_ablate_host.inc"
+#endif
 
 // Block boundaries, BlockStat sizes/offsets and meta layout (E1-E9).
 int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opts& o, Plan* pl,

@@ -18,10 +18,14 @@ ABLATE = os.path.join(ROOT, "objectkv_amd", "libokv_sst_ablate.so")
 # kernels of the measured alternative forms: ablation build only
 ABLATION_ONLY = [b"okv_value_sweep_kernel", b"okv_rows_kernel", b"okv_gather_staged_kernel",
                  b"okv_gather_kernel", b"okv_tile_kernel_w7", b"okv_scan_kernel",
-                 b"okv_tile_kernel_diag"]
+                 b"okv_tile_kernel_diag",
+                 # round 4's measured-and-not-kept forms
+                 b"okv_decode_stream_kernel", b"okv_enc_plan_kernel", b"fused_prefix_lookback"]
 KNOBS = [b"OKV_GATHER_THREADS", b"OKV_GATHER_GRID", b"OKV_DECODE_FUSED", b"OKV_GATHER_STAGED",
          b"OKV_VALUE_SWEEP", b"OKV_TILE", b"OKV_ZSTD_GENERAL", b"OKV_ZSTD_PROF",
-         b"OKV_ENC_VARIANT", b"OKV_ENC_IMAGE"]
+         b"OKV_ENC_VARIANT", b"OKV_ENC_IMAGE", b"OKV_DECODE_PIECES", b"OKV_DECODE_STREAM",
+         b"OKV_SMALL_PIECE_MB", b"OKV_COUNT_PREFETCH", b"OKV_ENC_ONEPASS", b"OKV_ENC_META_FUSED",
+         b"OKV_ZSTD_HUF_BLOCKS"]
 
 
 def _bytes(path):
@@ -55,8 +59,20 @@ def test_product_source_holds_only_product_kernels():
         assert not re.search(r"void\s+" + name + r"\s*\(", src), name
     for arm in ("kProbe", "kDirect", "kChunk", "kDiag == 1", "kDiag == 4", "kDiag == 5"):
         assert arm not in src, arm
-    inc = src.index('#include "okv_decode_ablate.inc"')
-    assert src.rfind("#ifdef OKV_ABLATE", 0, inc) > src.rfind("#endif", 0, inc)
+    for inc_name in ("okv_decode_ablate.inc", "okv_decode_ablate_host.inc",
+                     "okv_decode_ablate_lb.inc"):
+        inc = src.index(f'#include "{inc_name}"')
+        assert src.rfind("#ifdef OKV_ABLATE", 0, inc) > src.rfind("#endif", 0, inc), inc_name
+    # round 4's arms are in the includes, not in the product translation units
+    for name in ("okv_decode_stream_kernel", "launch_plan_pieces", "launch_count_piece",
+                 "piece_params"):
+        assert not re.search(r"\b" + name + r"\s*\([^;]*\)\s*\{", src), name
+    enc = open(os.path.join(ROOT, "objectkv_amd", "csrc", "okv_encode.hip")).read()
+    for name in ("okv_enc_plan_kernel", "enc_plan_fast"):
+        assert not re.search(r"\b" + name + r"\s*\([^;]*\)\s*\{", enc), name
+    for inc_name in ("okv_encode_ablate.inc", "okv_encode_ablate_host.inc"):
+        inc = enc.index(f'#include "{inc_name}"')
+        assert enc.rfind("#ifdef OKV_ABLATE", 0, inc) > enc.rfind("#endif", 0, inc), inc_name
 
 
 def test_product_reads_no_environment():
@@ -70,7 +86,8 @@ def test_product_reads_no_environment():
 
 def test_ablation_build_carries_the_alternatives():
     data = _bytes(ABLATE)
-    for name in (b"okv_value_sweep_kernel", b"okv_gather_staged_kernel", b"okv_tile_kernel_w7"):
+    for name in (b"okv_value_sweep_kernel", b"okv_gather_staged_kernel", b"okv_tile_kernel_w7",
+                 b"okv_decode_stream_kernel", b"okv_enc_plan_kernel"):
         assert name in data, name
     for knob in (b"OKV_VALUE_SWEEP", b"OKV_TILE", b"OKV_ZSTD_PROF"):
         assert knob in data, knob

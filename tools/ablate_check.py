@@ -1,0 +1,53 @@
+"""Parity of the ablation arms (ablation build, OKV_ABLATE=1 with the arm's
+knob set): the arm must be the path taken and its outputs equal the oracle's.
+usage: OKV_ABLATE=1 <knob>=1 python tools/ablate_check.py stream|pieces|small_pieces|onepass"""
+import os
+import random
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+import objectkv_amd as okv  # noqa: E402
+from objectkv_amd import _lib  # noqa: E402
+from tests import test_decode_gpu as TD  # noqa: E402
+from tests import test_encode_gpu as TE  # noqa: E402
+
+arm = sys.argv[1]
+assert _lib.LIB_PATH.endswith("libokv_sst_ablate.so"), _lib.LIB_PATH
+if arm in ("stream", "small_pieces"):
+    rng = np.random.default_rng(5)
+    kinds = list(rng.choice(["s"] * 12 + ["M"], size=3000))
+    seg, d = TD._mixed_segment(kinds, 8)
+    dec = okv.Decoder(0)
+    for index_only in (False, True):
+        got = dec.decode(seg, d, index_only=index_only)
+        if arm == "stream":
+            assert dec.last_path() & _lib.PATH_STREAM, dec.last_path()
+        TD._assert_same_as_oracle(got, seg, d, 0, index_only)
+    dec.close()
+elif arm == "pieces":
+    n = 9000
+    kinds = ["L"] * n
+    for i in (0, 3, 1023, 1024, 1025, 4000, n - 1):
+        kinds[i] = "M"
+    seg, d = TD._mixed_segment(kinds, 21)
+    seg = seg + bytes(4096)
+    dec = okv.Decoder(0)
+    for index_only in (False, True):
+        got = dec.decode(seg, d, index_only=index_only)
+        assert dec.last_path() & _lib.PATH_TILE, dec.last_path()
+        TD._assert_same_as_oracle(got, seg, d, 0, index_only)
+    dec.close()
+elif arm == "onepass":
+    enc = okv.Encoder(0)
+    for T, vmax in ((50, 60), (3584, 120), (9000, 60), (3584, 3000)):
+        rng = random.Random(T + vmax)
+        rows = TE._random_rows(rng, 30000 if vmax <= 120 else 9000, 8, vmax)
+        rc, want, meta = TE.oracle_segment(rows, T, 4096)
+        got = enc.encode(rows, T, 4096, strict_go=rc == 0)
+        if rc == 0:
+            assert got.seg.tobytes() == want
+        assert enc.last_path() & _lib.PATH_ENC_ONEPASS, enc.last_path()
+    enc.close()
+print(f"ablation arm {arm}: parity ok")

@@ -434,8 +434,6 @@ __device__ __forceinline__ void gather_tiles(const Src& src, const GatherSmem& s
   const uint32_t N = (total + 15) >> 4;  // chunks, including the padded tail
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t last = uint32_t(rows) - 1;
-  uint32_t r = 0;
-  bool searched = false;
   const uint32_t cmax = (N < t1 * 64 ? N : t1 * 64) - 1;  // last chunk of the range (ts == 1)
   for (uint32_t t = t0; t < t1; t += kU * ts) {
     uint4 v[kU];
@@ -446,21 +444,20 @@ __device__ __forceinline__ void gather_tiles(const Src& src, const GatherSmem& s
       const uint32_t c = (t + u * ts) * 64 + lane;
       const bool ok = (t + u * ts) < t1 && c < N;
       // lanes past the range reload the range's last chunk (an address a
-      // valid lane loads in this iteration; x stays monotone for the linear
-      // advance).  Pointing them at the range's first tile with the current
-      // row's bias re-fetched ~40 evicted lines per block (0.32 GB at C3).
+      // valid lane loads in this iteration).  Pointing them at the range's
+      // first tile with the current row's bias re-fetched ~40 evicted lines
+      // per block (0.32 GB at C3).
       const uint32_t x = (ok ? c : cmax) << 4;
-      if (!searched) {  // binary search: r = #{k in [1, rows] : pre[k] <= x}
-        uint32_t pos = 0;
+      // the row holding byte x: r = #{k in [1, rows) : pre[k] <= x}, a binary
+      // search per chunk (pre[rows] = total > x ends every probe past the
+      // last row).  The kU searches are independent, so their LDS reads
+      // overlap; advancing linearly from the previous chunk's row cost one
+      // dependent read per row passed (16 per tile for 64-byte rows).
+      uint32_t r = 0;
 #pragma unroll
-        for (uint32_t st = 64; st; st >>= 1) {
-          const uint32_t j = pos + st;
-          if (j <= last && pre[j] <= x) pos = j;
-        }
-        r = pos;
-        searched = true;
-      } else {
-        while (r < last && pre[r + 1] <= x) ++r;
+      for (uint32_t st = 64; st; st >>= 1) {
+        const uint32_t j = r + st;
+        r = pre[min(j, last + 1)] <= x ? j : r;
       }
       rr[u] = r;
       v[u] = src.at(int64_t(sb[r]) + int64_t(x));

@@ -1274,6 +1274,11 @@ struct MetaParams {
   int comp_byte;
   uint8_t* meta;
   uint64_t bloom_len;  // ~0: no bloom filter; else its WriteTo length
+  // the segment the pack kernel wrote (uncompressed blocks): each block's
+  // FirstKey is read from its first record there, one line per block, instead
+  // of through the row arrays (key_len, key_off and the key: three scattered
+  // lines); null: through the row arrays
+  const uint8_t* seg = nullptr;
 };
 
 __global__ __launch_bounds__(kThreads) void okv_enc_meta_kernel(MetaParams P) {
@@ -1314,6 +1319,20 @@ __global__ __launch_bounds__(kThreads) void okv_enc_meta_kernel(MetaParams P) {
   put_le(p + 32, P.hash[k], 8);
 }
 
+// Block k's FirstKey (block_stat.go:31-33): the key of its first record.
+__device__ __forceinline__ void first_key(const MetaParams& P, uint64_t k, const Desc& d,
+                                          uint32_t& kl, const uint8_t*& key) {
+  if (P.seg) {  // [u16 LE kl][u32 LE vl][key] at the block's start
+    const uint8_t* rec = P.seg + d.offset;
+    kl = uint32_t(rec[0]) | (uint32_t(rec[1]) << 8);
+    key = rec + 6;
+  } else {
+    const uint64_t r = P.first[k];
+    kl = P.key_len[r];
+    key = P.key_arena + P.key_off[r];
+  }
+}
+
 // E12 via LDS: one workgroup builds the entries of kThreads consecutive blocks
 // (one contiguous byte range of the meta block, <= kMetaImage bytes) in an LDS
 // image and stores it with aligned 16-byte stores; the range's unaligned head
@@ -1335,12 +1354,13 @@ __global__ __launch_bounds__(kThreads) void okv_enc_meta_lds_kernel(MetaParams P
   if (big) {  // long first keys: byte stores
     if (k < k1) {
       uint8_t* p = P.meta + P.moff[k];
-      const uint64_t r = P.first[k];
-      const uint32_t kl = P.key_len[r];
-      put_le(p, kl, 2);
-      put_bytes(p + 2, P.key_arena + P.key_off[r], kl);
-      p += 2 + kl;
       const Desc d = P.desc[k];
+      uint32_t kl;
+      const uint8_t* key;
+      first_key(P, k, d, kl, key);
+      put_le(p, kl, 2);
+      put_bytes(p + 2, key, kl);
+      p += 2 + kl;
       put_le(p, d.offset, 8);
       put_le(p + 8, d.block_size, 8);
       put_le(p + 16, d.original_size, 8);
@@ -1353,12 +1373,13 @@ __global__ __launch_bounds__(kThreads) void okv_enc_meta_lds_kernel(MetaParams P
   __syncthreads();
   if (k < k1) {
     const uint32_t d = uint32_t(P.moff[k] - a0);
-    const uint64_t r = P.first[k];
-    const uint32_t kl = P.key_len[r];
     const Desc ds = P.desc[k];
     const uint64_t h = P.hash[k];
+    uint32_t kl;
+    const uint8_t* key;
+    first_key(P, k, ds, kl, key);
     lds_or16(img, d, make_uint4(kl & 0xffffu, 0, 0, 0));  // only 2 bytes are non-zero
-    lds_copy_field(img, d + 2, P.key_arena + P.key_off[r], kl);
+    if (kl) lds_copy_field(img, d + 2, key, kl);
     const uint32_t e = d + 2 + kl;
     lds_or16(img, e, make_uint4(uint32_t(ds.offset), uint32_t(ds.offset >> 32),
                                 uint32_t(ds.block_size), uint32_t(ds.block_size >> 32)));
@@ -1779,6 +1800,7 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   mp.comp_byte = o.compression == OKV_COMP_LZ4 ? 2 : 0;
   mp.meta = seg + pl.data_bytes;
   mp.bloom_len = o.bloom ? o.bloom_len : ~uint64_t(0);
+  mp.seg = o.compression == OKV_COMP_NONE ? seg : nullptr;
   if (o.bloom && o.bloom_len)  // BloomFilter.WriteTo bytes at head - 10 - len (after flag + u64)
     OKV_HIP(hipMemcpyAsync(mp.meta + pl.head - 10 - o.bloom_len, o.bloom, o.bloom_len,
                            hipMemcpyHostToDevice, ctx->stream));

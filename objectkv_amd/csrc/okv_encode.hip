@@ -643,7 +643,9 @@ __global__ __launch_bounds__(kThreads) void okv_enc_offset_kernel(
   if (k >= nb) return;
   const uint64_t t = k / kETile;
   desc[k].offset = btile_pre[t] + bsl[k] - desc[k].block_size;
-  moff[k] = head + etile_pre[t] + esl[k] - (42u + key_len[first[k]]);
+  // esl: E8's tile-inclusive prefix of entry sizes, so the exclusive one is
+  // the previous block's (no second read of the block's first key length)
+  moff[k] = head + etile_pre[t] + (k % kETile ? esl[k - 1] : 0u);
 }
 
 __device__ __forceinline__ void put_le(uint8_t* p, uint64_t v, int nbytes) {

@@ -33,6 +33,7 @@ extern "C" {
 #define OKV_M_PANIC (-205)           /* mustReadBytes panic while parsing */
 #define OKV_M_IO (-206)              /* Seek/Read error */
 #define OKV_M_MAKESLICE (-207)       /* make([]byte, negative) panic :124 */
+#define OKV_M_BLOOM (-208)           /* BloomFilter.ReadFrom error: parseBloomFilterBlock :160-163 */
 #define OKV_R_NO_ROWS (-301)         /* ErrNoRows          :357 */
 #define OKV_R_EOF (-302)             /* io.EOF from RowIter.Next */
 #define OKV_R_CLOSED (-303)          /* ErrClosed          segment_row_iter.go:27 */
@@ -83,6 +84,13 @@ const uint8_t *okv_meta_last_key(const okv_meta *m, uint64_t *len);
 int okv_meta_block(const okv_meta *m, uint64_t i, okv_block_desc *desc, uint64_t *hash,
                    const uint8_t **first_key, uint64_t *first_key_len);
 void okv_meta_free(okv_meta *m);
+/* The meta block's bloom filter (parseBloomFilterBlock :183-201) and its Test
+ * (probeBloomFilter :245-258; bits-and-blooms v2.0.3 + murmur3 v1.1.0 +
+ * bitset v1.1.11 restated on the host, filter bytes parity-unpinned).
+ * okv_meta_bloom_test: 1 maybe present (also with no filter), 0 absent,
+ * OKV_R_PANIC for a filter with m == 0 (Go's integer division panic). */
+int okv_meta_has_bloom(const okv_meta *m);
+int okv_meta_bloom_test(const okv_meta *m, const uint8_t *key, size_t klen);
 
 /* ---- SegmentReader / RowIter over the GPU decode -------------------------- */
 /* A row as Go's KVPair (segment_reader.go:285-288): NULL pointer = nil slice.

@@ -31,10 +31,11 @@
 extern "C" {
 #endif
 
-#define OKV_ABI_VERSION 4 /* 2: okv_encode_opts.bloom / bloom_len, and okv_profile_read writes
+#define OKV_ABI_VERSION 5 /* 2: okv_encode_opts.bloom / bloom_len, and okv_profile_read writes
                              4 doubles (ms[4]: the zstd stage slot was added);
                              3: okv_open_ex / okv_open_opts
-                             4: okv_decode_chain */
+                             4: okv_decode_chain
+                             5: OKV_OPEN_NO_POINT / OKV_PATH_POINT (host-mode point path) */
 
 /* ---- return codes (int) -------------------------------------------------- */
 #define OKV_OK 0
@@ -136,6 +137,10 @@ okv_ctx *okv_open_on_stream(int device, void *stream);
 #define OKV_OPEN_ZSTD_ONE_PASS 2u /* zstd blocks: the one-wave-per-block decoder for every block
                                      (one launch, no host synchronisation between stages: lower
                                      latency for a few blocks); outputs identical */
+#define OKV_OPEN_NO_POINT 4u      /* host-mode calls never take the point path (okv_point_kernel:
+                                     <= 16 small uncompressed blocks in one launch over pinned
+                                     memory): every batch is staged to device memory and decoded
+                                     by the device-resident kernels; outputs identical */
 typedef struct okv_open_opts {
   uint32_t size;  /* sizeof(okv_open_opts) */
   uint32_t flags; /* OKV_OPEN_* */
@@ -389,6 +394,8 @@ int okv_profile_read(okv_ctx *ctx, double *ms, uint64_t *calls);
                                      builds only (OKV_ENC_ONEPASS=1); the product runs E1-E9 */
 #define OKV_PATH_ZSTD_REGROW 256u /* zstd frames outgrew their first output region and were
                                      measured and decoded again (io.Copy inflates them all) */
+#define OKV_PATH_POINT 2048u /* okv_point_kernel: a host-mode call of a few small uncompressed
+                                blocks (GetRow, GetRange) in one launch over pinned memory */
 uint32_t okv_last_path(const okv_ctx *ctx);
 
 /* Device / pinned-host memory helpers for callers without another allocator. */

@@ -20,11 +20,12 @@ OKV_OK, OKV_E_ARG, OKV_E_HIP, OKV_E_CAPACITY, OKV_E_NOMEM, OKV_E_NODEV = 0, -1, 
 BLK_OK, BLK_EOF, BLK_SHORT, BLK_PANIC, BLK_UNSUPPORTED, BLK_CAPACITY = 0, 1, 2, 3, 4, 5
 COMP_NONE, COMP_ZSTD, COMP_LZ4 = 0, 1, 2
 F_DEVICE_PTRS, F_INDEX_ONLY, F_ASYNC, F_NO_CLOSE = 1, 2, 4, 8
-OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS = 1, 2
+OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS, OPEN_NO_POINT = 1, 2, 4
 # okv_last_path bits (include/okv_sst.h OKV_PATH_*)
 PATH_FUSED, PATH_SMALL, PATH_TILE, PATH_SWEEP = 1, 2, 4, 8
 PATH_STAGED, PATH_GATHER, PATH_BIG, PATH_ZSTD = 16, 32, 64, 128
 PATH_ZSTD_REGROW, PATH_ENC_ONEPASS, PATH_STREAM = 256, 512, 1024
+PATH_POINT = 2048
 # SegmentWriter sentinels (okv_sst.h OKV_W_*)
 W_KEY_TOO_LARGE, W_VALUE_TOO_LARGE, W_CLOSED, W_INVALID_KEY = -101, -102, -103, -104
 W_NIL_WRITER, W_UNSUPPORTED, W_NO_ROWS = -105, -106, -107
@@ -47,7 +48,7 @@ SYMBOLS = [
     "okv_writer_set_bloom",
     "okv_meta_fetch", "okv_meta_parse", "okv_meta_num_blocks", "okv_meta_compression",
     "okv_meta_descs", "okv_meta_first_key", "okv_meta_last_key", "okv_meta_block",
-    "okv_meta_free", "okv_synth_segment",
+    "okv_meta_free", "okv_meta_has_bloom", "okv_meta_bloom_test", "okv_synth_segment",
     "okv_reader_open", "okv_reader_fetch_metadata", "okv_reader_load_metadata",
     "okv_reader_num_blocks", "okv_reader_read_block", "okv_reader_get_row",
     "okv_reader_get_range", "okv_reader_close", "okv_reader_free", "okv_reader_row_iter",
@@ -197,6 +198,8 @@ def lib():
         "okv_writer_set_bloom": (None, [p, p, u64]),
         "okv_meta_fetch": (i32, [p, u64, C.c_int64, C.POINTER(p)]),
         "okv_meta_parse": (i32, [p, u64, C.POINTER(p)]),
+        "okv_meta_has_bloom": (i32, [p]),
+        "okv_meta_bloom_test": (i32, [p, p, C.c_size_t]),
         "okv_meta_num_blocks": (u64, [p]),
         "okv_meta_compression": (i32, [p]),
         "okv_meta_descs": (p, [p]),

@@ -51,6 +51,7 @@ struct okv_ctx {
   bool fused = true;               // OKV_DECODE_FUSED=0: passes 1-3 as separate launches
   uint32_t fused_max = 0;          // largest fused batch: resident-capacity bound (okv_open)
   bool zstd_one_pass = false;      // OKV_OPEN_ZSTD_ONE_PASS: every zstd block by the general kernel
+  bool point = true;               // host-mode point path (okv_point_kernel); OKV_OPEN_NO_POINT: off
   uint32_t* f_flag = nullptr;      // [nblk] look-back flags, tagged with f_epoch
   okv::Prefix* f_agg = nullptr;
   okv::Prefix* f_incl = nullptr;
@@ -89,6 +90,10 @@ struct okv_ctx {
   size_t cap_out = 0;
   uint64_t* d_hash = nullptr;
   size_t cap_hash = 0;
+  // host-mode point reads (okv_point_kernel): one pinned slab holding the
+  // staged blocks, their descriptors and every output
+  uint8_t* h_slab = nullptr;
+  size_t cap_slab = 0;
   // per-pass event timing (okv_profile)
   uint32_t gather_grid = 0;  // 0: default grid; else workgroups (OKV_GATHER_GRID)
   uint32_t gather_threads = 0;  // 0: by average block size; else 64 or 256 (OKV_GATHER_THREADS)

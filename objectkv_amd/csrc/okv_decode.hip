@@ -258,6 +258,11 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
       __hip_atomic_store(&q->vb, t.vb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&q->bad, t.bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef OKV_COUNT_ARRIVE_RELAXED
+      const uint32_t a =
+          __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = a == gridDim.x - 1;
+#else
       const uint32_t a =
           __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       s_last = a == gridDim.x - 1;
@@ -265,6 +270,7 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+#endif
     }
   }
   __syncthreads();
@@ -632,17 +638,22 @@ __device__ __forceinline__ void sweep_handoff(const CopyParams& P, const GatherS
 // XCDs round-robin), so a block's metadata and the chunks two tiles share
 // meet in one L2.
 // ---------------------------------------------------------------------------
-struct TileRows {
+template <uint32_t kUnits>
+struct TileRowsT {
   uint32_t pre[2][kRCap + 1];  // [key, value] exclusive prefix of lengths (pre[rows] = total)
   uint32_t sb[2][kRCap];       // block position of region byte x of row r = sb[r] + x
   uint32_t x[4];               // owned key range [x0, x1), value range [x2, x3)
   // value runs (kRuns): whole value chunks in units of <= 64 inside one
   // row piece {dest chunk, stage byte of its first chunk, count}, and the
   // value chunks that mix rows, padding or a neighbouring tile's bytes
-  uint32_t unit[3][96];
+  uint32_t unit[3][kUnits];
   uint32_t bnd[kRCap + 2];
   uint32_t nunit, nbnd;
 };
+// value runs of a kT-byte tile: at most one partial run per row plus kT / 1 KiB
+// whole ones (16 KiB tiles: 96 entries, as before)
+template <uint32_t kT>
+using TileRows = TileRowsT<(kT / 1024 + kRCap + 16 + 15) & ~15u>;
 
 // 16 bytes at byte s (0..15, wave-uniform) of the 32-byte window (x, y): a
 // scalar branch picks the dwords, then 4 v_alignbyte.
@@ -689,7 +700,7 @@ __device__ __noinline__ uint4 tile_chunk_pieces(const uint8_t* seg, uint64_t seg
 template <uint32_t kT, uint32_t kNT, bool kXcd>
 __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uint32_t ntile) {
   constexpr uint32_t kG = kT / 64 + 8;  // 64-byte destination granules of the key range
-  __shared__ TileRows R;
+  __shared__ TileRows<kT> R;
   __shared__ uint8_t gt[1][kG];         // row holding key byte max(64 g, range start)
   __shared__ uint4 stage[kT / 16 + 4];
   uint32_t L = blockIdx.x;
@@ -942,7 +953,7 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
 // 8 waves per SIMD (8 workgroups per CU: the LDS bound; registers capped at
 // 64 per lane, no spills; the uncapped form measured equal).
 template <uint32_t kT, uint32_t kNT, bool kXcd>
-__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kT <= 16384 ? 8 : 4))) void okv_tile_kernel(
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(kT <= 16384 || kNT == 1024 ? 8 : 4))) void okv_tile_kernel(
     CopyParams P, uint32_t tpb, uint32_t ntile) {
   tile_pass<kT, kNT, kXcd>(P, tpb, ntile);
 }
@@ -1424,6 +1435,27 @@ __device__ __forceinline__ void copy_region_fast(const uint4* __restrict__ s4, u
   }
 }
 
+// SoA rows and both arena regions of a block staged in LDS whose row table
+// (rec / kpre / vpre, <= kFastRows rows) is built.
+template <int V>
+__device__ __forceinline__ void emit_fast(const CopyParams& P, CopySmem& sm, uint32_t bias,
+                                          int rows, uint64_t kbytes, uint64_t vbytes,
+                                          uint64_t row0, uint64_t kb0, uint64_t vb0) {
+  const uint32_t tid = threadIdx.x;
+  FastRows& t = sm.f;
+  for (int i = tid; i < rows; i += kThreads) {
+    const uint64_t g = row0 + i;
+    P.key_off[g] = kb0 + t.kpre[i];
+    P.key_len[g] = uint16_t(t.kpre[i + 1] - t.kpre[i]);
+    P.val_off[g] = vb0 + t.vpre[i];
+    P.val_len[g] = t.vpre[i + 1] - t.vpre[i];
+  }
+  if (V < 3) return;
+  const uint32_t Gk = group_size(kbytes / rows), Gv = group_size(vbytes / rows);
+  copy_region_fast<false, V>(sm.stage, bias, P.key_arena, kb0, t, rows, Gk);
+  copy_region_fast<true, V>(sm.stage, bias, P.val_arena, vb0, t, rows, Gv);
+}
+
 template <int V>
 __device__ __forceinline__ void materialise_fast(const CopyParams& P, CopySmem& sm,
                                                 uint32_t bias, int rows, uint64_t kbytes,
@@ -1455,17 +1487,7 @@ __device__ __forceinline__ void materialise_fast(const CopyParams& P, CopySmem& 
   }
   __syncthreads();
   if (V < 2) return;  // diagnostic ablation (okv_copy_kernel<V>)
-  for (int i = tid; i < rows; i += kThreads) {
-    const uint64_t g = row0 + i;
-    P.key_off[g] = kb0 + t.kpre[i];
-    P.key_len[g] = uint16_t(t.kpre[i + 1] - t.kpre[i]);
-    P.val_off[g] = vb0 + t.vpre[i];
-    P.val_len[g] = t.vpre[i + 1] - t.vpre[i];
-  }
-  if (V < 3) return;
-  const uint32_t Gk = group_size(kbytes / rows), Gv = group_size(vbytes / rows);
-  copy_region_fast<false, V>(sm.stage, bias, P.key_arena, kb0, t, rows, Gk);
-  copy_region_fast<true, V>(sm.stage, bias, P.val_arena, vb0, t, rows, Gv);
+  emit_fast<V>(P, sm, bias, rows, kbytes, vbytes, row0, kb0, vb0);
 }
 
 __global__ __launch_bounds__(kThreads) void okv_copy_kernel(CopyParams P) {
@@ -1497,6 +1519,99 @@ __global__ __launch_bounds__(kThreads) void okv_copy_kernel(CopyParams P) {
       materialise<3>(src, P, sm, c.rows, c.kbytes, c.vbytes, B.row0, B.kb0, B.vb0, c.pend);
     }
     __syncthreads();  // LDS is reused by the next big block
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Point reads: a host-mode call of a few small uncompressed blocks (GetRow's
+// one block, GetRange's few; segment_reader.go:362-404, :410-475).  One
+// workgroup decodes the batch block after block, reading the staged bytes
+// straight from the context's pinned slab and writing every output into it,
+// so the call is one launch and one synchronisation (no H2D / D2H copies,
+// no plan, no totals read-back).  Per block: the block's
+// bytes into LDS (one trip over PCIe), the header walk in LDS by lane 0 with
+// okv_count_kernel's checks in Go's order (:338-352), recording the row table
+// as it goes, then the SoA rows and both arena regions from LDS (emit_fast;
+// blocks of more than kFastRows rows re-walk in batches, materialise).  The
+// host admits only batches whose OK blocks stage (BlockSize <= kStage).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Totals* tot) {
+  __shared__ CopySmem sm;
+  __shared__ uint64_t s_walk[4];  // rows, key bytes, value bytes, walk end
+  __shared__ int32_t s_st;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t* sw = reinterpret_cast<const uint32_t*>(sm.stage);
+  uint64_t row0 = 0, kb0 = 0, vb0 = 0, bad = 0;  // exclusive prefixes (uniform)
+  for (uint32_t b = 0; b < P.nblk; ++b) {
+    const Desc d = P.descs[b];
+    const int32_t st0 = go_read_status(d, P.seg_bytes);  // :303-316
+    const uint64_t len = P.comp == OKV_COMP_LZ4 ? 0 : d.block_size;  // Q7 (:331-333)
+    const uint32_t shift = uint32_t(d.offset & 15);
+    if (st0 == OKV_BLK_OK && len) {  // stage [offset - shift, offset + len): one trip
+      const uint32_t nch = uint32_t((shift + len + 15) >> 4);
+      const uint4* g = reinterpret_cast<const uint4*>(P.seg + (d.offset - shift));
+      for (uint32_t ci = tid; ci < nch; ci += kThreads) sm.stage[1 + ci] = g[ci];
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int32_t st = st0;
+      uint64_t rows = 0, kb = 0, vb = 0, p = 0;
+      if (st == OKV_BLK_OK) {
+        const uint64_t orig = go_walk_bound(d.original_size);  // int(OriginalSize) (:340)
+        const uint32_t bias = 16u + shift;
+        while (p < orig) {                                    // :340
+          if (len - p < 6) { st = OKV_BLK_PANIC; break; }     // u16/u32 reads (:342-345)
+          uint32_t kl, vl;
+          header_lds(sw, bias + uint32_t(p), kl, vl);
+          const uint64_t room = len - p - 6;
+          if (kl > room || vl > room - kl) { st = OKV_BLK_PANIC; break; }  // :346-349
+          if (rows < uint64_t(kFastRows)) {
+            sm.f.rec[rows] = uint32_t(p);
+            sm.f.kpre[rows] = uint32_t(kb);
+            sm.f.vpre[rows] = uint32_t(vb);
+          }
+          rows++;
+          kb += kl;
+          vb += vl;
+          p += 6 + uint64_t(kl) + uint64_t(vl);
+        }
+        if (st == OKV_BLK_OK && rows <= uint64_t(kFastRows)) {
+          sm.f.rec[rows] = uint32_t(p);
+          sm.f.kpre[rows] = uint32_t(kb);
+          sm.f.vpre[rows] = uint32_t(vb);
+        }
+      }
+      if (st != OKV_BLK_OK) rows = kb = vb = p = 0;  // a failed block has no rows
+      s_walk[0] = rows;
+      s_walk[1] = kb;
+      s_walk[2] = vb;
+      s_walk[3] = p;
+      s_st = st;
+      P.row_start[b] = row0;
+      P.key_base[b] = kb0;
+      P.val_base[b] = vb0;
+      P.blk_status[b] = st;
+    }
+    __syncthreads();
+    const uint64_t rows = s_walk[0], kb = s_walk[1], vb = s_walk[2], pend = s_walk[3];
+    const int32_t st = s_st;
+    if (st == OKV_BLK_OK && rows) {
+      if (rows <= uint64_t(kFastRows)) {
+        emit_fast<3>(P, sm, 16u + shift, int(rows), kb, vb, row0, kb0, vb0);
+      } else {
+        LdsSrc src{sw, 16u + shift};
+        materialise<3>(src, P, sm, rows, kb, vb, row0, kb0, vb0, pend);
+      }
+    }
+    row0 += rows;
+    kb0 += round16(kb);
+    vb0 += round16(vb);
+    bad += st != OKV_BLK_OK;
+    __syncthreads();  // the stage and the row table are reused by the next block
+  }
+  if (tid == 0) {
+    P.row_start[P.nblk] = row0;
+    *tot = Totals{row0, kb0, vb0, bad};
   }
 }
 
@@ -1825,7 +1940,8 @@ const TileForm kTileForms[] = {OKV_TILE_FORM(16, 256, 0), OKV_TILE_FORM(8, 256, 
                                OKV_TILE_FORM(16, 256, 5), OKV_TILE_FORM(16, 256, 6),
                                OKV_TILE_FORM(16, 256, 7), OKV_TILE_FORM(16, 256, 8),
                                OKV_TILE_FORM(8, 256, 8), OKV_TILE_FORM(32, 512, 8),
-                               OKV_TILE_FORM(16, 256, 9)};
+                               OKV_TILE_FORM(16, 256, 9), OKV_TILE_FORM(64, 1024, 0),
+                               OKV_TILE_FORM(64, 512, 0)};
 const TileForm* tile_form(uint32_t kib, uint32_t threads, uint32_t diag) {
   for (const TileForm& f : kTileForms)
     if (f.kib == kib && f.threads == threads && f.diag == diag) return &f;
@@ -2165,11 +2281,122 @@ bool output_bounds(const uint8_t* /*seg*/, uint64_t seg_bytes, const okv_block_d
   return true;
 }
 
+// ---- point reads (okv_point_kernel) -----------------------------------------
+// A host-mode call goes through the point path when it is a few uncompressed
+// (or LZ4-flagged) blocks whose readable blocks each fit the LDS stage: the
+// shim's GetRow reads one block, GetRange the few its btree walks select.
+constexpr uint32_t kPointMaxBlocks = 16;
+constexpr uint64_t kPointMaxBytes = uint64_t(1) << 20;
+
+bool point_eligible(uint64_t seg_bytes, const okv_block_desc* descs, uint32_t nblk, int comp,
+                    uint32_t flags) {
+  if (comp == OKV_COMP_ZSTD || (flags & OKV_F_INDEX_ONLY) || nblk == 0 ||
+      nblk > kPointMaxBlocks || seg_bytes > kPointMaxBytes)
+    return false;
+  for (uint32_t b = 0; b < nblk; ++b) {
+    const Desc& d = reinterpret_cast<const Desc*>(descs)[b];
+    if (comp != OKV_COMP_LZ4 && go_read_status(d, seg_bytes) == OKV_BLK_OK &&
+        d.block_size > uint64_t(kStage))
+      return false;
+  }
+  return true;
+}
+
+int grow_host(okv_ctx* ctx, uint8_t** p, size_t* cap, size_t need) {
+  if (need <= *cap && *p) return OKV_OK;
+  if (*p) {
+    OKV_HIP(hipStreamSynchronize(ctx->stream));
+    OKV_HIP(hipHostFree(*p));
+    *p = nullptr;
+    *cap = 0;
+  }
+  const size_t c = (std::max<size_t>(need, size_t(1) << 20) + 4095) & ~size_t(4095);
+  OKV_HIP(hipHostMalloc(reinterpret_cast<void**>(p), c, hipHostMallocDefault));
+  *cap = c;
+  return OKV_OK;
+}
+
+// One launch, one synchronisation: the blocks and descriptors are copied into
+// the pinned slab, the kernel reads them there and writes every output there
+// (both over PCIe), and the outputs are copied into the caller's arrays.
+int decode_point(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv_block_desc* descs,
+                 uint32_t nblk, int comp, okv_decode_out* o) {
+  // output bounds from the descriptors: a readable block's records lie in its
+  // BlockSize bytes (>= 6 bytes each); each arena region pads to 16 bytes
+  uint64_t R = 0, A = 0;
+  for (uint32_t b = 0; b < nblk; ++b) {
+    const Desc& d = reinterpret_cast<const Desc*>(descs)[b];
+    if (comp == OKV_COMP_LZ4 || go_read_status(d, seg_bytes) != OKV_BLK_OK) continue;
+    R += d.block_size / 6;
+    A += round16(d.block_size);
+  }
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t n1 = size_t(nblk) + 1;
+  const size_t o_desc = al(seg_bytes + 64), o_rs = al(o_desc + nblk * sizeof(Desc)),
+               o_kb = al(o_rs + n1 * 8), o_vb = al(o_kb + n1 * 8), o_st = al(o_vb + n1 * 8),
+               o_tot = al(o_st + n1 * 4), o_ko = al(o_tot + sizeof(Totals)),
+               o_kl = al(o_ko + R * 8), o_vo = al(o_kl + R * 2), o_vl = al(o_vo + R * 8),
+               o_ka = al(o_vl + R * 4), o_va = al(o_ka + A + 16), total = al(o_va + A + 16);
+  int rc = grow_host(ctx, &ctx->h_slab, &ctx->cap_slab, total);
+  if (rc) return rc;
+  uint8_t* S = ctx->h_slab;
+  if (seg_bytes) std::memcpy(S, seg, seg_bytes);
+  std::memcpy(S + o_desc, descs, nblk * sizeof(Desc));
+  CopyParams P;
+  std::memset(&P, 0, sizeof(P));
+  P.seg = S;
+  P.seg_bytes = seg_bytes;
+  P.descs = reinterpret_cast<const Desc*>(S + o_desc);
+  P.nblk = nblk;
+  P.comp = comp;
+  P.row_start = reinterpret_cast<uint64_t*>(S + o_rs);
+  P.key_base = reinterpret_cast<uint64_t*>(S + o_kb);
+  P.val_base = reinterpret_cast<uint64_t*>(S + o_vb);
+  P.blk_status = reinterpret_cast<int32_t*>(S + o_st);
+  P.key_off = reinterpret_cast<uint64_t*>(S + o_ko);
+  P.key_len = reinterpret_cast<uint16_t*>(S + o_kl);
+  P.val_off = reinterpret_cast<uint64_t*>(S + o_vo);
+  P.val_len = reinterpret_cast<uint32_t*>(S + o_vl);
+  P.key_arena = S + o_ka;
+  P.val_arena = S + o_va;
+  P.row_cap = R;
+  P.key_cap = A + 16;
+  P.val_cap = A + 16;
+  Totals* tot = reinterpret_cast<Totals*>(S + o_tot);
+  ctx->last_path = OKV_PATH_POINT;
+  hipLaunchKernelGGL(okv_point_kernel, dim3(1), dim3(kThreads), 0, ctx->stream, P, tot);
+  OKV_HIP(hipGetLastError());
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  const Totals T = *tot;
+  o->n_rows = T.rows;
+  o->key_bytes = T.kb;
+  o->val_bytes = T.vb;
+  o->n_bad_blocks = T.bad;
+  if (T.rows > o->row_cap || T.kb > o->key_cap || T.vb > o->val_cap)
+    return set_err(ctx, OKV_E_CAPACITY, "output capacity too small (totals set)");
+  auto out = [](void* dst, const void* src, size_t n) {
+    if (dst && n) std::memcpy(dst, src, n);
+  };
+  out(o->row_start, P.row_start, n1 * 8);
+  out(o->blk_status, P.blk_status, size_t(nblk) * 4);
+  out(o->key_base, P.key_base, size_t(nblk) * 8);
+  out(o->val_base, P.val_base, size_t(nblk) * 8);
+  out(o->key_off, P.key_off, T.rows * 8);
+  out(o->key_len, P.key_len, T.rows * 2);
+  out(o->val_off, P.val_off, T.rows * 8);
+  out(o->val_len, P.val_len, T.rows * 4);
+  out(o->key_arena, P.key_arena, T.kb);
+  out(o->val_arena, P.val_arena, T.vb);
+  return OKV_OK;
+}
+
 // Host pointers: stage inputs to device scratch, decode, copy results back.
 // The device outputs are sized from the host descriptors' bounds when those
 // exist (one pass-1 walk per call); otherwise from a pass-1 plan first.
 int decode_host(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv_block_desc* descs,
                 uint32_t nblk, int comp, okv_decode_out* o, uint32_t flags) {
+  if (ctx->point && point_eligible(seg_bytes, descs, nblk, comp, flags))
+    return decode_point(ctx, seg, seg_bytes, descs, nblk, comp, o);
   const bool index_only = flags & OKV_F_INDEX_ONLY;
   int rc = grow(ctx, reinterpret_cast<void**>(&ctx->d_seg), &ctx->cap_seg, seg_bytes + 64);
   if (rc) return rc;
@@ -2282,6 +2509,7 @@ okv_ctx* okv_open_ex(int device, void* stream, const okv_open_opts* opts) {
   if (ctx && opts) {
     if (opts->flags & OKV_OPEN_NO_FUSED) ctx->fused = false;
     ctx->zstd_one_pass = (opts->flags & OKV_OPEN_ZSTD_ONE_PASS) != 0;
+    ctx->point = (opts->flags & OKV_OPEN_NO_POINT) == 0;
   }
   return ctx;
 }
@@ -2395,6 +2623,7 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->d_desc);
   (void)hipFree(ctx->d_out);
   (void)hipFree(ctx->d_hash);
+  if (ctx->h_slab) (void)hipHostFree(ctx->h_slab);
   (void)hipFree(ctx->d_vsrc);
   (void)hipFree(ctx->d_hdr);
   (void)hipFree(ctx->d_vtile);

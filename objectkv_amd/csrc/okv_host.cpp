@@ -248,6 +248,9 @@ struct okv_meta {
   uint64_t fk_off = 0, fk_len = 0, lk_off = 0, lk_len = 0;
   bool has_bloom = false;
   uint64_t bloom_off = 0, bloom_len = 0;
+  // the filter BloomFilter.ReadFrom decoded (parseBloomFilterBlock :197-198)
+  uint64_t bloom_m = 0, bloom_k = 0, bloom_length = 0;
+  std::vector<uint64_t> bloom_words;
   int compression = 0;
   std::vector<okv_block_desc> descs;  // file order
   std::vector<uint64_t> hashes, key_off, key_len;
@@ -269,6 +272,76 @@ struct MetaReader {  // bytes.Reader + mustReadBytes (:489-512)
   }
 };
 
+// ---- the bloom filter (parseBloomFilterBlock :183-201, probeBloomFilter
+// :245-258), restated from the published algorithms of the pinned versions
+// (go.sum): github.com/bits-and-blooms/bloom v2.0.3, github.com/spaolacci/
+// murmur3 v1.1.0, github.com/willf/bitset v1.1.11.  Filter bytes are
+// PARITY-UNPINNED (no reference test asserts them; oracle/bloom_ref.py is the
+// independent restatement the tests compare against).
+
+// murmur3.Sum128 (MurmurHash3_x64_128, seed 0) -> (h1, h2)
+void murmur3_128(const uint8_t* p, size_t n, uint64_t* o1, uint64_t* o2) {
+  const uint64_t c1 = 0x87C37B91114253D5ULL, c2 = 0x4CF5AD432745937FULL;
+  uint64_t h1 = 0, h2 = 0;
+  const size_t nb = n / 16;
+  for (size_t i = 0; i < nb; ++i) {
+    uint64_t k1 = rd64(p + 16 * i), k2 = rd64(p + 16 * i + 8);
+    k1 *= c1; k1 = rotl(k1, 31); k1 *= c2; h1 ^= k1;
+    h1 = rotl(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52DCE729;
+    k2 *= c2; k2 = rotl(k2, 33); k2 *= c1; h2 ^= k2;
+    h2 = rotl(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495AB5;
+  }
+  const uint8_t* t = p + 16 * nb;
+  const size_t tl = n & 15;
+  uint64_t k1 = 0, k2 = 0;
+  for (size_t i = tl; i > 8; --i) k2 = (k2 << 8) | t[i - 1];
+  if (tl > 8) { k2 *= c2; k2 = rotl(k2, 33); k2 *= c1; h2 ^= k2; }
+  for (size_t i = tl < 8 ? tl : 8; i > 0; --i) k1 = (k1 << 8) | t[i - 1];
+  if (tl) { k1 *= c1; k1 = rotl(k1, 31); k1 *= c2; h1 ^= k1; }
+  h1 ^= uint64_t(n);
+  h2 ^= uint64_t(n);
+  h1 += h2;
+  h2 += h1;
+  auto fmix = [](uint64_t k) {
+    k ^= k >> 33; k *= 0xFF51AFD7ED558CCDULL; k ^= k >> 33; k *= 0xC4CEB9FE1A85EC53ULL;
+    return k ^ (k >> 33);
+  };
+  h1 = fmix(h1);
+  h2 = fmix(h2);
+  h1 += h2;
+  h2 += h1;
+  *o1 = h1;
+  *o2 = h2;
+}
+
+inline uint64_t rdbe64(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int i = 0; i < 8; ++i) v = (v << 8) | p[i];
+  return v;
+}
+
+// BloomFilter.ReadFrom (bloom v2.0.3): binary.Read(BigEndian) of m and k, then
+// bitset.ReadFrom (v1.1.11): u64 length, New(length) -- wordsNeeded(length)
+// words, or length 0 when that allocation panics (recovered: "type mismatch")
+// -- and binary.Read of the words.  Any short read is an error (io.EOF /
+// io.ErrUnexpectedEOF); trailing bytes are not read.
+bool bloom_read_from(okv_meta* m) {
+  const uint8_t* b = m->bytes.data() + m->bloom_off;
+  const uint64_t n = m->bloom_len;
+  if (n < 24) return false;  // m, k, length
+  m->bloom_m = rdbe64(b);
+  m->bloom_k = rdbe64(b + 8);
+  m->bloom_length = rdbe64(b + 16);
+  const uint64_t cap = ~uint64_t(0);
+  const uint64_t words = m->bloom_length > cap - 64 + 1 ? cap >> 6 : (m->bloom_length + 63) >> 6;
+  // words beyond the bytes present: binary.Read fails (or make panicked first,
+  // which New recovers into a length mismatch: an error either way)
+  if (words > (n - 24) / 8) return false;
+  m->bloom_words.resize(size_t(words));
+  for (uint64_t i = 0; i < words; ++i) m->bloom_words[size_t(i)] = rdbe64(b + 24 + 8 * i);
+  return true;
+}
+
 int parse_meta(okv_meta* m) {  // BytesToMetadata :147-181
   MetaReader r{m->bytes.data(), m->bytes.size()};
   const uint8_t* b = m->bytes.data();
@@ -285,6 +358,7 @@ int parse_meta(okv_meta* m) {  // BytesToMetadata :147-181
     if (!r.must(8, &at)) return OKV_M_PANIC;
     m->bloom_len = rd64(b + at);
     if (!r.must(m->bloom_len, &m->bloom_off)) return OKV_M_PANIC;
+    if (!bloom_read_from(m)) return OKV_M_BLOOM;  // "error in parseBloomFilterBlock" (:160-163)
   }
   if (!r.must(1, &at)) return OKV_M_PANIC;  // :166-172
   m->compression = b[at] == 1 ? OKV_COMP_ZSTD : (b[at] == 2 ? OKV_COMP_LZ4 : OKV_COMP_NONE);
@@ -370,6 +444,30 @@ int okv_meta_block(const okv_meta* m, uint64_t i, okv_block_desc* desc, uint64_t
   return OKV_OK;
 }
 void okv_meta_free(okv_meta* m) { delete m; }
+
+int okv_meta_has_bloom(const okv_meta* m) { return m && m->has_bloom ? 1 : 0; }
+
+// BloomFilter.Test (bloom v2.0.3): baseHashes = murmur3 Sum128 of key, then of
+// key ++ [1] (the hasher keeps its state); bit i of k is
+// (h[i % 2] + i * h[2 + ((i + i % 2) % 4) / 2]) % m, tested by bitset.Test (a
+// position >= the bitset's length reads false).  m == 0 is Go's integer
+// division panic.
+int okv_meta_bloom_test(const okv_meta* m, const uint8_t* key, size_t klen) {
+  if (!m || !m->has_bloom) return 1;  // probeBloomFilter: no filter, no probe
+  if (m->bloom_k == 0) return 1;
+  if (m->bloom_m == 0) return OKV_R_PANIC;
+  uint64_t h[4];
+  murmur3_128(key, klen, &h[0], &h[1]);
+  std::vector<uint8_t> k1(key, key + klen);
+  k1.push_back(1);
+  murmur3_128(k1.data(), k1.size(), &h[2], &h[3]);
+  for (uint64_t i = 0; i < m->bloom_k; ++i) {
+    const uint64_t loc = (h[i % 2] + i * h[2 + ((i + (i % 2)) % 4) / 2]) % m->bloom_m;
+    if (loc >= m->bloom_length) return 0;
+    if (!((m->bloom_words[size_t(loc >> 6)] >> (loc & 63)) & 1)) return 0;
+  }
+  return 1;
+}
 
 // ---------------------------------------------------------------------------
 // Synthetic segments (BASELINE.md / SURVEY.md §8d)

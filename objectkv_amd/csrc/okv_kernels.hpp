@@ -51,7 +51,7 @@ struct SpanHint {  // okv_decode_plan's longest walk (host side)
   uint64_t span = 0;
 };
 
-__device__ __forceinline__ uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+__host__ __device__ inline uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
 // Go's int() conversions at the block boundary (segment_reader.go:303-340),
 // shared by every walk:
@@ -62,13 +62,13 @@ __device__ __forceinline__ uint64_t round16(uint64_t x) { return (x + 15) & ~uin
 // * `totalReadBytes < int(stat.OriginalSize)` (:340) has a negative bound
 //   from 2^63 on: the loop runs no iteration (nil rows, no error).
 constexpr uint64_t kGoMaxAlloc = uint64_t(1) << 48;
-__device__ __forceinline__ uint64_t go_walk_bound(uint64_t original_size) {
+__host__ __device__ inline uint64_t go_walk_bound(uint64_t original_size) {
   return int64_t(original_size) < 0 ? 0 : original_size;
 }
 // The raw-block outcome of :303-316 in Go's order: Seek(int64(Offset))
 // (negative -> error), make (panic), Read (io.EOF at / past the end, short).
 // OKV_BLK_OK when the block's BlockSize bytes are in the segment.
-__device__ __forceinline__ int32_t go_read_status(const Desc& d, uint64_t seg_bytes) {
+__host__ __device__ inline int32_t go_read_status(const Desc& d, uint64_t seg_bytes) {
   if (int64_t(d.offset) < 0) return OKV_BLK_EOF;                // Seek error
   if (d.block_size > kGoMaxAlloc) return OKV_BLK_PANIC;           // makeslice
   if (d.offset >= seg_bytes) return OKV_BLK_EOF;                  // io.EOF

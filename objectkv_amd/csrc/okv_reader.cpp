@@ -102,6 +102,7 @@ struct okv_reader {
   bool have_meta = false;
   int compression = 0;
   GoBytes first_key, last_key;
+  std::unique_ptr<okv_meta, void (*)(okv_meta*)> meta{nullptr, okv_meta_free};  // (its bloom filter)
   std::vector<Entry> file_entries;  // meta block order
   std::vector<Entry> tree;          // google/btree.BTreeG ordered by FirstKey (ReplaceOrInsert)
   // the iteration window: its batch and each file entry's slot in it (-1: absent)
@@ -174,7 +175,7 @@ int load_meta(okv_reader* r, okv_meta* m) {
     else
       r->tree.insert(r->tree.begin() + pos, e);
   }
-  okv_meta_free(m);
+  r->meta.reset(m);  // kept for GetRow's bloom probe
   r->have_meta = true;
   r->window.reset();
   r->window_slot.assign(r->file_entries.size(), -1);
@@ -396,8 +397,13 @@ int okv_reader_read_block(okv_reader* r, uint64_t i, const okv_row** rows, uint6
 int okv_reader_get_row(okv_reader* r, const uint8_t* key, size_t klen, okv_row* out) {
   int rc = ensure_meta(r);  // GetRow :362-404
   if (rc) return rc;
-  // bloom probe (:371-378): the filter has no false negatives, so skipping it
-  // changes no result (bits-and-blooms bytes are not restated).
+  // bloom probe (:371-378, probeBloomFilter :245-258) on the host: a key the
+  // filter rejects costs no block read and no GPU call
+  if (okv_meta_has_bloom(r->meta.get())) {
+    const int t = okv_meta_bloom_test(r->meta.get(), key, klen);
+    if (t < 0) return t;                 // Go's panic (a filter with m == 0)
+    if (t == 0) return OKV_R_NO_ROWS;    // "did not find row in bloom filter"
+  }
   const size_t up = upper(r, key, klen);  // DescendLessOrEqual first item (:381-385)
   if (up == 0) return OKV_R_NO_ROWS;
   const std::vector<okv_row>* rows = nullptr;

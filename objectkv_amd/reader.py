@@ -26,7 +26,7 @@ _KIND = {
     -203: "ErrMismatchedMetaBlockHash", -204: "ErrInvalidMetaBlock", -206: "ErrIO",
     -301: "ErrNoRows", -302: "EOF", -303: "ErrClosed", -304: "ErrAlreadyClosed",
     -305: "EOF", -306: "ErrUnexpectedBytesRead", -308: "ErrUnsupported", -309: "ErrGPU",
-    -310: "ErrZstd",
+    -310: "ErrZstd", -208: "ErrBloomReadFrom",
 }
 _PANIC = {-105, -205, -207, -307}
 FATAL = {"ErrInvalidMagicNumber", "ErrUnknownSegmentVersion", "ErrMismatchedMetaBlockHash",

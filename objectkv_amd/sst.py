@@ -233,7 +233,7 @@ class Decoder:
     """One okv_ctx bound to a GPU (HIP device ordinal)."""
 
     def __init__(self, device: int = 0, stream=None, flags: int = 0):
-        """flags: okv_open_opts.flags (OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS)."""
+        """flags: okv_open_opts.flags (OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS, OPEN_NO_POINT)."""
         L = lib()
         if flags:
             opts = _lib.OpenOpts(C.sizeof(_lib.OpenOpts), flags)

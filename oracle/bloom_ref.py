@@ -100,8 +100,10 @@ class BloomFilter:
 
     def _locations(self, data: bytes):
         h = self._base(data)
-        for i in range(self.k):
+        i = 0
+        while i < self.k:
             yield ((h[i % 2] + i * h[2 + ((i + (i % 2)) % 4) // 2]) & M64) % self.m
+            i += 1
 
     def add(self, data: bytes) -> "BloomFilter":
         for loc in self._locations(data):
@@ -109,7 +111,17 @@ class BloomFilter:
         return self
 
     def test(self, data: bytes) -> bool:
-        return all(self.words[loc >> 6] >> (loc & 63) & 1 for loc in self._locations(data))
+        """Test (bloom v2.0.3): k probes; bitset.Test reads positions >= the
+        bitset's length as false; m == 0 is Go's integer-division panic
+        (ZeroDivisionError here)."""
+        if self.k == 0:
+            return True
+        if self.m == 0:
+            raise ZeroDivisionError("integer divide by zero")
+        for loc in self._locations(data):
+            if loc >= self.length or not (self.words[loc >> 6] >> (loc & 63)) & 1:
+                return False
+        return True
 
     def to_bytes(self) -> bytes:
         """WriteTo: m, k, bitset length, words -- all big-endian uint64."""
@@ -117,10 +129,19 @@ class BloomFilter:
 
     @classmethod
     def from_bytes(cls, b: bytes) -> "BloomFilter":
+        """ReadFrom (bloom v2.0.3; bitset v1.1.11 ReadFrom): big-endian m, k,
+        bitset length, then wordsNeeded(length) words; any short read is an
+        error (ValueError), trailing bytes are not read."""
+        b = bytes(b or b"")
+        if len(b) < 24:
+            raise ValueError("bloom ReadFrom: unexpected EOF")
         m, k, length = struct.unpack_from(">QQQ", b)
-        f = cls(m, k)
-        f.length = length
-        f.words = list(struct.unpack_from(f">{len(f.words)}Q", b, 24))
+        words = (M64 >> 6) if length > M64 - 63 else (length + 63) >> 6
+        if words > (len(b) - 24) // 8:
+            raise ValueError("bloom ReadFrom: unexpected EOF / type mismatch")
+        f = cls.__new__(cls)
+        f.m, f.k, f.length = m, k, length
+        f.words = list(struct.unpack_from(f">{words}Q", b, 24))
         return f
 
 

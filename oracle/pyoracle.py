@@ -47,6 +47,7 @@ ErrInvalidMetaBlock = "ErrInvalidMetaBlock"  # :83
 ErrUnexpectedBytesRead = "ErrUnexpectedBytesRead"  # :477
 ErrAlreadyClosed = "ErrAlreadyClosed"  # :478
 ErrNoRows = "ErrNoRows"  # :357
+ErrBloomReadFrom = "ErrBloomReadFrom"  # BytesToMetadata: "error in parseBloomFilterBlock" (:160-163)
 ErrClosed = "ErrClosed"  # segment_row_iter.go:27
 EOF = "EOF"  # io.EOF
 ErrIO = "ErrIO"  # any other Seek/Read error
@@ -368,6 +369,11 @@ def bytes_to_metadata(meta: bytes) -> SegmentMetadata:
     if r.must(1)[0] == 1:  # :184
         blen = struct.unpack("<Q", r.must(8))[0]
         md.BloomFilter = r.must(blen)  # WriteTo bytes; GetRow probes them (bloom_ref)
+        from oracle.bloom_ref import BloomFilter
+        try:  # bloomFilter.ReadFrom (:197-200)
+            md._bloom = BloomFilter.from_bytes(md.BloomFilter)
+        except ValueError as e:
+            raise GoError(ErrBloomReadFrom, f"error in parseBloomFilterBlock: {e}")
     c = r.must(1)[0]
     md.ZSTDCompression = c == 1
     md.LZ4Compression = c == 2
@@ -503,8 +509,11 @@ class SegmentReader:
     def GetRow(self, key):  # :362-404
         md = self._md()
         if md.BloomFilter is not None:  # :371-378 (probeBloomFilter :245-258)
-            from oracle.bloom_ref import BloomFilter
-            if not BloomFilter.from_bytes(md.BloomFilter).test(_b(key)):
+            try:
+                maybe = md._bloom.test(_b(key))
+            except ZeroDivisionError:  # a filter with m == 0: Go's runtime panic
+                raise GoPanic("integer divide by zero")
+            if not maybe:
                 raise GoError(ErrNoRows, "did not find row in bloom filter")
         cand = md.BlockIndex.descend_le(key)
         if not cand:

@@ -293,34 +293,55 @@ def _mixed_segment(kinds, seed):
 
 @pytest.fixture(scope="module")
 def nofused_decoder():
-    """A context opened with OKV_OPEN_NO_FUSED: small batches of small blocks
-    take the three-launch path (count, scan, okv_gather_small_kernel)."""
-    dec = okv.Decoder(0, flags=_lib.OPEN_NO_FUSED)
+    """A context opened with OKV_OPEN_NO_FUSED (and NO_POINT): small batches
+    of small blocks take the three-launch path (count, scan,
+    okv_gather_small_kernel)."""
+    dec = okv.Decoder(0, flags=_lib.OPEN_NO_FUSED | _lib.OPEN_NO_POINT)
     yield dec
     dec.close()
 
 
-# The shipping decode paths.  Which kernels run follows from the call: the
-# average block span (segment bytes / blocks) picks the small-block kernels
-# (<= 16 KiB) or the large-block tile pass; <= 512 small blocks run the
-# single-pass fused kernel unless the context was opened with NO_FUSED; big
-# blocks (> 64 rows, or past the tile span) go to okv_copy_kernel on either.
-PATHS = ["as_given", "nofused", "large"]
+@pytest.fixture(scope="module")
+def nopoint_decoder():
+    """A context opened with OKV_OPEN_NO_POINT: host-mode calls of a few small
+    blocks are staged to device memory (the fused / tile kernels) instead of
+    taking the point path."""
+    dec = okv.Decoder(0, flags=_lib.OPEN_NO_POINT)
+    yield dec
+    dec.close()
 
 
-def decode_path(path, decoder, nofused, seg, d, **kw):
+# The shipping decode paths.  Which kernels run follows from the call: a
+# host-mode call of <= 16 small uncompressed blocks takes the point path
+# (okv_point_kernel) unless the context was opened with NO_POINT; otherwise
+# the average block span (segment bytes / blocks) picks the small-block
+# kernels (<= 16 KiB) or the large-block tile pass; <= 512 small blocks run
+# the single-pass fused kernel unless the context was opened with NO_FUSED;
+# big blocks (> 64 rows, or past the tile span) go to okv_copy_kernel on either.
+PATHS = ["as_given", "fused", "nofused", "large"]
+
+
+def decode_path(path, decoder, nofused, seg, d, nopoint=None, **kw):
     """Decode (seg, d) through one shipping path; returns (decoded, seg used).
-    "large": the segment buffer padded with zeros so the blocks average more
-    than 16 KiB (a caller decoding some blocks of a larger segment) -- every
-    block goes through the large-block pass."""
+    "as_given": the default context (the point path when the call is
+    eligible); "fused": a NO_POINT context; "large": the segment buffer
+    padded with zeros so the blocks average more than 16 KiB (a caller
+    decoding some blocks of a larger segment), NO_POINT -- every block goes
+    through the large-block pass."""
     seg = bytes(seg)
     if path == "large":
         n = max(1, d.shape[0])
         seg = seg + bytes(max(0, 16385 * n - len(seg)) + 4096)
-    dec = nofused if path == "nofused" else decoder
+    if path in ("fused", "large"):
+        assert nopoint is not None
+        dec = nopoint
+    else:
+        dec = nofused if path == "nofused" else decoder
     got = dec.decode(seg, d, **kw)
     lp = dec.last_path()
     if d.shape[0]:
+        if path != "as_given":
+            assert not lp & _lib.PATH_POINT, lp
         if path == "nofused":
             assert not lp & _lib.PATH_FUSED, lp
         if path == "large":
@@ -364,30 +385,30 @@ def _wide_segment(seed, nblk=120):
 
 
 @pytest.mark.parametrize("path", PATHS)
-def test_wide_spans_all_paths(decoder, nofused_decoder, path):
+def test_wide_spans_all_paths(decoder, nofused_decoder, nopoint_decoder, path):
     """Long keys with tiny values (a value tile spans many records), stage
     overflow, the segment's first and last bytes, odd block offsets: every
     shipping path vs the oracle."""
     for seed in (1, 2):
         seg, d = _wide_segment(seed)
-        got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d)
+        got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d, nopoint=nopoint_decoder)
         _assert_same_as_oracle(got, seg2, d, 0, False)
 
 
 @pytest.mark.parametrize("path", PATHS)
-def test_mixed_blocks_all_paths(decoder, nofused_decoder, path):
+def test_mixed_blocks_all_paths(decoder, nofused_decoder, nopoint_decoder, path):
     """A segment mixing 4 KiB blocks, 64 KiB blocks with few rows and blocks
     over kRCap rows, full and index-only, through every shipping path."""
     rng = np.random.default_rng(11)
     kinds = list(rng.choice(["s", "s", "L", "M"], size=300))
     seg, d = _mixed_segment(kinds, 5)
     for index_only in (False, True):
-        got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d, index_only=index_only)
+        got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d, index_only=index_only, nopoint=nopoint_decoder)
         _assert_same_as_oracle(got, seg2, d, 0, index_only)
 
 
 @pytest.mark.parametrize("nblk", [255, 256, 257, 513])
-def test_single_tile_and_scan_paths(decoder, nofused_decoder, nblk):
+def test_single_tile_and_scan_paths(decoder, nofused_decoder, nopoint_decoder, nblk):
     """<= 256 blocks: pass 1 writes the totals itself (one tile, no scan
     launch, in-kernel big-block counter reset); more: okv_scan_kernel.  Both
     with a block over kRCap rows, through every shipping path, against the
@@ -398,7 +419,7 @@ def test_single_tile_and_scan_paths(decoder, nofused_decoder, nblk):
     seg, d = _mixed_segment(kinds, nblk)
     outs = []
     for path in PATHS:
-        got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d)
+        got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d, nopoint=nopoint_decoder)
         _assert_same_as_oracle(got, seg2, d, 0, False)
         outs.append(got)
     for got in outs[1:]:
@@ -427,7 +448,7 @@ def _tiny_value_segment(seed, nblk=300):
 
 
 @pytest.mark.parametrize("path", PATHS)
-def test_tiny_values_fuzz_and_capacity(decoder, nofused_decoder, path):
+def test_tiny_values_fuzz_and_capacity(decoder, nofused_decoder, nopoint_decoder, path):
     """C3 blocks; tiny values (thousands of rows per 4 KiB of values, many
     rows per destination chunk); a fuzz of corrupt / truncated blocks
     (statuses with other blocks' rows around them) -- every shipping path vs
@@ -435,11 +456,11 @@ def test_tiny_values_fuzz_and_capacity(decoder, nofused_decoder, path):
     it report OKV_BLK_CAPACITY, the blocks before it match the oracle."""
     w = okv.synth_segment(okv.sst.SYNTH_ZIPF, 7, nblocks=96, threshold=57344, block_size=65536)
     seg, d = w.data(), w.descs()
-    got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d)
+    got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d, nopoint=nopoint_decoder)
     _assert_same_as_oracle(got, seg2, d, 0, False)
     for seed in (3, 4):
         seg, d = _tiny_value_segment(seed)
-        got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d)
+        got, seg2 = decode_path(path, decoder, nofused_decoder, seg, d, nopoint=nopoint_decoder)
         _assert_same_as_oracle(got, seg2, d, 0, False)
     rng = np.random.default_rng(77)
     for trial in range(12):
@@ -463,7 +484,7 @@ def test_tiny_values_fuzz_and_capacity(decoder, nofused_decoder, path):
             seg += body + bytes(bsize - len(body))
             descs.append((off, bsize, orig, 0))
         d = np.array(descs, np.uint64).reshape(-1, 4)
-        got, seg2 = decode_path(path, decoder, nofused_decoder, bytes(seg), d)
+        got, seg2 = decode_path(path, decoder, nofused_decoder, bytes(seg), d, nopoint=nopoint_decoder)
         _assert_same_as_oracle(got, seg2, d, 0, False)
     # device path with an undersized value arena
     import torch

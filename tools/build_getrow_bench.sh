@@ -1,0 +1,5 @@
+#!/bin/bash
+# Builds tools/getrow_bench against the in-tree product library (run from the repo root).
+set -e
+/opt/rocm/bin/hipcc -O2 -std=c++17 -Iinclude tools/getrow_bench.cpp -o tools/getrow_bench \
+  -Lobjectkv_amd -lokv_sst -Wl,-rpath,'$ORIGIN/../objectkv_amd' -ldl

@@ -1,0 +1,133 @@
+// getrow_bench.cpp -- C++-level GetRow latency through the product reader
+// (okv_reader_get_row: btree floor, one host-mode decode of the block --
+// the point path, okv_point_kernel -- row lookup), timed without Python.
+// Beside it: the CPU restatement's decode of the same one block
+// (oref_read_block from oracle/build/liboref.so, Go allocation semantics:
+// a measurement baseline, dlopen'ed by this tool only) and the bloom-negative
+// GetRow (host probe, no GPU call).
+//
+// build: tools/build_getrow_bench.sh   run: tools/getrow_bench [calls]
+// prints one JSON line per block size.
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "okv_host.h"
+#include "okv_sst.h"
+
+namespace {
+
+typedef struct {
+  uint8_t* key;
+  uint64_t key_len;
+  uint8_t* val;
+  uint64_t val_len;
+} oref_kv;
+typedef struct {
+  oref_kv* rows;
+  uint64_t n, cap;
+} oref_rows;
+typedef int (*read_block_fn)(const uint8_t*, uint64_t, const okv_block_desc*, int, oref_rows*);
+typedef void (*rows_free_fn)(oref_rows*);
+
+double now_us() {
+  return std::chrono::duration<double, std::micro>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+double pct(std::vector<double> v, double p) {
+  std::sort(v.begin(), v.end());
+  return v[std::min(v.size() - 1, size_t(p * double(v.size())))];
+}
+
+void key_of(uint64_t i, uint8_t* k) {  // OKV_SYNTH_FIXED: 8 zero bytes + big-endian index
+  std::memset(k, 0, 8);
+  for (int b = 0; b < 8; ++b) k[8 + b] = uint8_t(i >> (56 - 8 * b));
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const int calls = argc > 1 ? std::atoi(argv[1]) : 2000;
+  okv_ctx* ctx = okv_open(0);
+  if (!ctx) {
+    std::fprintf(stderr, "okv_open failed\n");
+    return 1;
+  }
+  void* oref = dlopen("oracle/build/liboref.so", RTLD_NOW);
+  read_block_fn oref_read = oref ? (read_block_fn)dlsym(oref, "oref_read_block") : nullptr;
+  rows_free_fn oref_free = oref ? (rows_free_fn)dlsym(oref, "oref_rows_free") : nullptr;
+  struct Cfg {
+    const char* name;
+    uint64_t rows, threshold, block;
+  } cfgs[] = {{"4KiB_blocks", 100000, 3584, 4096}, {"64KiB_blocks", 400000, 57344, 65536}};
+  for (const Cfg& c : cfgs) {
+    okv_writer* w = okv_synth_segment(OKV_SYNTH_FIXED, 3, c.rows, 0, c.threshold, c.block);
+    uint64_t dlen = 0;  // (a closed writer)
+    const uint8_t* data = okv_writer_data(w, &dlen);
+    okv_reader* r = okv_reader_open(ctx, data, dlen, int64_t(dlen));
+    if (okv_reader_fetch_metadata(r)) {
+      std::fprintf(stderr, "metadata\n");
+      return 1;
+    }
+    std::mt19937_64 rng(7);
+    uint8_t key[16];
+    okv_row row;
+    for (int i = 0; i < 50; ++i) {  // warm (slab allocation, code objects)
+      key_of(rng() % c.rows, key);
+      okv_reader_get_row(r, key, 16, &row);
+    }
+    std::vector<double> t;
+    okv_reader_io io0, io1;
+    okv_reader_io_stats(r, &io0);
+    for (int i = 0; i < calls; ++i) {
+      const uint64_t idx = rng() % c.rows;
+      key_of(idx, key);
+      const double t0 = now_us();
+      const int rc = okv_reader_get_row(r, key, 16, &row);
+      t.push_back(now_us() - t0);
+      if (rc || row.key_len != 16 || std::memcmp(row.key, key, 16) != 0) {
+        std::fprintf(stderr, "GetRow(%llu) rc %d\n", (unsigned long long)idx, rc);
+        return 1;
+      }
+    }
+    okv_reader_io_stats(r, &io1);
+    // the CPU restatement's one-block decode of the same blocks
+    std::vector<double> tc;
+    const uint64_t nb = okv_writer_num_blocks(w);
+    if (oref_read) {
+      for (int i = 0; i < calls; ++i) {
+        okv_block_desc d;
+        uint64_t h, fl;
+        const uint8_t* fk;
+        okv_writer_block(w, rng() % nb, &d, &h, &fk, &fl);
+        oref_rows rows{nullptr, 0, 0};
+        const double t0 = now_us();
+        oref_read(data, dlen, &d, 0, &rows);
+        tc.push_back(now_us() - t0);
+        oref_free(&rows);
+      }
+    }
+    std::printf(
+        "{\"config\": \"%s\", \"calls\": %d, \"gpu_calls\": %llu, \"blocks\": %llu, "
+        "\"getrow_us\": {\"median\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"min\": %.1f}, "
+        "\"cpu_restatement_one_block_us\": {\"median\": %.2f, \"p90\": %.2f}, "
+        "\"path\": %u}\n",
+        c.name, calls, (unsigned long long)(io1.calls - io0.calls),
+        (unsigned long long)nb, pct(t, 0.5), pct(t, 0.9), pct(t, 0.99), pct(t, 0.0),
+        tc.empty() ? -1.0 : pct(tc, 0.5), tc.empty() ? -1.0 : pct(tc, 0.9), okv_last_path(ctx));
+    std::fflush(stdout);
+    okv_reader_free(r);
+    okv_writer_free(w);
+  }
+  okv_close(ctx);
+  return 0;
+}

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 5: point path + bloom tests, C++ GetRow latency, then the count-arrival
+# A/B and the 64 KiB tile forms (tools/gpu_r5a.sh).
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r5b; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_point_gpu.py tests/test_reader_gpu.py tests/test_decode_gpu.py -m gpu > $O/tests.log 2>&1
+rc=$?; tail -3 $O/tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 120 tools/getrow_bench 2000 > $O/getrow.log 2>&1
+rc=$?; cat $O/getrow.log; [ $rc -ne 0 ] && exit $rc
+bash tools/gpu_r5a.sh

@@ -1901,6 +1901,8 @@ TileGeo tile_geo(const okv_ctx* ctx, const Work& w, uint32_t nblk, bool index_on
   const SpanHint& h = ctx->span_hint;
   if (h.nblk == nblk && h.seg == w.seg && h.descs == w.descs && h.seg_bytes == w.seg_bytes)
     span = std::max<uint64_t>(span, (h.span + 4095) & ~uint64_t(4095));
+  // (the hint is consumed by the decode that uses it -- decode_device clears
+  // it -- so a later batch staged into the same buffers is not sized by it)
   uint64_t tpb = std::min<uint64_t>(64, (span + kT - 1) / kT);
   while (tpb > 1 && uint64_t(nblk) * tpb >= (uint64_t(1) << 31)) tpb >>= 1;
   return {uint32_t(tpb), tpb * kT};
@@ -2032,6 +2034,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   constexpr bool sweep = false;
 #endif
   const TileGeo geo = tile ? tile_geo(ctx, w, nblk, index_only) : TileGeo{1, ~0ull};
+  ctx->span_hint = SpanHint{};  // a plan's hint sizes the one decode that follows it
   uint16_t* rt_kl = nullptr;
   if (tile || sweep) {
     if ((rc = ensure_blocks(ctx, nblk)) ||

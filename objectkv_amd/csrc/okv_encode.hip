@@ -1037,6 +1037,7 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
   __shared__ uint32_t s_wt[2][kThreads / 64];  // VL == 7: per-wave record-size totals
   __syncthreads();
   const uint64_t R0 = bfirst[0], R1 = bfirst[g];
+  const uint64_t abs0 = VL == 7 ? 0 : Pg(P.pl, P.tp, int64_t(R0) - 1);
   uint32_t carry = 0;  // VL == 7: image bytes of the rows before this pass
   for (uint64_t base = R0; base < R1; base += kThreads) {  // uniform trip count (VL == 7 barriers)
     const uint64_t r = base + threadIdx.x;
@@ -1077,8 +1078,12 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
         hi = m;
     }
     if (kMeta && r == bfirst[lo]) bfkl[lo] = kl;
+    // (the other arms: the row's absolute row-stream position from the row
+    // prefix, less the block's -- the region's first row's absolute position
+    // abs0 plus the block's region-relative base)
     const uint32_t d = VL == 7 ? uint32_t(brel[lo] + srel - (bbase[lo] - bbase[0]))
-                              : uint32_t(brel[lo] + Pg(P.pl, P.tp, int64_t(r) - 1) - bbase[lo]);
+                              : uint32_t(brel[lo] + Pg(P.pl, P.tp, int64_t(r) - 1) -
+                                         (abs0 + bbase[lo]));
     if (VL == 5) {
       lds_or16(img, d, make_uint4(kl | (vl << 16), vl >> 16, 0, 0));
     } else if (VL == 6 && kl <= 64 && vl <= 64) {
@@ -1677,27 +1682,55 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   return OKV_OK;
 }
 
-// Data blocks, block hashes and the meta block into seg (E10-E12).
-int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opts& o,
-              const Plan& pl, uint8_t* seg) {
-  enc_mark(ctx, e, 1);
+// Blocks per chunk-major region launch (okv_enc_pack_region_kernel).
+uint64_t pack_region_blocks(const Plan& pl) {
+  return std::min<uint64_t>({uint64_t(kMaxRegion), kPackRows / std::max<uint64_t>(pl.w, 1),
+                             uint64_t(kMaxChunks) * 16 / std::max<uint64_t>(pl.bmax, 1)});
+}
+
+// The product's pack launch (E10-E11): record-major LDS assembly + block hashes
+// for small records, chunk-major regions for large ones, a per-block kernel
+// or a byte kernel when the segment is not 16-byte aligned.  *hashed: the
+// launch also wrote the block hashes.
+int enc_pack(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opts& o,
+             const Plan& pl, uint8_t* seg, const PackParams& pp, bool* hashed) {
   // record-major LDS assembly pays off for small records (most chunks would
   // mix fields); large records take the chunk-major kernels, which read the
   // row prefix (E1-E2; a single-pass plan does not write it)
   const bool aligned = o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0;
   const uint64_t GL = std::min<uint64_t>(kMaxRegion, kImage / std::max<uint64_t>(pl.bmax, 1));
-  const bool lds = aligned && GL >= 1 && pl.avg_rec <= 512;
+  const uint64_t G = pack_region_blocks(pl);
   int rc;
-#ifdef OKV_ABLATE
-  // OKV_ENC_META_FUSED=1: the product arm (meta entries written by the pack kernel)
-  const bool meta_fused = okv::knob("OKV_ENC_META_FUSED") && atoi(okv::knob("OKV_ENC_META_FUSED"));
-  const char* evar0 = okv::knob("OKV_ENC_VARIANT");
-  if (!(lds && (evar0 ? atoi(evar0) : 7) == 7 && !okv::knob("OKV_ENC_IMAGE")) &&
-      (rc = enc_row_prefix(ctx, e, R, o.threshold_bytes)))
-    return rc;  // the arms that read it
-#else
-  if (!lds && (rc = enc_row_prefix(ctx, e, R, o.threshold_bytes))) return rc;
+  if (aligned && GL >= 1 && pl.avg_rec <= 512) {
+    // small records: record-major LDS assembly and the block hashes
+    hipLaunchKernelGGL((okv_enc_pack_lds_kernel<kImage, 7>), dim3(ceil_div(pl.nb, GL)),
+                       dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
+    *hashed = true;
+    return OKV_OK;
+  }
+  if ((rc = enc_row_prefix(ctx, e, R, o.threshold_bytes))) return rc;
+  if (aligned && G >= 1) {  // large records: chunk-major regions
+    hipLaunchKernelGGL(okv_enc_pack_region_kernel<0>, dim3(ceil_div(pl.nb, G)), dim3(kThreads), 0,
+                       ctx->stream, pp, pl.nb, uint32_t(G));
+  } else if (aligned) {
+    hipLaunchKernelGGL(okv_enc_pack_kernel, dim3(uint32_t(pl.nb)), dim3(kThreads), 0,
+                       ctx->stream, pp);
+  } else {
+    const uint32_t g = std::min<uint64_t>(65536, (pl.data_bytes + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(okv_enc_pack_bytes_kernel, dim3(std::max<uint32_t>(g, 1)),
+                       dim3(kThreads), 0, ctx->stream, pp, pl.nb, pl.data_bytes);
+  }
+  return OKV_OK;
+}
+
+#ifdef OKV_ABLATE  // the measured pack variants (OKV_ENC_VARIANT / _IMAGE / _META_FUSED)
+#include "okv_encode_ablate_pack.inc"
 #endif
+
+// Data blocks, block hashes and the meta block into seg (E10-E12).
+int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opts& o,
+              const Plan& pl, uint8_t* seg) {
+  enc_mark(ctx, e, 1);
   PackParams pp;
   pp.key_arena = R.ka;
   pp.key_off = R.ko;
@@ -1715,76 +1748,13 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   pp.meta = nullptr;
   pp.moff = e->moff;
   bool hashed = false, meta_done = false;
-  const uint64_t G = std::min<uint64_t>(
-      {uint64_t(kMaxRegion), kPackRows / std::max<uint64_t>(pl.w, 1),
-       uint64_t(kMaxChunks) * 16 / std::max<uint64_t>(pl.bmax, 1)});
+  int rc;
 #ifdef OKV_ABLATE
-  const char* eimg = okv::knob("OKV_ENC_IMAGE");  // diagnostic: LDS image bytes (16384 / 32768)
-  const int eimg_v = eimg ? atoi(eimg) : 0;
-  const uint32_t img = (eimg_v == 32768 || eimg_v == 8192 || eimg_v == 12288) ? uint32_t(eimg_v)
-                                                                              : kImage;
-  const uint64_t GLa = std::min<uint64_t>(kMaxRegion, img / std::max<uint64_t>(pl.bmax, 1));
-  const char* evar = okv::knob("OKV_ENC_VARIANT");
-  const int EV = evar ? atoi(evar) : 7;
-  if (aligned && GLa >= 1 && pl.avg_rec <= 512 && EV != 3) {
-    if (img == 32768)
-      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<32768>, dim3(ceil_div(pl.nb, GLa)),
-                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GLa));
-    else if (img == 8192)
-      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<8192>, dim3(ceil_div(pl.nb, GLa)),
-                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GLa));
-    else if (img == 12288)
-      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<12288>, dim3(ceil_div(pl.nb, GLa)),
-                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GLa));
-    else if (EV >= 4 && EV <= 9) {
-      void (*kern)(PackParams, uint64_t, uint32_t) = EV == 4   ? okv_enc_pack_lds_kernel<kImage, 4>
-                   : EV == 5 ? okv_enc_pack_lds_kernel<kImage, 5>
-                   : EV == 6 ? okv_enc_pack_lds_kernel<kImage, 6>
-                   : EV == 8 ? okv_enc_pack_lds_kernel<kImage, 8>
-                   : EV == 9 ? okv_enc_pack_lds_kernel<kImage, 9>
-                             : okv_enc_pack_lds_kernel<kImage, 7>;
-      if (EV == 7 && meta_fused) {
-        pp.meta = seg + pl.data_bytes;
-        meta_done = true;
-        kern = okv_enc_pack_lds_kernel<kImage, 7, true>;
-      }
-      hipLaunchKernelGGL(kern, dim3(ceil_div(pl.nb, GLa)), dim3(kThreads), 0, ctx->stream, pp,
-                         pl.nb, uint32_t(GLa));
-    } else
-      hipLaunchKernelGGL(okv_enc_pack_lds_kernel<kImage>, dim3(ceil_div(pl.nb, GLa)),
-                         dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GLa));
-    hashed = true;
-  } else if (aligned && G >= 1) {
-    const int V = EV == 7 ? 0 : EV;
-    const dim3 grid(ceil_div(pl.nb, G)), blk(kThreads);
-    if (V == 1)
-      hipLaunchKernelGGL(okv_enc_pack_region_kernel<1>, grid, blk, 0, ctx->stream, pp, pl.nb,
-                         uint32_t(G));
-    else if (V == 2)
-      hipLaunchKernelGGL(okv_enc_pack_region_kernel<2>, grid, blk, 0, ctx->stream, pp, pl.nb,
-                         uint32_t(G));
-    else
-      hipLaunchKernelGGL(okv_enc_pack_region_kernel<0>, grid, blk, 0, ctx->stream, pp, pl.nb,
-                         uint32_t(G));
-#else
-  if (lds) {
-    // small records: record-major LDS assembly and the block hashes
-    hipLaunchKernelGGL((okv_enc_pack_lds_kernel<kImage, 7>), dim3(ceil_div(pl.nb, GL)),
-                       dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
-    hashed = true;
-  } else if (aligned && G >= 1) {
-    // large records: chunk-major regions
-    hipLaunchKernelGGL(okv_enc_pack_region_kernel<0>, dim3(ceil_div(pl.nb, G)), dim3(kThreads), 0,
-                       ctx->stream, pp, pl.nb, uint32_t(G));
+  bool handled = false;  // an ablation knob chose the pack launch
+  if ((rc = enc_pack_ablate(ctx, e, R, o, pl, seg, pp, &hashed, &meta_done, &handled))) return rc;
+  if (!handled)
 #endif
-  } else if (o.block_size % 16 == 0 && (reinterpret_cast<uintptr_t>(seg) & 15) == 0) {
-    hipLaunchKernelGGL(okv_enc_pack_kernel, dim3(uint32_t(pl.nb)), dim3(kThreads), 0,
-                       ctx->stream, pp);
-  } else {
-    const uint32_t g = std::min<uint64_t>(65536, (pl.data_bytes + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL(okv_enc_pack_bytes_kernel, dim3(std::max<uint32_t>(g, 1)),
-                       dim3(kThreads), 0, ctx->stream, pp, pl.nb, pl.data_bytes);
-  }
+    if ((rc = enc_pack(ctx, e, R, o, pl, seg, pp, &hashed))) return rc;
   enc_mark(ctx, e, 2);
   if (!hashed) launch_hash(ctx->stream, seg, pl.data_bytes, e->desc, uint32_t(pl.nb), e->hash);
   enc_mark(ctx, e, 3);

@@ -308,6 +308,9 @@ int read_block(okv_reader* r, size_t t, const std::vector<okv_row>** rows, Batch
   if (rc) return rc;
   const uint32_t e = uint32_t(r->tree[t].file_index);
   if (r->window && r->window_slot[e] >= 0) {
+    // the rows must outlive a later window replacement (okv_host.h: valid
+    // until the next read_block / get_row / get_range call)
+    r->last_read = r->window;
     *keep = r->window;
     return batch_rows(*r->window, uint32_t(r->window_slot[e]), rows);
   }
@@ -339,7 +342,14 @@ int read_block_iter(okv_reader* r, size_t t, int direction, const std::vector<ok
       batch.push_back(uint32_t(r->tree[i].file_index));
   }
   BatchP B;
-  if ((rc = decode_batch(r, batch, &B))) return rc;
+  if ((rc = decode_batch(r, batch, &B))) {
+    // a failure of the whole window call (e.g. an allocation for a later,
+    // highly inflating block) is not this block's outcome: read it alone, as
+    // Go's Next would, and keep the current window
+    if (batch.size() == 1 || (rc = decode_batch(r, {e}, &B))) return rc;
+    *keep = B;
+    return batch_rows(*B, 0, rows);
+  }
   if (r->window)
     for (uint32_t x : r->window->entries) r->window_slot[x] = -1;
   r->window = B;

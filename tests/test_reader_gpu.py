@@ -269,3 +269,36 @@ def test_getrow_on_large_segment_stages_one_block(decoder, nblk):
     k = last[-1].Key
     assert pr.GetRow(k).Key == k
     assert pr.io_stats()["bytes_staged"] == 2 * 65536
+
+
+def test_getrow_rows_outlive_window_replacement(decoder):
+    """Rows GetRow serves from the iteration window stay valid until the next
+    GetRow / ReadBlock / GetRange call (okv_host.h), even when a later RowIter
+    replaces the window: iterate, free the iterator, GetRow (from the
+    window), seek a new iterator far away (window miss), then read the row's
+    bytes through the returned pointers (okv_reader.cpp
+    read_block)."""
+    import ctypes as C
+    from objectkv_amd._lib import Row, lib
+    rows, data, flen, meta = _segment(nrows=12000, vmax=300)
+    pr = R.SegmentReader(data, flen, decoder)
+    L = lib()
+    it = L.okv_reader_row_iter(pr._h, 0)
+    row = Row()
+    assert L.okv_iter_next(it, C.byref(row)) == 0  # window = the first 256 blocks
+    L.okv_iter_free(it)
+    k, v = rows[700]
+    kb = C.create_string_buffer(k, len(k))
+    got = Row()
+    before = pr.io_stats()["calls"]
+    assert L.okv_reader_get_row(pr._h, kb, len(k), C.byref(got)) == 0
+    assert pr.io_stats()["calls"] == before  # served from the window
+    it2 = L.okv_reader_row_iter(pr._h, 0)
+    far = rows[-5][0]
+    assert L.okv_iter_seek(it2, C.create_string_buffer(far, len(far)), len(far)) == 0
+    assert pr.io_stats()["calls"] > before  # the window moved
+    junk = [bytes(4096) for _ in range(2000)]  # reuse freed memory if any was freed
+    assert C.string_at(got.key, got.key_len) == k
+    assert (C.string_at(got.val, got.val_len) if got.val_len else b"") == v
+    L.okv_iter_free(it2)
+    del junk

@@ -1,6 +1,7 @@
 """Parity of the ablation arms (ablation build, OKV_ABLATE=1 with the arm's
 knob set): the arm must be the path taken and its outputs equal the oracle's.
-usage: OKV_ABLATE=1 <knob>=1 python tools/ablate_check.py stream|pieces|small_pieces|onepass"""
+usage: OKV_ABLATE=1 <knob>=1 python tools/ablate_check.py stream|pieces|small_pieces|onepass
+       OKV_ABLATE=1 python tools/ablate_check.py enc_arms   (sets each encode knob itself)"""
 import os
 import random
 import sys
@@ -49,5 +50,25 @@ elif arm == "onepass":
         if rc == 0:
             assert got.seg.tobytes() == want
         assert enc.last_path() & _lib.PATH_ENC_ONEPASS, enc.last_path()
+    enc.close()
+elif arm == "enc_arms":
+    # the pack launch's variants that write whole segments (the others --
+    # OKV_ENC_VARIANT 1, 2, 4, 5, 6 -- are diagnostics that skip work):
+    # every one byte-equal to the oracle writer over many LDS regions
+    enc = okv.Encoder(0)
+    for knob, val in (("OKV_ENC_VARIANT", "8"), ("OKV_ENC_VARIANT", "9"),
+                      ("OKV_ENC_VARIANT", "3"), ("OKV_ENC_IMAGE", "8192"),
+                      ("OKV_ENC_IMAGE", "12288"), ("OKV_ENC_IMAGE", "32768"),
+                      ("OKV_ENC_META_FUSED", "1")):
+        os.environ[knob] = val
+        for T, vmax in ((3584, 120), (3584, 60), (9000, 60)):
+            rng = random.Random(T + vmax)
+            rows = TE._random_rows(rng, 30000, 8, vmax)
+            rc, want, meta = TE.oracle_segment(rows, T, 4096)
+            got = enc.encode(rows, T, 4096, strict_go=rc == 0)
+            if rc == 0:
+                assert got.seg.tobytes() == want, (knob, val, T, vmax)
+        del os.environ[knob]
+        print(f"  {knob}={val}: parity ok", flush=True)
     enc.close()
 print(f"ablation arm {arm}: parity ok")

@@ -4,8 +4,10 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r5b; mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_point_gpu.py tests/test_reader_gpu.py tests/test_decode_gpu.py -m gpu > $O/tests.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_point_gpu.py tests/test_reader_gpu.py tests/test_decode_gpu.py tests/test_encode_gpu.py -m gpu > $O/tests.log 2>&1
 rc=$?; tail -3 $O/tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 tools/getrow_bench 2000 > $O/getrow.log 2>&1
 rc=$?; cat $O/getrow.log; [ $rc -ne 0 ] && exit $rc
+OKV_ABLATE=1 timeout -k 10 300 python3 tools/ablate_check.py enc_arms > $O/enc_arms.log 2>&1
+rc=$?; tail -9 $O/enc_arms.log; [ $rc -ne 0 ] && exit $rc
 bash tools/gpu_r5a.sh

@@ -63,6 +63,8 @@ CONFIGS = {
            "C1: single segment round trip, 10 000 x 16 B key / 64 B value: write (WriteRow x n "
            "+ Close) + full ascending read"),
 }
+ALLOC_NOTE = ("; allocations from a per-thread bump arena (the analogue of Go's per-P mcache "
+              "fast path: glibc malloc contended past 16 threads), reset every 4 MiB")
 ENC_METRIC = "GiB/s device-resident segment encode (data blocks written, Close included) + M rows/s"
 CMP_METRIC = "GiB/s device-resident compaction (input segment bytes) + M rows/s"
 RT_METRIC = "MB/s segment round trip (write + full ascending read, segment bytes) + rows/s"
@@ -565,8 +567,10 @@ def run_decode(args, torch, okv, D):
                      "traffic_source": traffic_src, "decode_source_sha": source_sha(),
                      # the same kernel's rocprofv3 trace average (another process, maybe
                      # another box) and the event time the traced process measured itself
-                     "trace": trace_roofline(args.config, alg,
-                                             ZSTD_SOURCES if comp else DECODE_SOURCES)},
+                     # (one GPU alone: omitted when ranks share the box's GPUs)
+                     "trace": (trace_roofline(args.config, alg,
+                                              ZSTD_SOURCES if comp else DECODE_SOURCES)
+                               if world == 1 else None)},
         "cpu_baseline": cpu,
         "verify": ver,
         "dist": D.info(),
@@ -610,7 +614,7 @@ def cpu_decode_baseline(args, seg, descs, nblk, comp):
                          f"{max(res)} threads), whole passes for "
                          f"{args.cpu_seconds / len(thread_counts()):.1f} s per thread count; C "
                          f"restatement of Go ReadBlockWithStat with Go allocation semantics (Go "
-                         f"toolchain unavailable)")
+                         f"toolchain unavailable)" + ALLOC_NOTE)
 
 
 # ---- encode (C4) ------------------------------------------------------------------
@@ -798,7 +802,8 @@ def cpu_encode_baseline(args, rows, n, th, bs):
     return sweep_summary(res, 1 / 2**30, "GiB/s", "port",
                          f"min({sample}, 1 M x threads) rows per pass as one key-range segment "
                          f"per thread; C restatement of Go WriteRow+Close with per-row rowBuf "
-                         f"allocation (Go toolchain unavailable); segment bytes written / s")
+                         f"allocation (Go toolchain unavailable); segment bytes written / s"
+                         + ALLOC_NOTE)
 
 
 # ---- compaction (CM) -----------------------------------------------------------------
@@ -956,8 +961,10 @@ def run_compact(args, torch, okv, D):
     achieved = alg / (gather_ms * 1e-3) / 1e9
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:  # (after every rank's timing)
         cpu = cpu_compact_baseline(args, segs, n, per_block, th, bs, K)
+        if world > 1:
+            cpu["sample"] += f"; run on rank 0 of {world} after the timed region"
 
     line = {
         "metric": CMP_METRIC, "value": round(in_bytes * world / t_step / 2**30, 3),
@@ -1023,7 +1030,7 @@ def cpu_compact_baseline(args, segs, n, per_block, th, bs, K):
                          f"({in_b} B in, {n_out} rows merged and written{q1}) per compaction, one "
                          f"independent compaction per thread; C restatement: "
                          f"ReadBlockWithStat per block, newest-wins merge, Go writer (the "
-                         f"reference's compactor is a stub)")
+                         f"reference's compactor is a stub)" + ALLOC_NOTE)
 
 
 # ---- C1 round trip ---------------------------------------------------------------------
@@ -1085,7 +1092,7 @@ def run_roundtrip(args, torch, okv, D):
     t_step = t_max / args.steps
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:  # (after every rank's timing)
         def once(nth):
             _r, b_ = coracle.roundtrip_go(host, n, th, bs, nth)
             return b_
@@ -1093,7 +1100,9 @@ def run_roundtrip(args, torch, okv, D):
         cpu = sweep_summary(res, 1e-6, "MB/s", "port",
                             "the whole C1 round trip per pass, one independent segment per "
                             "thread; C restatement of Go WriteRow/Close + ReadBlockWithStat "
-                            "with Go allocations")
+                            "with Go allocations" + ALLOC_NOTE)
+        if world > 1:
+            cpu["sample"] += f"; run on rank 0 of {world} after the timed region"
     line = {
         "metric": RT_METRIC, "value": round(fb * world / t_step / 1e6, 3), "unit": "MB/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

@@ -584,6 +584,99 @@ static int walk_records(const uint8_t *buf, uint64_t len, uint64_t orig, row_cb 
   return OREF_BLK_OK;
 }
 
+/* ---- Go's allocation fast path for the CPU baselines ---------------------
+ * Go serves each make([]byte, n) from the P's mcache span of its size class:
+ * no lock and no contention between Ps.  glibc malloc contends past ~16
+ * threads on the GPU box's host, which a Go program would not,
+ * so the baseline jobs (oref_*_go) allocate from a per-thread bump arena
+ * (16-byte granules, like the small size classes) whose frees are no-ops; a
+ * decode or encode job resets it between blocks / rows once 4 MiB are in use
+ * (the GC's own work is not counted).  Outside those jobs (the oracle proper)
+ * the functions below are plain malloc / realloc / free. */
+typedef struct arena_chunk {
+  struct arena_chunk *next;
+  size_t cap, used;
+  uint8_t *data;
+} arena_chunk;
+static __thread arena_chunk *t_arena;
+static __thread int t_arena_on;
+static __thread size_t t_arena_since;  /* bytes handed out since the last reset */
+/* chunks of finished jobs, kept faulted-in for the next job (threads are
+ * created per call; touching fresh pages would make every pass pay page faults) */
+static arena_chunk *g_pool;
+static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
+static const size_t kArenaChunk = (size_t)16 << 20;
+
+static void arena_begin(void) {
+  t_arena_on = 1;
+  t_arena_since = 0;
+}
+static void arena_release(arena_chunk *c) { /* to the pool (standard-size chunks) or freed */
+  if (c->cap != kArenaChunk) {
+    free(c->data);
+    free(c);
+    return;
+  }
+  pthread_mutex_lock(&g_pool_mu);
+  c->next = g_pool;
+  g_pool = c;
+  pthread_mutex_unlock(&g_pool_mu);
+}
+static void arena_reset(void) {
+  if (!t_arena) return;
+  arena_chunk *keep = t_arena, *c = keep->next;
+  while (c) {
+    arena_chunk *n = c->next;
+    arena_release(c);
+    c = n;
+  }
+  keep->next = NULL;
+  keep->used = 0;
+  t_arena_since = 0;
+}
+static void arena_end(void) {
+  arena_reset();
+  if (t_arena) arena_release(t_arena);
+  t_arena = NULL;
+  t_arena_on = 0;
+}
+static void *go_alloc(size_t n) {
+  if (!t_arena_on) return malloc(n ? n : 1);
+  n = n ? (n + 15) & ~(size_t)15 : 16;
+  if (!t_arena || t_arena->used + n > t_arena->cap) {
+    arena_chunk *c = NULL;
+    if (n <= kArenaChunk) {
+      pthread_mutex_lock(&g_pool_mu);
+      if ((c = g_pool)) g_pool = c->next;
+      pthread_mutex_unlock(&g_pool_mu);
+    }
+    if (!c) {
+      c = (arena_chunk *)malloc(sizeof(*c));
+      c->cap = n > kArenaChunk ? n : kArenaChunk;
+      c->data = (uint8_t *)malloc(c->cap);
+    }
+    c->used = 0;
+    c->next = t_arena;
+    t_arena = c;
+  }
+  void *p = t_arena->data + t_arena->used;
+  t_arena->used += n;
+  t_arena_since += n;
+  return p;
+}
+static void go_free(void *p) {
+  if (!t_arena_on) free(p);
+}
+static void *go_realloc(void *p, size_t old, size_t n) {
+  if (!t_arena_on) return realloc(p, n);
+  void *q = go_alloc(n); /* append growth: a new backing array, the old one is garbage */
+  if (p && old) memcpy(q, p, old < n ? old : n);
+  return q;
+}
+static void arena_maybe_reset(void) {
+  if (t_arena_on && t_arena_since > ((size_t)4 << 20)) arena_reset();
+}
+
 typedef struct {
   const uint8_t *buf;
   oref_rows *out;
@@ -592,15 +685,16 @@ static void go_row(void *c, uint64_t rec, uint64_t kl, uint64_t vl) {
   go_ctx *g = (go_ctx *)c;
   oref_rows *o = g->out;
   if (o->n == o->cap) { /* append growth :351 */
+    const size_t old = o->cap * sizeof(oref_kv);
     o->cap = o->cap ? 2 * o->cap : 4;
-    o->rows = (oref_kv *)realloc(o->rows, o->cap * sizeof(oref_kv));
+    o->rows = (oref_kv *)go_realloc(o->rows, old, o->cap * sizeof(oref_kv));
   }
   oref_kv *kv = &o->rows[o->n++];
   kv->key_len = kl;
   kv->val_len = vl;
-  kv->key = kl ? (uint8_t *)malloc(kl) : NULL; /* readBytes :490-494 */
+  kv->key = kl ? (uint8_t *)go_alloc(kl) : NULL; /* readBytes :490-494 */
   if (kl) memcpy(kv->key, g->buf + rec + 6, kl);
-  kv->val = vl ? (uint8_t *)malloc(vl) : NULL;
+  kv->val = vl ? (uint8_t *)go_alloc(vl) : NULL;
   if (vl) memcpy(kv->val, g->buf + rec + 6 + kl, vl);
 }
 
@@ -613,22 +707,22 @@ int oref_read_block(const uint8_t *seg, uint64_t seg_len, const oref_block_desc 
   int st = block_buffer(seg, seg_len, d, compression, &buf, &len, &owned);
   if (st) return st;
   /* rawBlockBytes := make([]byte, BlockSize); Read (:309-310) -- a copy */
-  uint8_t *copy = (uint8_t *)malloc(len ? len : 1);
+  uint8_t *copy = (uint8_t *)go_alloc(len ? len : 1);
   if (len) memcpy(copy, buf, len);
   free(owned);
   go_ctx g = {copy, out};
   st = walk_records(copy, len, d->original_size, go_row, &g);
-  free(copy);
+  go_free(copy);
   if (st) oref_rows_free(out);
   return st;
 }
 
 void oref_rows_free(oref_rows *r) {
   for (uint64_t i = 0; i < r->n; i++) {
-    free(r->rows[i].key);
-    free(r->rows[i].val);
+    go_free(r->rows[i].key);
+    go_free(r->rows[i].val);
   }
-  free(r->rows);
+  go_free(r->rows);
   memset(r, 0, sizeof(*r));
 }
 
@@ -643,6 +737,7 @@ typedef struct {
 } job_t;
 static void *job_run(void *a) {
   job_t *j = (job_t *)a;
+  arena_begin();
   for (uint64_t b = j->b0; b < j->b1; b++) {
     oref_rows r;
     if (oref_read_block(j->seg, j->seg_len, &j->d[b], j->comp, &r) == OREF_BLK_OK) {
@@ -650,7 +745,9 @@ static void *job_run(void *a) {
       for (uint64_t i = 0; i < r.n; i++) j->payload += r.rows[i].key_len + r.rows[i].val_len;
       oref_rows_free(&r);
     }
+    arena_maybe_reset();
   }
+  arena_end();
   return NULL;
 }
 uint64_t oref_decode_range_go(const uint8_t *seg, uint64_t seg_len, const oref_block_desc *d,
@@ -697,14 +794,17 @@ static void *enc_run(void *arg) {
   enc_job *j = (enc_job *)arg;
   oref_writer *w = oref_writer_new(j->T, j->D, 0, j->lz4);
   j->rc = 0;
+  arena_begin();
   for (uint64_t i = j->lo; i < j->hi && !j->rc; i++) {
     const size_t k = j->kl[i], v = j->vl[i];
-    uint8_t *row = (uint8_t *)malloc(6 + k + v); /* :121 make */
-    memcpy(row + 6, j->ka + j->ko[i], k);        /* :124 */
-    memcpy(row + 6 + k, j->va + j->vo[i], v);    /* :125 */
+    uint8_t *row = (uint8_t *)go_alloc(6 + k + v); /* :121 make */
+    memcpy(row + 6, j->ka + j->ko[i], k);          /* :124 */
+    memcpy(row + 6 + k, j->va + j->vo[i], v);      /* :125 */
     j->rc = oref_writer_write_row(w, row + 6, k, row + 6 + k, v);
-    free(row);
+    go_free(row);
+    arena_maybe_reset();
   }
+  arena_end();
   uint64_t flen = 0;
   /* Close panics in Go when the last WriteRow flushed (Q1); the rows are
      written either way, and the throughput baseline counts them */
@@ -783,13 +883,15 @@ static void *rt_run(void *arg) {
   enc_job e = {j->ka, j->va, j->ko, j->vo, j->kl, j->vl, 0, j->n, j->T, j->D, 0, 0, 0};
   oref_writer *w = oref_writer_new(j->T, j->D, 0, 0);
   j->rc = 0;
+  arena_begin();
   for (uint64_t i = 0; i < j->n && !j->rc; i++) {
     const size_t k = e.kl[i], v = e.vl[i];
-    uint8_t *row = (uint8_t *)malloc(6 + k + v);
+    uint8_t *row = (uint8_t *)go_alloc(6 + k + v);
     memcpy(row + 6, e.ka + e.ko[i], k);
     memcpy(row + 6 + k, e.va + e.vo[i], v);
     j->rc = oref_writer_write_row(w, row + 6, k, row + 6 + k, v);
-    free(row);
+    go_free(row);
+    arena_maybe_reset();
   }
   const uint8_t *file = NULL;
   uint64_t flen = 0;
@@ -802,7 +904,9 @@ static void *rt_run(void *arg) {
     oref_rows r = {0, 0, 0};
     if (oref_read_block(file, flen, &d, 0, &r) == OREF_BLK_OK) j->rows += r.n;
     oref_rows_free(&r);
+    arena_maybe_reset();
   }
+  arena_end();
   oref_writer_free(w);
   return NULL;
 }
@@ -866,6 +970,7 @@ static void *cm_run(void *arg) {
   cm_job *j = (cm_job *)arg;
   oref_rows *all = (oref_rows *)calloc((size_t)j->k, sizeof(oref_rows));
   j->rc = 0;
+  arena_begin();  /* (no reset: the decoded rows live until the merge has written them) */
   for (int s = 0; s < j->k && !j->rc; s++) { /* decode: ReadBlockWithStat per block */
     for (uint64_t b = 0; b < j->nblks[s] && !j->rc; b++) {
       oref_rows r = {0, 0, 0};
@@ -874,12 +979,13 @@ static void *cm_run(void *arg) {
       } else {
         for (uint64_t i = 0; i < r.n; i++) { /* append (the RowIter's rows) */
           if (all[s].n == all[s].cap) {
+            const size_t old = all[s].cap * sizeof(oref_kv);
             all[s].cap = all[s].cap ? 2 * all[s].cap : 1024;
-            all[s].rows = (oref_kv *)realloc(all[s].rows, all[s].cap * sizeof(oref_kv));
+            all[s].rows = (oref_kv *)go_realloc(all[s].rows, old, all[s].cap * sizeof(oref_kv));
           }
           all[s].rows[all[s].n++] = r.rows[i];
         }
-        free(r.rows); /* the row copies now belong to all[s] */
+        go_free(r.rows); /* the row copies now belong to all[s] */
       }
     }
   }
@@ -909,6 +1015,7 @@ static void *cm_run(void *arg) {
   j->bytes_out = flen;
   oref_writer_free(w);
   for (int s = 0; s < j->k; s++) oref_rows_free(&all[s]);
+  arena_end();
   free(all);
   free(pos);
   return NULL;

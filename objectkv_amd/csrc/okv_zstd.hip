@@ -219,16 +219,21 @@ struct RegWin {
   uint32_t w;     // this lane's dword
   int32_t boff;   // window bit of the stream's bit 0
 };
+// Every lane's dword is computed with the whole wave active and no branch:
+// the window is read back by v_readlane from arbitrary lanes, and a lane that
+// was inactive when its VGPR was written holds no defined value (DESIGN.md
+// 15.3).  Lanes past the stream load the stream's first dword (always
+// readable) and select 0.
 __device__ __forceinline__ RegWin regwin_load(const uint8_t* p, int64_t n) {
   const uintptr_t pa = reinterpret_cast<uintptr_t>(p), base = pa & ~uintptr_t(3);
   const uintptr_t a = base + 4 * (threadIdx.x & 63);
   const int64_t rel = int64_t(a) - int64_t(pa);  // stream byte of the dword's first byte
-  uint32_t v = 0;
-  if (rel + 4 > 0 && rel < n) v = *reinterpret_cast<const uint32_t*>(a);
+  const bool in = rel + 4 > 0 && rel < n;
+  const uint32_t x = *reinterpret_cast<const uint32_t*>(in ? a : base);
+  uint32_t keep = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    if (rel + k < 0 || rel + k >= n) v &= ~(0xffu << (8 * k));
-  return RegWin{v, int32_t(8 * (pa - base))};
+  for (int k = 0; k < 4; ++k) keep |= (rel + k >= 0 && rel + k < n) ? (0xffu << (8 * k)) : 0u;
+  return RegWin{in ? (x & keep) : 0u, int32_t(8 * (pa - base))};
 }
 // Window bits fit: stream bits [b, b + 32) lie below the window's end.
 __device__ __forceinline__ bool regwin_has(const RegWin& r, int64_t b) {
@@ -255,7 +260,7 @@ __device__ int32_t read_ncount(const uint8_t* p, int64_t n, int16_t* norm, uint3
     if (regwin_has(win, bit))
       return regwin_get32(win, int32_t(bit)) & ((1u << k) - 1u);
     const uint64_t v = ld64z(p, bit >> 3, n) >> (bit & 7);
-    return uint32_t(v & ((uint64_t(1) << k) - 1));
+    return rfl(uint32_t(v & ((uint64_t(1) << k) - 1)));  // (a flat load: uniform by fiat)
   };
   const uint32_t al = peek(4) + 5;
   bit += 4;
@@ -322,6 +327,8 @@ __device__ int32_t read_ncount(const uint8_t* p, int64_t n, int16_t* norm, uint3
 __device__ bool build_fse(uint32_t* table, const int16_t* norm, uint32_t nsym, uint32_t al,
                           uint16_t* next) {
   __shared__ uint16_t s_cum[64];  // first placement of each symbol
+  nsym = rfl(nsym);  // (uniform: every branch below holds a ballot, DPP or barrier)
+  al = rfl(al);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t size = 1u << al, mask = size - 1;
   const uint64_t below = (uint64_t(1) << lane) - 1;
@@ -396,7 +403,7 @@ __device__ __forceinline__ void build_rle(uint32_t* table, uint32_t sym) {
 // sets max_bits.
 __device__ int32_t read_huf_tree(SmemCore& sm, const uint8_t* p, int64_t n, uint32_t& max_bits) {
   if (n < 1) return -1;
-  const uint32_t hb = p[0];
+  const uint32_t hb = rfl(p[0]);
   uint32_t nw;  // weights given explicitly (the last one is implied)
   int32_t used;
   const bool w0 = (threadIdx.x & 63) == 0;
@@ -414,6 +421,7 @@ __device__ int32_t read_huf_tree(SmemCore& sm, const uint8_t* p, int64_t n, uint
     uint32_t al, nsym;
     const int32_t hlen = read_ncount(p + 1, csz, sm.norm, 15, 6, al, nsym);
     if (hlen < 0) return -1;
+    __syncthreads();  // norm[] (every lane's stores) before the build reads it
     if (!build_fse(sm.hw, sm.norm, nsym, al, sm.next)) return -1;
     // The weight stream (< 128 bytes) and the table (<= 64 states, lane =
     // state) live in registers: the serial decode below reads both with
@@ -795,6 +803,8 @@ __device__ __forceinline__ uint32_t seqbits_read(SeqBits& b, uint32_t nb) {
 __device__ int32_t seq_table(SmemCore& sm, uint32_t* table, uint32_t mode, const int16_t* def,
                              uint32_t def_al, uint32_t def_n, uint32_t max_sym, uint32_t max_al,
                              const uint8_t* p, int64_t n, bool& ok, uint32_t& al) {
+  mode = rfl(mode);  // (uniform: the table builds hold ballots, DPP and barriers)
+  n = rfls64(n);
   switch (mode) {
     case 0: {  // Predefined_Mode
       for (uint32_t s = threadIdx.x & 63; s < def_n; s += 64) sm.norm[s] = def[s];
@@ -805,8 +815,8 @@ __device__ int32_t seq_table(SmemCore& sm, uint32_t* table, uint32_t mode, const
       return 0;
     }
     case 1: {  // RLE_Mode
-      if (n < 1 || p[0] > max_sym) return ZFAIL(-1);
-      build_rle(table, p[0]);
+      if (n < 1 || rfl(p[0]) > max_sym) return ZFAIL(-1);
+      build_rle(table, rfl(p[0]));
       ok = true;
       al = 0;
       return 1;
@@ -825,22 +835,6 @@ __device__ int32_t seq_table(SmemCore& sm, uint32_t* table, uint32_t mode, const
   }
 }
 
-// seq_table as a real call, for the one-wave-per-block kernel: inlined into
-// okv_zstd_kernel (ROCm 7.2 clang, gfx950, -O3) the offset table came out
-// wrong for every block of the zstd test cases (OKV_BLK_ZSTD_ERROR at the OF
-// table) while the same source inlined into the prologue kernel decodes them;
-// any change of the inlined code's shape (a diagnostic store, -O2 elsewhere)
-// moved the failure, a call removes it.  tests/test_zstd_gpu.py::test_zstd_cases
-// [one_pass-*] is the check.
-__device__ __attribute__((noinline)) int32_t seq_table_call(SmemCore& sm, uint32_t* table,
-                                                           uint32_t mode, const int16_t* def,
-                                                           uint32_t def_al, uint32_t def_n,
-                                                           uint32_t max_sym, uint32_t max_al,
-                                                           const uint8_t* p, int64_t n, bool& ok,
-                                                           uint32_t& al) {
-  return seq_table(sm, table, mode, def, def_al, def_n, max_sym, max_al, p, n, ok, al);
-}
-
 // Decompress one compressed zstd block (RFC 8878 3.1.1.3) into the output.
 template <bool PRO, class SM>
 __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_t* p, int64_t n,
@@ -855,7 +849,7 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
   const uint64_t blk_end = o.pos + rfl(o.bmax);
   const long long t0 = o.prof ? clock64() : 0;
   // ---- literals section header (3.1.1.3.1.1)
-  const uint32_t b0 = p[0];
+  const uint32_t b0 = rfl(p[0]);
   const uint32_t ltype = b0 & 3, sf = (b0 >> 2) & 3;
   uint32_t regen = 0, csize = 0, hdr = 0, nstreams = 1;
   if (ltype <= 1) {
@@ -896,6 +890,8 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       nstreams = 4;
     }
   }
+  regen = rfl(regen);  // (flat loads: uniform by fiat, as every header field here)
+  csize = rfl(csize);
   if (regen > kBlockMax) return ZERR;
   const uint8_t* lits = nullptr;  // literal source for the sequences
   uint8_t rle_byte = 0;
@@ -938,12 +934,13 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       // decodes 16 blocks' streams per wave, one lane each (here 4 of the
       // wave's 64 lanes would).  nseq == 0 (the byte after the literals is 0)
       // emits the literals in this stage and decodes them here.
-      if (pro->deferrable && at + int64_t(csize) < n && p[at + csize] != 0) {
+      if (pro->deferrable && at + int64_t(csize) < n && rfl(p[at + csize]) != 0) {
         const uint32_t mb = fs.huf_bits;
         if (nstreams == 4) {
           if (qn < 6) return ZERR;
-          const uint32_t s1 = q[0] | (uint32_t(q[1]) << 8), s2 = q[2] | (uint32_t(q[3]) << 8),
-                         s3 = q[4] | (uint32_t(q[5]) << 8);
+          const uint32_t s1 = rfl(q[0] | (uint32_t(q[1]) << 8)),
+                         s2 = rfl(q[2] | (uint32_t(q[3]) << 8)),
+                         s3 = rfl(q[4] | (uint32_t(q[5]) << 8));
           const int64_t s4 = qn - 6 - int64_t(s1) - s2 - s3;
           if (s4 < 0) return ZERR;
           if (3 * ((regen + 3) / 4) > regen) return ZERR;
@@ -973,8 +970,8 @@ __device__ int32_t compressed_block(SM& sm, FrameState& fs, Out& o, const uint8_
       if (lane == 0) good = huf_stream(sm.huf, fs.huf_bits, q, qn, lit_buf, regen);
     } else {
       if (qn < 6) return ZERR;
-      const uint32_t s1 = q[0] | (uint32_t(q[1]) << 8), s2 = q[2] | (uint32_t(q[3]) << 8),
-                     s3 = q[4] | (uint32_t(q[5]) << 8);
+      const uint32_t s1 = rfl(q[0] | (uint32_t(q[1]) << 8)), s2 = rfl(q[2] | (uint32_t(q[3]) << 8)),
+                     s3 = rfl(q[4] | (uint32_t(q[5]) << 8));
       const int64_t s4 = qn - 6 - int64_t(s1) - s2 - s3;
       if (s4 < 0) return ZERR;
       const uint32_t seg = (regen + 3) / 4;
@@ -1037,11 +1034,10 @@ sequences:
     if (!pro->deferrable) return kSlow;
   }
   if (at >= n) return ZERR;
-  const uint32_t modes = p[at++];
+  const uint32_t modes = rfl(p[at++]);
   if (modes & 3) return ZERR;  // reserved bits
   int32_t used;
-  // (the one-pass kernel calls the table builds, see seq_table_call)
-  auto table = [&](auto&&... a) { return PRO ? seq_table(sm, a...) : seq_table_call(sm, a...); };
+  auto table = [&](auto&&... a) { return seq_table(sm, a...); };
   used = table(sm.ll, modes >> 6, LL_DEF, 6, 36, 35, kLLMaxAL, p + at, n - at, fs.ll_ok, fs.ll_al);
   if (used < 0) return ZERR;
   at += used;

@@ -1315,7 +1315,7 @@ __device__ __forceinline__ void copy_region(const Src& src, uint8_t* __restrict_
                                             const uint32_t* len, bool is_val, int nb,
                                             uint32_t G) {
   const uint32_t tid = threadIdx.x;
-  const uint32_t grp = tid / G, sub = tid % G, ngrp = kThreads / G;
+  const uint32_t grp = tid / G, sub = tid % G, ngrp = blockDim.x / G;
   for (uint32_t i = grp; i < uint32_t(nb); i += ngrp) {
     const uint64_t L = len[i];
     if (L == 0) continue;
@@ -1371,7 +1371,7 @@ __device__ __forceinline__ void materialise(const Src& src, const CopyParams& P,
     }
     __syncthreads();
     // SoA row index (coalesced over rows)
-    for (int i = tid; i < nb; i += kThreads) {
+    for (int i = tid; i < nb; i += blockDim.x) {
       const uint64_t g = row0 + r0 + i;
       P.key_off[g] = kb0 + sm.s.kpre[i];
       P.key_len[g] = uint16_t(sm.s.klen[i]);
@@ -1403,7 +1403,7 @@ __device__ __forceinline__ void copy_region_fast(const uint4* __restrict__ s4, u
                                                  const FastRows& t, int rows, uint32_t G) {
   const uint32_t* pre = kVal ? t.vpre : t.kpre;
   const uint32_t tid = threadIdx.x;
-  const uint32_t grp = tid / G, sub = tid % G, ngrp = kThreads / G;
+  const uint32_t grp = tid / G, sub = tid % G, ngrp = blockDim.x / G;
   for (uint32_t i = grp; i < uint32_t(rows); i += ngrp) {
     const uint32_t p0 = pre[i], p1 = pre[i + 1];
     if (p1 == p0) continue;
@@ -1443,7 +1443,7 @@ __device__ __forceinline__ void emit_fast(const CopyParams& P, CopySmem& sm, uin
                                           uint64_t row0, uint64_t kb0, uint64_t vb0) {
   const uint32_t tid = threadIdx.x;
   FastRows& t = sm.f;
-  for (int i = tid; i < rows; i += kThreads) {
+  for (int i = tid; i < rows; i += blockDim.x) {
     const uint64_t g = row0 + i;
     P.key_off[g] = kb0 + t.kpre[i];
     P.key_len[g] = uint16_t(t.kpre[i + 1] - t.kpre[i]);
@@ -2026,12 +2026,16 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   // the round-2 forms (row pass + address-ordered value sweep)
   const bool large = nblk && !fused && !stream && gather_threads(ctx, w, nblk) == 256;
 #ifdef OKV_ABLATE
-  const bool tile = large && ctx->value_sweep == 8;
-  const bool sweep = large && !tile && ctx->value_sweep && !index_only && ctx->gather_staged &&
-                     o->row_cap < (uint64_t(1) << 32);
+  // OKV_VALUE_SWEEP=9: the one-launch per-block decode (okv_block_kernel)
+  // (10: the same with 512-thread workgroups)
+  const bool block = large && (ctx->value_sweep == 9 || ctx->value_sweep == 10) && !index_only &&
+                     !w.pre;
+  const bool tile = large && !block && ctx->value_sweep >= 8;
+  const bool sweep = large && !tile && !block && ctx->value_sweep && !index_only &&
+                     ctx->gather_staged && o->row_cap < (uint64_t(1) << 32);
 #else
   const bool tile = large;  // the product: okv_tile_kernel for every large-block decode
-  constexpr bool sweep = false;
+  constexpr bool sweep = false, block = false;
 #endif
   const TileGeo geo = tile ? tile_geo(ctx, w, nblk, index_only) : TileGeo{1, ~0ull};
   ctx->span_hint = SpanHint{};  // a plan's hint sizes the one decode that follows it
@@ -2054,7 +2058,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
                                         ~uint32_t(kTile - 1));
   if (spn >= nblk) spn = 0;
 #endif
-  if (fused || stream) {
+  if (fused || stream || block) {
     if ((rc = ensure_fused(ctx, nblk))) return rc;
     prof_mark(ctx, 2);
     prof_mark(ctx, 3);
@@ -2132,7 +2136,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
     OKV_HIP(hipStreamWaitEvent(ctx->stream, ctx->chain->p3_done, 0));
   if (nblk) {
     const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
-    if (fused || stream) {
+    if (fused || stream || block) {
       FusedParams F;
       F.pre = w.pre;
       F.cnt = ctx->d_cnt;
@@ -2149,7 +2153,11 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       F.tot = ctx->d_tot;
       F.big_zero = big_counter(ctx, 1);
 #ifdef OKV_ABLATE
-      if (stream)
+      if (block && ctx->value_sweep == 10)
+        hipLaunchKernelGGL(okv_block_kernel<512>, dim3(nblk), dim3(512), 0, ctx->stream, P, F);
+      else if (block)
+        hipLaunchKernelGGL(okv_block_kernel<1024>, dim3(nblk), dim3(1024), 0, ctx->stream, P, F);
+      else if (stream)
         hipLaunchKernelGGL(okv_decode_stream_kernel, dim3(nblk), dim3(64), 0, ctx->stream, P, F);
       else
 #endif
@@ -2160,7 +2168,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
         return set_err(ctx, OKV_E_HIP, "okv_decode_fused_kernel launch", le);
       }
       ctx->f_base += nblk;  // both counters advanced by nblk once the grid completes
-      ctx->big_slot ^= 1u;  // the kernel zeroed the other slot (see big_counter)
+      if (!block) ctx->big_slot ^= 1u;  // the kernel zeroed the other slot (see big_counter)
     } else if (tile) {
       if ((ctx->tile_diag >= 3 && ctx->tile_diag <= 5) || ctx->tile_diag == 7) {
         // phase probe: 8 timestamps per 256th workgroup
@@ -2236,7 +2244,9 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
     }
 #endif
     const uint32_t nbig_grid = std::min<uint32_t>(nblk, 512);
-    if (index_only)
+    if (block) {
+      // (the block kernel decodes every block itself)
+    } else if (index_only)
       hipLaunchKernelGGL(okv_index_kernel, dim3((nbig_grid + kThreads - 1) / kThreads),
                          dim3(kThreads), 0, ctx->stream, P);
     else
@@ -2555,7 +2565,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
   if (const char* v = getenv("OKV_VALUE_SWEEP")) {
     ctx->value_sweep = uint32_t(atoi(v));
-    if (ctx->value_sweep > 8 || ctx->value_sweep == 3) {
+    if (ctx->value_sweep > 10 || ctx->value_sweep == 3) {
       delete ctx;
       return nullptr;
     }

@@ -93,8 +93,12 @@ struct EncScratch {
   uint64_t* bsl = nullptr;       // [nb] tile-local inclusive BlockSize scan
   uint64_t* esl = nullptr;       // [nb] tile-local inclusive meta entry size scan
   uint64_t* moff = nullptr;      // [nb] meta entry offsets (relative to the meta block)
-  uint64_t* pbase = nullptr;     // [nb] P(first row - 1): the block's start in the row prefix
+  uint64_t* orig = nullptr;      // [nb] OriginalSize (the rows' record bytes) of each block
+  uint16_t* fkl = nullptr;       // [nb] key length of each block's first row (its FirstKey)
   size_t cap_blocks = 0;
+  uint32_t* jts = nullptr;       // [ntiles][kCutS] level-0 chain table of the one-pass cut
+  uint32_t* jbs = nullptr;
+  size_t cap_cut = 0;
   uint64_t* btile = nullptr;     // [4][nbtiles]: BlockSize tot/pre, entry tot/pre
   size_t cap_btiles = 0;
   // single-pass plan (okv_enc_plan_kernel): per-chunk look-back state
@@ -127,7 +131,8 @@ void enc_release(okv_ctx* ctx) {
   EncScratch* e = ctx->enc;
   if (!e) return;
   void* ps[] = {e->pl, e->nx, e->tile_tot, e->tile_pre, e->jt, e->jb, e->entry, e->kbase,
-                e->first, e->desc, e->hash, e->bsl, e->esl, e->moff, e->pbase, e->btile,
+                e->first, e->desc, e->hash, e->bsl, e->esl, e->moff, e->orig, e->fkl, e->jts,
+                e->jbs, e->btile,
                 e->d_tot, e->d_in, e->d_outseg, e->p_flag, e->p_inc, e->p_tab, e->p_jlim,
                 e->p_ctr};
   for (void* p : ps)
@@ -537,10 +542,14 @@ __global__ __launch_bounds__(kThreads) void okv_enc_resolve_kernel(
   if (c == nch - 1) tot->nb = cnt + jb[c * W + pos];
 }
 
+// (the general path, after E3 over global P: a block longer than the fused
+// lookahead; okv_enc_emit_tile_kernel is the usual one)
 __global__ __launch_bounds__(kThreads) void okv_enc_emit_kernel(
     const uint32_t* __restrict__ nx, uint64_t n, uint64_t C, uint64_t nch,
     const uint32_t* __restrict__ entry, const uint64_t* __restrict__ kbase,
-    uint64_t* __restrict__ first, uint64_t nb, EncTotals* __restrict__ tot) {
+    uint64_t* __restrict__ first, uint64_t nb, const uint64_t* __restrict__ pl,
+    const uint64_t* __restrict__ tp, const uint16_t* __restrict__ key_len,
+    uint64_t* __restrict__ orig, uint16_t* __restrict__ fkl, EncTotals* __restrict__ tot) {
   const uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (c >= nch) return;
   const uint64_t ce = std::min<uint64_t>(n, (c + 1) * C);
@@ -550,11 +559,202 @@ __global__ __launch_bounds__(kThreads) void okv_enc_emit_kernel(
       tot->fault = 1;
       return;
     }
-    first[k++] = pos;
-    pos += nx[pos];
+    const uint64_t nxt = pos + nx[pos];
+    first[k] = pos;
+    orig[k] = Pg(pl, tp, int64_t(nxt) - 1) - Pg(pl, tp, int64_t(pos) - 1);
+    fkl[k] = key_len[pos];
+    ++k;
+    pos = nxt;
   }
   if (c == nch - 1) {
     if (k != nb) tot->fault = 1;
+    first[nb] = n;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The tile cut: E1 + E3 + E4 per kETile-row tile in LDS --
+// record sizes, next(a) and the tile's level-0 chain table -- and, after the
+// pointer doubling (E5-E6), E7 per tile in LDS again with each block's
+// OriginalSize and FirstKey length for E8.  No per-row array is written
+// (round 4 wrote the record prefix and next(a), 12 B per row, and read them
+// back in scattered chain walks and the stat kernel); each tile reads its
+// rows' lengths (6 B per row) twice instead.  A block longer than the
+// lookahead (tot->far) takes the general kernels above.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kCutS = kFuseLook + 1;  // entry offsets into a tile: chains enter at <= kFuseLook
+
+struct CutSmem {
+  uint64_t W[kFuseWin + 1];  // W[m] = record bytes of window rows [0, m)
+  uint16_t nx[kETile];       // next(a) - a of the tile's rows
+  uint16_t kl[kETile];       // their key lengths
+  uint64_t sm[kThreads / 64 + 1];
+};
+
+// The tile's window (its rows + kFuseLook lookahead rows): sizes, prefix and
+// next(a) for the tile's rows into S (okv_enc_size_next_kernel's rules).
+// Returns the tile's row count.
+__device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
+                              const uint32_t* __restrict__ val_len, uint64_t n, uint64_t T,
+                              uint64_t cs, CutSmem& S, uint64_t& mn, uint64_t& bad, uint64_t& wmax,
+                              bool& far) {
+  const uint64_t nwin = std::min<uint64_t>(n - cs, kFuseWin);
+  mn = kNone;
+  bad = kNone;
+  for (int i = 0; i < kFuseItems; ++i) {  // coalesced loads
+    const uint32_t j = i * kThreads + threadIdx.x;
+    uint64_t sz = 0;
+    if (j < nwin) {
+      const uint64_t r = cs + j;
+      const uint32_t kl = key_len[r];
+      sz = 6u + uint64_t(kl) + uint64_t(val_len[r]);
+      if (j < kETile) {
+        S.kl[j] = uint16_t(kl);
+        if (kl == 0 && r < bad) bad = r;
+        mn = sz < mn ? sz : mn;
+      }
+    }
+    S.W[j + 1] = sz;
+  }
+  __syncthreads();
+  uint64_t loc[kFuseItems], sum = 0;
+#pragma unroll
+  for (int i = 0; i < kFuseItems; ++i) {
+    sum += S.W[1 + threadIdx.x * kFuseItems + i];
+    loc[i] = sum;
+  }
+  uint64_t total;
+  const uint64_t ex = wg_excl_scan(sum, S.sm, total);
+#pragma unroll
+  for (int i = 0; i < kFuseItems; ++i) S.W[1 + threadIdx.x * kFuseItems + i] = ex + loc[i];
+  if (threadIdx.x == 0) S.W[0] = 0;
+  __syncthreads();
+  const uint32_t rows = uint32_t(std::min<uint64_t>(n - cs, kETile));
+  // next(a): first m > a - cs with W[m] >= W[a - cs] + T  (b = cs + m - 1)
+  const uint32_t M = uint32_t(nwin) + 1;
+  const bool complete = cs + nwin == n;
+  const uint32_t a0 = threadIdx.x * kEItems;
+  wmax = 0;
+  far = false;
+  uint32_t mb = 0;
+  for (int i = 0; i < kEItems; ++i) {
+    const uint32_t ar = a0 + i;
+    if (ar >= rows) break;
+    const uint64_t target = S.W[ar] + T;
+    if (i == 0) {
+      uint32_t L = ar + 1, H = M;
+      while (L < H) {
+        const uint32_t m = (L + H) >> 1;
+        if (S.W[m] >= target)
+          H = m;
+        else
+          L = m + 1;
+      }
+      mb = L;
+    } else {
+      mb = std::max(mb, ar + 1);
+      while (mb < M && S.W[mb] < target) ++mb;
+    }
+    uint32_t d;
+    if (mb < M)
+      d = mb - ar;
+    else if (complete)
+      d = uint32_t(n - cs) - ar;
+    else {
+      far = true;
+      d = 1;
+    }
+    S.nx[ar] = uint16_t(d);
+    wmax = d > wmax ? d : wmax;
+  }
+  __syncthreads();
+  return rows;
+}
+
+// E1 + E3 + E4: the level-0 chain table of each tile -- for every entry offset
+// j < kCutS, where a chain entering at row j leaves the tile (its offset into
+// the next one, <= kFuseLook) and how many blocks it starts on the way.
+__global__ __launch_bounds__(kThreads) void okv_enc_cut_kernel(
+    const uint16_t* __restrict__ key_len, const uint32_t* __restrict__ val_len, uint64_t n,
+    uint64_t T, uint32_t* __restrict__ jts, uint32_t* __restrict__ jbs,
+    EncTotals* __restrict__ tot) {
+  __shared__ CutSmem S;
+  const uint64_t cs = uint64_t(blockIdx.x) * kETile;
+  uint64_t mn, bad, wmax;
+  bool far;
+  const uint32_t rows = cut_stage(key_len, val_len, n, T, cs, S, mn, bad, wmax, far);
+  for (uint32_t j = threadIdx.x; j < kCutS; j += kThreads) {
+    uint32_t pos = j, cnt = 0;
+    while (pos < rows) {
+      pos += S.nx[pos];
+      ++cnt;
+    }
+    jts[uint64_t(blockIdx.x) * kCutS + j] = pos - rows;
+    jbs[uint64_t(blockIdx.x) * kCutS + j] = cnt;
+  }
+  mn = wave_min64(mn);
+  bad = wave_min64(bad);
+  wmax = wave_max64(wmax);
+  const bool anyfar = __any(far);
+  if ((threadIdx.x & 63) == 0) {
+    if (mn < __atomic_load_n(&tot->min_size, __ATOMIC_RELAXED))
+      atomicMin(&tot->min_size, (unsigned long long)mn);
+    if (bad != kNone) atomicMin(&tot->bad_row, (unsigned long long)bad);
+    if (wmax > __atomic_load_n(&tot->wmax, __ATOMIC_RELAXED))
+      atomicMax(&tot->wmax, (unsigned long long)wmax);
+    if (anyfar) atomicOr(&tot->far, 1ull);
+  }
+  if (threadIdx.x == 0) atomicAdd(&tot->total_raw, (unsigned long long)S.W[rows]);
+}
+
+// The level-0 table at the width the pointer doubling uses (W entries per tile).
+__global__ __launch_bounds__(kThreads) void okv_enc_restride_kernel(
+    const uint32_t* __restrict__ jts, const uint32_t* __restrict__ jbs, uint64_t nch, uint32_t W,
+    uint32_t* __restrict__ jt, uint32_t* __restrict__ jb) {
+  const uint64_t gid = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  const uint64_t c = gid / W, j = gid % W;
+  if (c >= nch) return;
+  jt[gid] = jts[c * kCutS + j];
+  jb[gid] = jbs[c * kCutS + j];
+}
+
+// E7 per tile: the chain from the tile's entry row (E6) in LDS; each block
+// started here gets its first row, OriginalSize and FirstKey length.
+__global__ __launch_bounds__(kThreads) void okv_enc_emit_tile_kernel(
+    const uint16_t* __restrict__ key_len, const uint32_t* __restrict__ val_len, uint64_t n,
+    uint64_t T, const uint32_t* __restrict__ entry, const uint64_t* __restrict__ kbase,
+    uint64_t* __restrict__ first, uint64_t* __restrict__ orig, uint16_t* __restrict__ fkl,
+    uint64_t nb, uint64_t nch, EncTotals* __restrict__ tot) {
+  __shared__ CutSmem S;
+  __shared__ uint16_t starts[kETile];
+  __shared__ uint32_t s_m;
+  const uint64_t c = blockIdx.x, cs = c * kETile;
+  uint64_t mn, bad, wmax;
+  bool far;
+  const uint32_t rows = cut_stage(key_len, val_len, n, T, cs, S, mn, bad, wmax, far);
+  if (threadIdx.x == 0) {
+    uint32_t pos = entry[c], m = 0;
+    while (pos < rows) {
+      starts[m++] = uint16_t(pos);
+      pos += S.nx[pos];
+    }
+    s_m = m;
+  }
+  __syncthreads();
+  const uint32_t m = s_m;
+  const uint64_t k0 = kbase[c];
+  if (k0 + m > nb) {
+    if (threadIdx.x == 0) tot->fault = 1;
+    return;
+  }
+  for (uint32_t i = threadIdx.x; i < m; i += kThreads) {
+    const uint32_t a = starts[i];
+    first[k0 + i] = cs + a;
+    orig[k0 + i] = S.W[a + S.nx[a]] - S.W[a];
+    fkl[k0 + i] = S.kl[a];
+  }
+  if (c == nch - 1 && threadIdx.x == 0) {
+    if (k0 + m != nb) tot->fault = 1;
     first[nb] = n;
   }
 }
@@ -565,14 +765,11 @@ __global__ __launch_bounds__(kThreads) void okv_enc_emit_kernel(
 // entry size (2 + len(FirstKey) + 40, block_stat.go:27-42) and tile scans.
 // ---------------------------------------------------------------------------
 struct StatParams {
-  const uint64_t* first;
-  const uint64_t* pl;
-  const uint64_t* tp;
-  const uint16_t* key_len;
+  const uint64_t* orig;   // [nb] OriginalSize (the emit kernels)
+  const uint16_t* fkl;    // [nb] FirstKey length
   uint64_t nb, D;
   int lz4;
   Desc* desc;
-  uint64_t* pbase;
   uint64_t* bsl;
   uint64_t* esl;
   uint64_t* btile_tot;
@@ -589,12 +786,9 @@ __global__ __launch_bounds__(kThreads) void okv_enc_stat_kernel(StatParams P) {
   for (int i = 0; i < kEItems; ++i) {
     const uint64_t k = base + i;
     if (k < P.nb) {
-      const uint64_t r0 = P.first[k], r1 = P.first[k + 1];
-      const uint64_t p0 = Pg(P.pl, P.tp, int64_t(r0) - 1);
-      const uint64_t raw = Pg(P.pl, P.tp, int64_t(r1) - 1) - p0;
-      P.pbase[k] = p0;
+      const uint64_t raw = P.orig[k];
       const uint64_t bs = (raw / P.D + 1) * P.D;
-      const uint64_t es = 42u + P.key_len[r0];
+      const uint64_t es = 42u + P.fkl[k];
       Desc d;
       d.offset = 0;
       d.block_size = bs;
@@ -677,7 +871,6 @@ struct PackParams {
   const uint64_t* tp;
   const uint64_t* first;
   const Desc* desc;
-  const uint64_t* pbase;  // [nb] P(first row - 1) (okv_enc_stat_kernel)
   uint8_t* seg;
   uint64_t* hash;  // BlockStat.Hash, written by kernels that hash in LDS
   uint8_t* meta;   // non-null: okv_enc_pack_lds_kernel also writes the blocks' meta
@@ -1528,7 +1721,8 @@ int ensure_blocks_enc(okv_ctx* ctx, EncScratch* e, uint64_t nb) {
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->bsl), c * 8))) return rc;
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->esl), c * 8))) return rc;
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->moff), c * 8))) return rc;
-    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->pbase), c * 8))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->orig), c * 8))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->fkl), c * 2))) return rc;
     e->cap_blocks = c;
   }
   if (nbt > e->cap_btiles || !e->btile) {
@@ -1586,6 +1780,16 @@ int enc_row_prefix(okv_ctx* ctx, EncScratch* e, const DevRows& R, uint64_t T) {
 #include "okv_encode_ablate_host.inc"
 #endif
 
+int ensure_cut(okv_ctx* ctx, EncScratch* e, uint64_t ntiles) {
+  int rc;
+  if (ntiles * kCutS > e->cap_cut || !e->jts) {
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->jts), ntiles * kCutS * 4))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->jbs), ntiles * kCutS * 4))) return rc;
+    e->cap_cut = ntiles * kCutS;
+  }
+  return OKV_OK;
+}
+
 // Block boundaries, BlockStat sizes/offsets and meta layout (E1-E9).
 int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opts& o, Plan* pl,
              uint64_t* bad_row) {
@@ -1593,16 +1797,25 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   const uint64_t T = o.threshold_bytes, D = o.block_size;
   const uint32_t ntiles = ceil_div(n, kETile);
   int rc;
-  if ((rc = ensure_rows(ctx, e, n))) return rc;
-  e->have_pl = true;
+  // the tile cut (E1 + E3 + E4 in LDS per tile, no per-row arrays)
+  if ((rc = ensure_cut(ctx, e, ntiles))) return rc;
+  e->have_pl = false;
   hipLaunchKernelGGL(okv_enc_init_kernel, dim3(1), dim3(1), 0, ctx->stream, e->d_tot);
-  hipLaunchKernelGGL(okv_enc_size_next_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream,
-                     R.kl, R.vl, n, T, e->pl, e->tile_tot, e->nx, e->d_tot);
-  hipLaunchKernelGGL(okv_enc_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, e->tile_tot,
-                     uint64_t(ntiles), e->tile_pre, &e->d_tot->total_raw);
+  hipLaunchKernelGGL(okv_enc_cut_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, R.kl, R.vl,
+                     n, T, e->jts, e->jbs, e->d_tot);
   OKV_HIP(hipGetLastError());
   if ((rc = read_enc_totals(ctx, e))) return rc;
-  if (e->h_tot->far) {  // some block holds more rows than the fused lookahead: E3 over global P
+  const bool tile_cut = !e->h_tot->far;
+  if (!tile_cut) {
+    // a block longer than the lookahead: the general kernels (E1-E2 over every
+    // row, E3 over the global prefix)
+    if ((rc = ensure_rows(ctx, e, n))) return rc;
+    e->have_pl = true;
+    hipLaunchKernelGGL(okv_enc_init_kernel, dim3(1), dim3(1), 0, ctx->stream, e->d_tot);
+    hipLaunchKernelGGL(okv_enc_size_next_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream,
+                       R.kl, R.vl, n, T, e->pl, e->tile_tot, e->nx, e->d_tot);
+    hipLaunchKernelGGL(okv_enc_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, e->tile_tot,
+                       uint64_t(ntiles), e->tile_pre, &e->d_tot->total_raw);
     hipLaunchKernelGGL(okv_enc_init_wmax_kernel, dim3(1), dim3(1), 0, ctx->stream, e->d_tot);
     hipLaunchKernelGGL(okv_enc_next_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, e->pl,
                        e->tile_pre, n, T, e->nx, e->d_tot);
@@ -1613,17 +1826,23 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
     *bad_row = e->h_tot->bad_row;
     return set_err(ctx, OKV_W_INVALID_KEY, "key cannot be empty (ErrInvalidKey)");
   }
-  // chunking for the chain: C >= W rows per chunk
-  const uint64_t W = std::max<uint64_t>(1, e->h_tot->wmax);
-  uint64_t C = 4096;
+  // chunking for the chain: C >= W rows per chunk (the tile cut: its tiles,
+  // entered at offsets <= kFuseLook, so its tables are at most kCutS wide)
+  const uint64_t wmax = std::max<uint64_t>(1, e->h_tot->wmax);
+  const uint64_t W = tile_cut ? std::min<uint64_t>(wmax, kCutS) : wmax;
+  uint64_t C = tile_cut ? kETile : 4096;
   while (C < W) C <<= 1;
   const uint64_t nch = (n + C - 1) / C;
   uint32_t levels = 0;
   while ((uint64_t(1) << levels) < nch) ++levels;  // 2^levels >= nch
   const uint64_t lv = nch * W;
   if ((rc = ensure_jump(ctx, e, lv * std::max<uint32_t>(levels, 1), nch))) return rc;
-  hipLaunchKernelGGL(okv_enc_jump0_kernel, dim3(ceil_div(lv, kThreads)), dim3(kThreads), 0,
-                     ctx->stream, e->nx, n, C, uint32_t(W), nch, e->jt, e->jb);
+  if (tile_cut)
+    hipLaunchKernelGGL(okv_enc_restride_kernel, dim3(ceil_div(lv, kThreads)), dim3(kThreads), 0,
+                       ctx->stream, e->jts, e->jbs, nch, uint32_t(W), e->jt, e->jb);
+  else
+    hipLaunchKernelGGL(okv_enc_jump0_kernel, dim3(ceil_div(lv, kThreads)), dim3(kThreads), 0,
+                       ctx->stream, e->nx, n, C, uint32_t(W), nch, e->jt, e->jb);
   for (uint32_t k = 1; k < levels; ++k)
     hipLaunchKernelGGL(okv_enc_jump_kernel, dim3(ceil_div(lv, kThreads)), dim3(kThreads), 0,
                        ctx->stream, e->jt + (k - 1) * lv, e->jb + (k - 1) * lv, e->jt + k * lv,
@@ -1642,18 +1861,21 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   uint64_t* bpre = e->btile + e->cap_btiles;
   uint64_t* etot = e->btile + 2 * e->cap_btiles;
   uint64_t* epre = e->btile + 3 * e->cap_btiles;
-  hipLaunchKernelGGL(okv_enc_emit_kernel, dim3(ceil_div(nch, kThreads)), dim3(kThreads), 0,
-                     ctx->stream, e->nx, n, C, nch, e->entry, e->kbase, e->first, nb, e->d_tot);
+  if (tile_cut)
+    hipLaunchKernelGGL(okv_enc_emit_tile_kernel, dim3(uint32_t(nch)), dim3(kThreads), 0,
+                       ctx->stream, R.kl, R.vl, n, T, e->entry, e->kbase, e->first, e->orig,
+                       e->fkl, nb, nch, e->d_tot);
+  else
+    hipLaunchKernelGGL(okv_enc_emit_kernel, dim3(ceil_div(nch, kThreads)), dim3(kThreads), 0,
+                       ctx->stream, e->nx, n, C, nch, e->entry, e->kbase, e->first, nb, e->pl,
+                       e->tile_pre, R.kl, e->orig, e->fkl, e->d_tot);
   StatParams sp;
-  sp.first = e->first;
-  sp.pl = e->pl;
-  sp.tp = e->tile_pre;
-  sp.key_len = R.kl;
+  sp.orig = e->orig;
+  sp.fkl = e->fkl;
   sp.nb = nb;
   sp.D = D;
   sp.lz4 = o.compression == OKV_COMP_LZ4;
   sp.desc = e->desc;
-  sp.pbase = e->pbase;
   sp.bsl = e->bsl;
   sp.esl = e->esl;
   sp.btile_tot = btot;
@@ -1742,7 +1964,6 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   pp.tp = e->tile_pre;
   pp.first = e->first;
   pp.desc = e->desc;
-  pp.pbase = e->pbase;
   pp.seg = seg;
   pp.hash = e->hash;
   pp.meta = nullptr;

@@ -372,3 +372,19 @@ def test_multi_chunk_encode(enc, T, vmax):
     # a second encode reuses the context's buffers
     got2 = enc.encode(rows, T, 4096, strict_go=strict)
     assert got2.seg.tobytes() == got.seg.tobytes()
+
+
+@pytest.mark.parametrize("T", [60, 3584, 4400, 5200, 20000])
+def test_tile_cut_boundaries_and_general_path(enc, T):
+    """The greedy cut across many 2048-row tiles (okv_enc_cut_kernel /
+    okv_enc_emit_tile_kernel): small records so blocks hold ~4, ~200, ~250,
+    ~290 (past the 256-row lookahead: the general kernels) and ~1 300 rows
+    -- every segment byte-equal to the oracle writer."""
+    rng = random.Random(T)
+    rows = [(b"%08d" % i, bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 8))))
+            for i in range(20000)]
+    rc, want, meta = oracle_segment(rows, T, 4096)
+    got = enc.encode(rows, T, 4096, strict_go=rc == 0)
+    if rc == 0:
+        assert got.seg.tobytes() == want
+        assert got.meta() == meta

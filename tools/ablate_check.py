@@ -1,6 +1,7 @@
 """Parity of the ablation arms (ablation build, OKV_ABLATE=1 with the arm's
 knob set): the arm must be the path taken and its outputs equal the oracle's.
 usage: OKV_ABLATE=1 <knob>=1 python tools/ablate_check.py stream|pieces|small_pieces|onepass
+       OKV_ABLATE=1 python tools/ablate_check.py block|block512
        OKV_ABLATE=1 python tools/ablate_check.py enc_arms   (sets each encode knob itself)"""
 import os
 import random
@@ -51,6 +52,37 @@ elif arm == "onepass":
             assert got.seg.tobytes() == want
         assert enc.last_path() & _lib.PATH_ENC_ONEPASS, enc.last_path()
     enc.close()
+elif arm in ("block", "block512"):
+    # OKV_VALUE_SWEEP=9 / 10 (set here): the one-launch per-block decode on
+    # every large-block edge shape the tests use, against the oracle
+    os.environ["OKV_VALUE_SWEEP"] = "9" if arm == "block" else "10"
+    dec = okv.Decoder(0, flags=_lib.OPEN_NO_POINT)
+    del os.environ["OKV_VALUE_SWEEP"]
+    cases = []
+    for seed in (1, 2):
+        cases.append(TD._wide_segment(seed))
+    rng = np.random.default_rng(11)
+    cases.append(TD._mixed_segment(list(rng.choice(["s", "s", "L", "M"], size=300)), 5))
+    for seed in (3, 4):
+        cases.append(TD._tiny_value_segment(seed))
+    w = okv.synth_segment(okv.sst.SYNTH_ZIPF, 7, nblocks=2000, threshold=57344, block_size=65536)
+    cases.append((w.data().tobytes(), w.descs()[:2000]))
+    # > kFastRows rows (the re-walk), a block over the 64 KiB stage (HBM walk)
+    big = bytearray()
+    for i in range(1500):
+        big += (3).to_bytes(2, "little") + (5).to_bytes(4, "little") + b"k%02d" % (i % 100) + b"vvvvv"
+    huge = bytearray()
+    for i in range(30):
+        huge += (8).to_bytes(2, "little") + (3000).to_bytes(4, "little") + b"K%07d" % i + bytes(3000)
+    seg = bytes(big) + bytes(huge)
+    d = np.array([(0, len(big), len(big), 0), (len(big), len(huge), len(huge), 0)], np.uint64)
+    cases.append((seg, d))
+    for seg, d in cases:
+        n = max(1, d.shape[0])
+        seg = bytes(seg) + bytes(max(0, 16385 * n - len(seg)) + 4096)  # large-block path
+        got = dec.decode(seg, d)
+        TD._assert_same_as_oracle(got, seg, d, 0, False)
+    dec.close()
 elif arm == "enc_arms":
     # the pack launch's variants that write whole segments (the others --
     # OKV_ENC_VARIANT 1, 2, 4, 5, 6 -- are diagnostics that skip work):

@@ -2027,15 +2027,16 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   const bool large = nblk && !fused && !stream && gather_threads(ctx, w, nblk) == 256;
 #ifdef OKV_ABLATE
   // OKV_VALUE_SWEEP=9: the one-launch per-block decode (okv_block_kernel)
-  // (10: the same with 512-thread workgroups)
-  const bool block = large && (ctx->value_sweep == 9 || ctx->value_sweep == 10) && !index_only &&
-                     !w.pre;
+  // (10: the same with 512-thread workgroups; 11: diagnostic, the prefix from
+  // okv_count_kernel instead of the look-back)
+  const bool block = large && ctx->value_sweep >= 9 && !index_only && !w.pre;
+  const bool block_diag = block && ctx->value_sweep == 11;
   const bool tile = large && !block && ctx->value_sweep >= 8;
   const bool sweep = large && !tile && !block && ctx->value_sweep && !index_only &&
                      ctx->gather_staged && o->row_cap < (uint64_t(1) << 32);
 #else
   const bool tile = large;  // the product: okv_tile_kernel for every large-block decode
-  constexpr bool sweep = false, block = false;
+  constexpr bool sweep = false, block = false, block_diag = false;
 #endif
   const TileGeo geo = tile ? tile_geo(ctx, w, nblk, index_only) : TileGeo{1, ~0ull};
   ctx->span_hint = SpanHint{};  // a plan's hint sizes the one decode that follows it
@@ -2058,7 +2059,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
                                         ~uint32_t(kTile - 1));
   if (spn >= nblk) spn = 0;
 #endif
-  if (fused || stream || block) {
+  if (fused || stream || (block && !block_diag)) {
     if ((rc = ensure_fused(ctx, nblk))) return rc;
     prof_mark(ctx, 2);
     prof_mark(ctx, 3);
@@ -2136,6 +2137,12 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
     OKV_HIP(hipStreamWaitEvent(ctx->stream, ctx->chain->p3_done, 0));
   if (nblk) {
     const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
+#ifdef OKV_ABLATE
+    if (block_diag) {
+      hipLaunchKernelGGL((okv_block_kernel<1024, false>), dim3(nblk), dim3(1024), 0, ctx->stream, P,
+                         FusedParams{});
+    } else
+#endif
     if (fused || stream || block) {
       FusedParams F;
       F.pre = w.pre;
@@ -2565,7 +2572,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   if (const char* v = getenv("OKV_GATHER_STAGED")) ctx->gather_staged = atoi(v) != 0;
   if (const char* v = getenv("OKV_VALUE_SWEEP")) {
     ctx->value_sweep = uint32_t(atoi(v));
-    if (ctx->value_sweep > 10 || ctx->value_sweep == 3) {
+    if (ctx->value_sweep > 11 || ctx->value_sweep == 3) {
       delete ctx;
       return nullptr;
     }

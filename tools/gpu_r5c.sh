@@ -9,5 +9,5 @@ for a in block block512; do
   OKV_ABLATE=1 timeout -k 10 300 python3 tools/ablate_check.py $a > $O/check_$a.log 2>&1
   rc=$?; tail -2 $O/check_$a.log; [ $rc -ne 0 ] && exit $rc
 done
-OKV_ABLATE=1 ABL_VERIFY=1 ABL_ROUNDS=5 timeout -k 10 400 python3 tools/ablate_tile.py 8:16x 9 10 > $O/block_ab.log 2>&1
+OKV_ABLATE=1 ABL_VERIFY=1 ABL_ROUNDS=5 timeout -k 10 400 python3 tools/ablate_tile.py 8:16x 9 10 11 > $O/block_ab.log 2>&1
 rc=$?; tail -8 $O/block_ab.log; exit $rc

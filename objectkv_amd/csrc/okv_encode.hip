@@ -1898,7 +1898,7 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   pl->meta_bytes = e->h_tot->head + e->h_tot->meta_ent;
   pl->file_bytes = pl->data_bytes + pl->meta_bytes + 25;
   pl->last_raw = e->h_tot->last_raw;
-  pl->w = W;
+  pl->w = wmax;  // (the chain tables above are capped at kCutS; blocks are not)
   pl->bmax = e->h_tot->bmax;
   pl->avg_rec = e->h_tot->total_raw / n;
   return OKV_OK;

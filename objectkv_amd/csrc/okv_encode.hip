@@ -1930,17 +1930,22 @@ int enc_pack(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
     *hashed = true;
     return OKV_OK;
   }
+  // the other kernels read the row prefix: computed here (the tile cut writes
+  // none), so the parameters take its buffers after the call
   if ((rc = enc_row_prefix(ctx, e, R, o.threshold_bytes))) return rc;
+  PackParams q = pp;
+  q.pl = e->pl;
+  q.tp = e->tile_pre;
   if (aligned && G >= 1) {  // large records: chunk-major regions
     hipLaunchKernelGGL(okv_enc_pack_region_kernel<0>, dim3(ceil_div(pl.nb, G)), dim3(kThreads), 0,
-                       ctx->stream, pp, pl.nb, uint32_t(G));
+                       ctx->stream, q, pl.nb, uint32_t(G));
   } else if (aligned) {
     hipLaunchKernelGGL(okv_enc_pack_kernel, dim3(uint32_t(pl.nb)), dim3(kThreads), 0,
-                       ctx->stream, pp);
+                       ctx->stream, q);
   } else {
     const uint32_t g = std::min<uint64_t>(65536, (pl.data_bytes + kThreads - 1) / kThreads);
     hipLaunchKernelGGL(okv_enc_pack_bytes_kernel, dim3(std::max<uint32_t>(g, 1)),
-                       dim3(kThreads), 0, ctx->stream, pp, pl.nb, pl.data_bytes);
+                       dim3(kThreads), 0, ctx->stream, q, pl.nb, pl.data_bytes);
   }
   return OKV_OK;
 }
@@ -1960,7 +1965,7 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   pp.val_arena = R.va;
   pp.val_off = R.vo;
   pp.val_len = R.vl;
-  pp.pl = e->pl;
+  pp.pl = e->pl;  // (null until the row prefix is computed: enc_pack / the ablation arms)
   pp.tp = e->tile_pre;
   pp.first = e->first;
   pp.desc = e->desc;

@@ -11,8 +11,11 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # The product library; OKV_ABLATE=1 loads the ablation build instead (the
-# measured alternative kernel forms and their OKV_* knobs, tools/ablate*.py).
+# measured alternative kernel forms and their OKV_* knobs, tools/ablate*.py);
+# OKV_ZTRACE=1 the product configuration with the zstd exit-line recorder
+# (`make ztrace`).
 LIB_PATH = os.path.join(_HERE, "libokv_sst_ablate.so" if os.environ.get("OKV_ABLATE") == "1"
+                        else "libokv_sst_ztrace.so" if os.environ.get("OKV_ZTRACE") == "1"
                         else "libokv_sst.so")
 
 # ---- constants (include/okv_sst.h) -------------------------------------------

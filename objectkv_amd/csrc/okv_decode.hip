@@ -235,13 +235,14 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
     lp[b] = e;
   }
   // Pass 2 in the same launch: the workgroup whose arrival is counted last
-  // scans the tile totals.  Hand-off: one lane per workgroup stores its totals
-  // with sc1 stores, drains them, then adds to one counter with release
-  // semantics; the last adder (told by the value its add returns) issues an
-  // agent-scope acquire and reads every total with sc1 loads.  (The sc1 form
-  // alone is the measured-valid row 1 of MI355X_MICROARCH.md's hand-off table;
-  // the release/acquire pair makes the ordering the memory model's, at one
-  // L2 write-back per workgroup and one invalidate in the last.)
+  // scans the tile totals.  Hand-off (MI355X_MICROARCH.md, inter-workgroup
+  // hand-off table, row 1): one lane per workgroup stores its totals with sc1
+  // stores, drains them (vmcnt(0)), then adds to one unsharded agent-scope
+  // counter; the workgroup whose add came last (told by the value it returns)
+  // reads every total with sc1 loads.  Round 4 made the add a release and
+  // the last adder acquire: an L2 write-back per workgroup of the ~66 KB of
+  // record table each has just written -- 6.5 us more per C3 count (A/B,
+  // profiles/r5/session/ab_count_arrival.log), and not needed by this row.
   __shared__ uint32_t s_last;
   if (tid == kThreads - 1) {
     const Prefix t{inc[0] + v[0], inc[1] + v[1], inc[2] + v[2], inc[3] + v[3]};
@@ -258,19 +259,9 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
       __hip_atomic_store(&q->vb, t.vb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&q->bad, t.bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef OKV_COUNT_ARRIVE_RELAXED
       const uint32_t a =
           __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       s_last = a == gridDim.x - 1;
-#else
-      const uint32_t a =
-          __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = a == gridDim.x - 1;
-      if (s_last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-#endif
     }
   }
   __syncthreads();
@@ -1538,6 +1529,7 @@ __global__ __launch_bounds__(kThreads) void okv_copy_kernel(CopyParams P) {
 __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Totals* tot) {
   __shared__ CopySmem sm;
   __shared__ uint64_t s_walk[4];  // rows, key bytes, value bytes, walk end
+  __shared__ uint32_t s_wsum[2][kThreads / 64];
   __shared__ int32_t s_st;
   const uint32_t tid = threadIdx.x;
   const uint32_t* sw = reinterpret_cast<const uint32_t*>(sm.stage);
@@ -1548,43 +1540,42 @@ __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Total
     const uint64_t len = P.comp == OKV_COMP_LZ4 ? 0 : d.block_size;  // Q7 (:331-333)
     const uint32_t shift = uint32_t(d.offset & 15);
     if (st0 == OKV_BLK_OK && len) {  // stage [offset - shift, offset + len): one trip
+      // (LDS DMA: every 16-byte piece in flight at once -- a load/store loop
+      // paid one PCIe round trip per iteration, ~16 for a 64 KiB block)
       const uint32_t nch = uint32_t((shift + len + 15) >> 4);
-      const uint4* g = reinterpret_cast<const uint4*>(P.seg + (d.offset - shift));
-      for (uint32_t ci = tid; ci < nch; ci += kThreads) sm.stage[1 + ci] = g[ci];
+      const uint8_t* g = P.seg + (d.offset - shift);
+      const uint32_t lane = tid & 63, wave = tid >> 6;
+      for (uint32_t c0 = wave * 64; c0 < nch; c0 += kThreads) {
+        if (c0 + lane < nch)  // (an inactive lane writes no LDS)
+          __builtin_amdgcn_global_load_lds(g + 16ull * (c0 + lane), OKV_LDS_PTR(sm.stage + 1 + c0),
+                                           16, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    const uint32_t bias = 16u + shift;
     if (tid == 0) {
+      // the header walk (Go's checks in its order), as short a dependent chain
+      // as it can be: record positions only -- the key / value prefixes follow
+      // in parallel from the recorded headers
       int32_t st = st0;
-      uint64_t rows = 0, kb = 0, vb = 0, p = 0;
+      uint32_t rows = 0, p = 0;
       if (st == OKV_BLK_OK) {
         const uint64_t orig = go_walk_bound(d.original_size);  // int(OriginalSize) (:340)
-        const uint32_t bias = 16u + shift;
-        while (p < orig) {                                    // :340
-          if (len - p < 6) { st = OKV_BLK_PANIC; break; }     // u16/u32 reads (:342-345)
+        const uint32_t L = uint32_t(len);                      // <= kStage
+        while (p < orig) {                                     // :340
+          if (L - p < 6) { st = OKV_BLK_PANIC; break; }        // u16/u32 reads (:342-345)
           uint32_t kl, vl;
-          header_lds(sw, bias + uint32_t(p), kl, vl);
-          const uint64_t room = len - p - 6;
+          header_lds(sw, bias + p, kl, vl);
+          const uint32_t room = L - p - 6;
           if (kl > room || vl > room - kl) { st = OKV_BLK_PANIC; break; }  // :346-349
-          if (rows < uint64_t(kFastRows)) {
-            sm.f.rec[rows] = uint32_t(p);
-            sm.f.kpre[rows] = uint32_t(kb);
-            sm.f.vpre[rows] = uint32_t(vb);
-          }
-          rows++;
-          kb += kl;
-          vb += vl;
-          p += 6 + uint64_t(kl) + uint64_t(vl);
-        }
-        if (st == OKV_BLK_OK && rows <= uint64_t(kFastRows)) {
-          sm.f.rec[rows] = uint32_t(p);
-          sm.f.kpre[rows] = uint32_t(kb);
-          sm.f.vpre[rows] = uint32_t(vb);
+          if (rows < uint32_t(kFastRows)) sm.f.rec[rows] = p;
+          ++rows;
+          p += 6 + kl + vl;
         }
       }
-      if (st != OKV_BLK_OK) rows = kb = vb = p = 0;  // a failed block has no rows
+      if (st != OKV_BLK_OK) rows = p = 0;  // a failed block has no rows
       s_walk[0] = rows;
-      s_walk[1] = kb;
-      s_walk[2] = vb;
       s_walk[3] = p;
       s_st = st;
       P.row_start[b] = row0;
@@ -1593,13 +1584,76 @@ __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Total
       P.blk_status[b] = st;
     }
     __syncthreads();
-    const uint64_t rows = s_walk[0], kb = s_walk[1], vb = s_walk[2], pend = s_walk[3];
+    const uint64_t rows = s_walk[0], pend = s_walk[3];
     const int32_t st = s_st;
+    uint64_t kb = 0, vb = 0;
     if (st == OKV_BLK_OK && rows) {
       if (rows <= uint64_t(kFastRows)) {
-        emit_fast<3>(P, sm, 16u + shift, int(rows), kb, vb, row0, kb0, vb0);
+        // key / value lengths of the recorded rows, exclusive prefixes (4 rows a lane)
+        constexpr int kPer = kFastRows / kThreads;
+        uint32_t kls[kPer], vls[kPer], ks = 0, vs = 0;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          const uint32_t i = tid * kPer + j;
+          kls[j] = vls[j] = 0;
+          if (i < rows) header_lds(sw, bias + sm.f.rec[i], kls[j], vls[j]);
+          ks += kls[j];
+          vs += vls[j];
+        }
+        const uint32_t ki = wave_scan_dpp(ks), vi = wave_scan_dpp(vs);
+        const uint32_t wave = tid >> 6;
+        if ((tid & 63) == 63) {
+          s_wsum[0][wave] = ki;
+          s_wsum[1][wave] = vi;
+        }
+        __syncthreads();
+        uint32_t kx = ki - ks, vx = vi - vs;
+        uint32_t ktot = 0, vtot = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kThreads / 64; ++w) {
+          kx += w < wave ? s_wsum[0][w] : 0u;
+          vx += w < wave ? s_wsum[1][w] : 0u;
+          ktot += s_wsum[0][w];
+          vtot += s_wsum[1][w];
+        }
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          const uint32_t i = tid * kPer + j;
+          if (i < rows) {
+            sm.f.kpre[i] = kx;
+            sm.f.vpre[i] = vx;
+          }
+          kx += kls[j];
+          vx += vls[j];
+        }
+        if (tid == 0) {
+          sm.f.rec[rows] = uint32_t(pend);
+          sm.f.kpre[rows] = ktot;
+          sm.f.vpre[rows] = vtot;
+        }
+        kb = ktot;
+        vb = vtot;
+        __syncthreads();
+        emit_fast<3>(P, sm, bias, int(rows), kb, vb, row0, kb0, vb0);
       } else {
-        LdsSrc src{sw, 16u + shift};
+        // more rows than the row table holds: the byte totals by a second
+        // walk (the block passed its checks), then the batched row tables
+        if (tid == 0) {
+          uint64_t k = 0, v = 0;
+          for (uint32_t q = 0; q < uint32_t(pend);) {
+            uint32_t kl, vl;
+            header_lds(sw, bias + q, kl, vl);
+            k += kl;
+            v += vl;
+            q += 6 + kl + vl;
+          }
+          s_walk[1] = k;
+          s_walk[2] = v;
+        }
+        __syncthreads();
+        kb = s_walk[1];
+        vb = s_walk[2];
+        LdsSrc src{sw, bias};
         materialise<3>(src, P, sm, rows, kb, vb, row0, kb0, vb0, pend);
       }
     }

@@ -379,6 +379,34 @@ __global__ __launch_bounds__(1024) void okv_enc_scan_kernel(const uint64_t* __re
   if (threadIdx.x == 0 && total) *total = carry;
 }
 
+// The sum of n u64 values (one workgroup; loads unrolled so they overlap --
+// okv_enc_scan_kernel's carried chunks took 88 us over C4's 48 828 tiles).
+__global__ __launch_bounds__(1024) void okv_enc_sum_kernel(const uint64_t* __restrict__ in,
+                                                           uint64_t n,
+                                                           unsigned long long* __restrict__ total) {
+  __shared__ uint64_t sm[16];
+  uint64_t acc = 0;
+  for (uint64_t b = 0; b < n; b += 8 * 1024) {
+    uint64_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint64_t i = b + u * 1024 + threadIdx.x;
+      v[u] = i < n ? in[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  acc = wave_sum64_u(acc);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += sm[w];
+    *total = t;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // E3: next(a) = 1 + min{b >= a : P(b) >= P(a-1) + T}, or n if none
 // (WriteRow's `blockBuffer.Len() >= DataBlockThresholdBytes`, :138).
@@ -585,11 +613,49 @@ __global__ __launch_bounds__(kThreads) void okv_enc_emit_kernel(
 constexpr uint32_t kCutS = kFuseLook + 1;  // entry offsets into a tile: chains enter at <= kFuseLook
 
 struct CutSmem {
-  uint64_t W[kFuseWin + 1];  // W[m] = record bytes of window rows [0, m)
-  uint16_t nx[kETile];       // next(a) - a of the tile's rows
-  uint16_t kl[kETile];       // their key lengths
+  union {
+    uint32_t W[kFuseWin + 1];  // W[m] = record bytes of window rows [0, m) (a window of
+                               // 2^32 bytes or more: tot->far, the general kernels)
+    struct {                   // okv_enc_cut_kernel, once next(a) is known
+      uint16_t nx4[kETile];    // four blocks on (kNoJump: the chain leaves the tile first)
+      uint32_t ex[kCutS];      // per entry: exit offset, blocks started
+      uint32_t nb[kCutS];
+    } c;
+  };
+  uint16_t nx[kETile];  // next(a) - a of the tile's rows
+  union {
+    uint16_t kl[kETile];   // their key lengths (okv_enc_emit_tile_kernel)
+    uint16_t nx2[kETile];  // two blocks on (okv_enc_cut_kernel)
+  };
   uint64_t sm[kThreads / 64 + 1];
 };
+static_assert(sizeof(uint16_t) * kETile + 8 * kCutS <= sizeof(uint32_t) * (kFuseWin + 1),
+              "cut tables fit the prefix's LDS");
+constexpr uint16_t kNoJump = 0xffff;
+
+// nx2 / nx4: where the chain from row a is two / four blocks on, when every
+// block of those starts inside the tile (else kNoJump).  A chain walk then
+// takes four blocks per dependent LDS read (49 -> ~15 reads at C4's 42-row blocks).
+__device__ __forceinline__ void cut_jumps(CutSmem& S, uint32_t rows) {
+  for (int i = 0; i < kEItems; ++i) {
+    const uint32_t a = i * kThreads + threadIdx.x;
+    if (a < rows) {
+      const uint32_t b = a + S.nx[a];
+      S.nx2[a] = b < rows ? uint16_t(b - a + S.nx[b]) : kNoJump;
+    }
+  }
+  __syncthreads();
+  for (int i = 0; i < kEItems; ++i) {
+    const uint32_t a = i * kThreads + threadIdx.x;
+    if (a < rows) {
+      const uint32_t x = S.nx2[a];
+      const uint32_t c = a + x;
+      S.c.nx4[a] = x != kNoJump && c < rows && S.nx2[c] != kNoJump ? uint16_t(x + S.nx2[c])
+                                                                  : kNoJump;
+    }
+  }
+  __syncthreads();
+}
 
 // The tile's window (its rows + kFuseLook lookahead rows): sizes, prefix and
 // next(a) for the tile's rows into S (okv_enc_size_next_kernel's rules).
@@ -601,6 +667,7 @@ __device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
   const uint64_t nwin = std::min<uint64_t>(n - cs, kFuseWin);
   mn = kNone;
   bad = kNone;
+  bool wide = false;
   for (int i = 0; i < kFuseItems; ++i) {  // coalesced loads
     const uint32_t j = i * kThreads + threadIdx.x;
     uint64_t sz = 0;
@@ -613,10 +680,11 @@ __device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
         if (kl == 0 && r < bad) bad = r;
         mn = sz < mn ? sz : mn;
       }
+      wide |= sz > 0xffffffffull;
     }
-    S.W[j + 1] = sz;
+    S.W[j + 1] = uint32_t(sz);
   }
-  __syncthreads();
+  wide = __syncthreads_or(wide);
   uint64_t loc[kFuseItems], sum = 0;
 #pragma unroll
   for (int i = 0; i < kFuseItems; ++i) {
@@ -626,10 +694,11 @@ __device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
   uint64_t total;
   const uint64_t ex = wg_excl_scan(sum, S.sm, total);
 #pragma unroll
-  for (int i = 0; i < kFuseItems; ++i) S.W[1 + threadIdx.x * kFuseItems + i] = ex + loc[i];
+  for (int i = 0; i < kFuseItems; ++i) S.W[1 + threadIdx.x * kFuseItems + i] = uint32_t(ex + loc[i]);
   if (threadIdx.x == 0) S.W[0] = 0;
   __syncthreads();
   const uint32_t rows = uint32_t(std::min<uint64_t>(n - cs, kETile));
+  wide |= (total >> 32) != 0;
   // next(a): first m > a - cs with W[m] >= W[a - cs] + T  (b = cs + m - 1)
   const uint32_t M = uint32_t(nwin) + 1;
   const bool complete = cs + nwin == n;
@@ -640,12 +709,12 @@ __device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
   for (int i = 0; i < kEItems; ++i) {
     const uint32_t ar = a0 + i;
     if (ar >= rows) break;
-    const uint64_t target = S.W[ar] + T;
+    const uint64_t target = uint64_t(S.W[ar]) + T;
     if (i == 0) {
       uint32_t L = ar + 1, H = M;
       while (L < H) {
         const uint32_t m = (L + H) >> 1;
-        if (S.W[m] >= target)
+        if (uint64_t(S.W[m]) >= target)
           H = m;
         else
           L = m + 1;
@@ -653,7 +722,7 @@ __device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
       mb = L;
     } else {
       mb = std::max(mb, ar + 1);
-      while (mb < M && S.W[mb] < target) ++mb;
+      while (mb < M && uint64_t(S.W[mb]) < target) ++mb;
     }
     uint32_t d;
     if (mb < M)
@@ -667,6 +736,7 @@ __device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
     S.nx[ar] = uint16_t(d);
     wmax = d > wmax ? d : wmax;
   }
+  far |= wide;
   __syncthreads();
   return rows;
 }
@@ -677,20 +747,51 @@ __device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
 __global__ __launch_bounds__(kThreads) void okv_enc_cut_kernel(
     const uint16_t* __restrict__ key_len, const uint32_t* __restrict__ val_len, uint64_t n,
     uint64_t T, uint32_t* __restrict__ jts, uint32_t* __restrict__ jbs,
-    EncTotals* __restrict__ tot) {
+    uint64_t* __restrict__ tile_raw, EncTotals* __restrict__ tot) {
   __shared__ CutSmem S;
   const uint64_t cs = uint64_t(blockIdx.x) * kETile;
   uint64_t mn, bad, wmax;
   bool far;
   const uint32_t rows = cut_stage(key_len, val_len, n, T, cs, S, mn, bad, wmax, far);
-  for (uint32_t j = threadIdx.x; j < kCutS; j += kThreads) {
+  const uint32_t w_rows = S.W[rows];  // (before the jump tables overwrite W)
+  __syncthreads();
+  cut_jumps(S, rows);
+  // entries 1..256, one lane each; entry 0 enters the chain of entry nx[0]
+  {
+    const uint32_t j = threadIdx.x + 1;
     uint32_t pos = j, cnt = 0;
     while (pos < rows) {
-      pos += S.nx[pos];
-      ++cnt;
+      const uint32_t j4 = S.c.nx4[pos], j1 = S.nx[pos];
+      const bool four = j4 != kNoJump;
+      pos += four ? j4 : j1;
+      cnt += four ? 4u : 1u;
     }
-    jts[uint64_t(blockIdx.x) * kCutS + j] = pos - rows;
-    jbs[uint64_t(blockIdx.x) * kCutS + j] = cnt;
+    S.c.ex[j] = pos - rows;
+    S.c.nb[j] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t pos = 0, cnt = 0;
+    if (rows) {
+      pos = S.nx[0];
+      cnt = 1;
+      if (pos < rows && pos < kCutS) {
+        cnt += S.c.nb[pos];
+        pos = rows + S.c.ex[pos];
+      } else {
+        while (pos < rows) {
+          pos += S.nx[pos];
+          ++cnt;
+        }
+      }
+    }
+    S.c.ex[0] = pos - rows;
+    S.c.nb[0] = cnt;
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < kCutS; j += kThreads) {
+    jts[uint64_t(blockIdx.x) * kCutS + j] = S.c.ex[j];
+    jbs[uint64_t(blockIdx.x) * kCutS + j] = S.c.nb[j];
   }
   mn = wave_min64(mn);
   bad = wave_min64(bad);
@@ -704,7 +805,9 @@ __global__ __launch_bounds__(kThreads) void okv_enc_cut_kernel(
       atomicMax(&tot->wmax, (unsigned long long)wmax);
     if (anyfar) atomicOr(&tot->far, 1ull);
   }
-  if (threadIdx.x == 0) atomicAdd(&tot->total_raw, (unsigned long long)S.W[rows]);
+  // (the tiles' record bytes are summed by okv_enc_scan_kernel: one atomic add
+  // per workgroup on one word cost 1.7 ms of C4's 2.1 ms cut launch)
+  if (threadIdx.x == 0) tile_raw[blockIdx.x] = w_rows;
 }
 
 // The level-0 table at the width the pointer doubling uses (W entries per tile).
@@ -726,19 +829,57 @@ __global__ __launch_bounds__(kThreads) void okv_enc_emit_tile_kernel(
     uint64_t* __restrict__ first, uint64_t* __restrict__ orig, uint16_t* __restrict__ fkl,
     uint64_t nb, uint64_t nch, EncTotals* __restrict__ tot) {
   __shared__ CutSmem S;
-  __shared__ uint16_t starts[kETile];
-  __shared__ uint32_t s_m;
+  __shared__ uint16_t starts[kETile];  // (first the two-block table)
+  __shared__ uint16_t nx4[kETile];
+  __shared__ uint16_t coarse[kETile / 4 + 1];
+  __shared__ uint32_t s_m, s_q;
   const uint64_t c = blockIdx.x, cs = c * kETile;
   uint64_t mn, bad, wmax;
   bool far;
   const uint32_t rows = cut_stage(key_len, val_len, n, T, cs, S, mn, bad, wmax, far);
+  // the jump tables (cut_jumps' rules; nx2 held in `starts` until the walk)
+  uint16_t* nx2 = starts;
+  for (int i = 0; i < kEItems; ++i) {
+    const uint32_t a = i * kThreads + threadIdx.x;
+    if (a < rows) {
+      const uint32_t b = a + S.nx[a];
+      nx2[a] = b < rows ? uint16_t(b - a + S.nx[b]) : kNoJump;
+    }
+  }
+  __syncthreads();
+  for (int i = 0; i < kEItems; ++i) {
+    const uint32_t a = i * kThreads + threadIdx.x;
+    if (a < rows) {
+      const uint32_t x = nx2[a];
+      const uint32_t q = a + x;
+      nx4[a] = x != kNoJump && q < rows && nx2[q] != kNoJump ? uint16_t(x + nx2[q]) : kNoJump;
+    }
+  }
+  __syncthreads();
+  // lane 0: the chain from the entry row four blocks a step (the last <= 3
+  // blocks one at a time); then lane i expands the i-th four-block step
   if (threadIdx.x == 0) {
-    uint32_t pos = entry[c], m = 0;
+    uint32_t pos = entry[c], q = 0, m = 0;
+    while (pos < rows && nx4[pos] != kNoJump) {
+      coarse[q++] = uint16_t(pos);
+      pos += nx4[pos];
+    }
+    m = 4 * q;
     while (pos < rows) {
       starts[m++] = uint16_t(pos);
       pos += S.nx[pos];
     }
     s_m = m;
+    s_q = q;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < s_q; i += kThreads) {
+    uint32_t pos = coarse[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      starts[4 * i + k] = uint16_t(pos);
+      pos += S.nx[pos];
+    }
   }
   __syncthreads();
   const uint32_t m = s_m;
@@ -1679,6 +1820,17 @@ int enc_scratch(okv_ctx* ctx, EncScratch** out) {
   return OKV_OK;
 }
 
+int ensure_tiles(okv_ctx* ctx, EncScratch* e, uint64_t n) {
+  const uint64_t nt = (n + kETile - 1) / kETile + 1;
+  int rc;
+  if (nt > e->cap_tiles || !e->tile_tot) {
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->tile_tot), nt * 8))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->tile_pre), nt * 8))) return rc;
+    e->cap_tiles = nt;
+  }
+  return OKV_OK;
+}
+
 int ensure_rows(okv_ctx* ctx, EncScratch* e, uint64_t n) {
   const uint64_t nt = (n + kETile - 1) / kETile + 1;
   int rc;
@@ -1798,11 +1950,13 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   const uint32_t ntiles = ceil_div(n, kETile);
   int rc;
   // the tile cut (E1 + E3 + E4 in LDS per tile, no per-row arrays)
-  if ((rc = ensure_cut(ctx, e, ntiles))) return rc;
+  if ((rc = ensure_cut(ctx, e, ntiles)) || (rc = ensure_tiles(ctx, e, n))) return rc;
   e->have_pl = false;
   hipLaunchKernelGGL(okv_enc_init_kernel, dim3(1), dim3(1), 0, ctx->stream, e->d_tot);
   hipLaunchKernelGGL(okv_enc_cut_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream, R.kl, R.vl,
-                     n, T, e->jts, e->jbs, e->d_tot);
+                     n, T, e->jts, e->jbs, e->tile_tot, e->d_tot);
+  hipLaunchKernelGGL(okv_enc_sum_kernel, dim3(1), dim3(1024), 0, ctx->stream, e->tile_tot,
+                     uint64_t(ntiles), &e->d_tot->total_raw);
   OKV_HIP(hipGetLastError());
   if ((rc = read_enc_totals(ctx, e))) return rc;
   const bool tile_cut = !e->h_tot->far;

@@ -1526,15 +1526,50 @@ __global__ __launch_bounds__(kThreads) void okv_copy_kernel(CopyParams P) {
 // blocks of more than kFastRows rows re-walk in batches, materialise).  The
 // host admits only batches whose OK blocks stage (BlockSize <= kStage).
 // ---------------------------------------------------------------------------
+constexpr uint32_t kPointWin = 8192;  // hop-table window (byte positions)
+constexpr uint16_t kBadHop = 0xffff;
+// Hop lengths from byte position q < L of a staged block: h1 = the record at
+// q's length - 6, h2 = that record's and the next one's - 12, kBadHop where
+// Go's checks (:342-349) fail at q (h1) or at either record (h2).  Branch-free:
+// header reads past the block end stay inside the stage's guard.
+__device__ __forceinline__ void point_hops(const uint32_t* sw, uint32_t bias, uint32_t L,
+                                           uint32_t q, uint16_t& h1, uint16_t& h2) {
+  uint32_t kl, vl;
+  header_lds(sw, bias + q, kl, vl);
+  const uint32_t room = L - q - 6;
+  const bool ok1 = (L - q >= 6) & (kl <= room) & (vl <= room - kl);
+  const uint32_t len = ok1 ? 6 + kl + vl : 0u;
+  const uint32_t q1 = q + len;  // <= L
+  uint32_t kl1, vl1;
+  header_lds(sw, bias + q1, kl1, vl1);
+  const uint32_t room1 = L - q1 - 6;
+  const bool ok2 = ok1 & (L - q1 >= 6) & (kl1 <= room1) & (vl1 <= room1 - kl1);
+  h1 = ok1 ? uint16_t(len - 6) : kBadHop;
+  h2 = ok2 ? uint16_t(len + kl1 + vl1 - 6) : kBadHop;
+}
+
+#ifdef OKV_ABLATE
+// (ablation build: wall-clock stamps of the point kernel's phases for the
+// last block of the last call -- start, staged, walked, prefixes, emitted;
+// okv_debug_point_times, tools/point_phases.py)
+__device__ uint64_t g_point_t[8];
+#define OKV_POINT_STAMP(i) \
+  if (tid == 0) g_point_t[i] = wall_clock64()
+#else
+#define OKV_POINT_STAMP(i)
+#endif
 __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Totals* tot) {
   __shared__ CopySmem sm;
   __shared__ uint64_t s_walk[4];  // rows, key bytes, value bytes, walk end
   __shared__ uint32_t s_wsum[2][kThreads / 64];
-  __shared__ int32_t s_st;
+  __shared__ int32_t s_st, s_pst;
+  __shared__ uint32_t s_pw[3];
+  __shared__ uint16_t s_hop1[2][kPointWin], s_hop2[2][kPointWin];
   const uint32_t tid = threadIdx.x;
   const uint32_t* sw = reinterpret_cast<const uint32_t*>(sm.stage);
   uint64_t row0 = 0, kb0 = 0, vb0 = 0, bad = 0;  // exclusive prefixes (uniform)
   for (uint32_t b = 0; b < P.nblk; ++b) {
+    OKV_POINT_STAMP(0);
     const Desc d = P.descs[b];
     const int32_t st0 = go_read_status(d, P.seg_bytes);  // :303-316
     const uint64_t len = P.comp == OKV_COMP_LZ4 ? 0 : d.block_size;  // Q7 (:331-333)
@@ -1553,27 +1588,64 @@ __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Total
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    OKV_POINT_STAMP(1);
     const uint32_t bias = 16u + shift;
+    // The header walk (Go's checks in its order) with the hop table: for every
+    // byte position q of an 8 KiB window, the length of the record at q and of
+    // the two records from q (or kBadHop where Go's checks fail), computed by
+    // all lanes; lane 0 then walks the window two records per LDS read while
+    // waves 1-3 fill the next window's table into the other slot.  (Lane 0
+    // alone, one dependent header decode per record: 120 ns a record, 80 us
+    // of a 64 KiB block's 116 us GetRow.)
+    const uint32_t L = st0 == OKV_BLK_OK ? uint32_t(len) : 0u;  // <= kStage
+    const uint64_t orig = go_walk_bound(d.original_size);       // int(OriginalSize) (:340)
+    const uint32_t nwin = (L + kPointWin - 1) / kPointWin;
     if (tid == 0) {
-      // the header walk (Go's checks in its order), as short a dependent chain
-      // as it can be: record positions only -- the key / value prefixes follow
-      // in parallel from the recorded headers
-      int32_t st = st0;
-      uint32_t rows = 0, p = 0;
-      if (st == OKV_BLK_OK) {
-        const uint64_t orig = go_walk_bound(d.original_size);  // int(OriginalSize) (:340)
-        const uint32_t L = uint32_t(len);                      // <= kStage
-        while (p < orig) {                                     // :340
-          if (L - p < 6) { st = OKV_BLK_PANIC; break; }        // u16/u32 reads (:342-345)
-          uint32_t kl, vl;
-          header_lds(sw, bias + p, kl, vl);
-          const uint32_t room = L - p - 6;
-          if (kl > room || vl > room - kl) { st = OKV_BLK_PANIC; break; }  // :346-349
-          if (rows < uint32_t(kFastRows)) sm.f.rec[rows] = p;
+      s_pw[0] = 0;          // position
+      s_pw[1] = 0;          // rows
+      s_pw[2] = orig == 0;  // done
+      s_pst = st0;
+    }
+    for (uint32_t q = tid; q < min(L, kPointWin); q += kThreads)
+      point_hops(sw, bias, L, q, s_hop1[0][q], s_hop2[0][q]);
+    __syncthreads();
+    for (uint32_t k = 0; k < nwin; ++k) {
+      const uint32_t wb = k * kPointWin, we = min(L, wb + kPointWin);
+      if (tid == 0 && !s_pw[2]) {
+        const uint16_t* h1 = s_hop1[k & 1];
+        const uint16_t* h2 = s_hop2[k & 1];
+        uint32_t p = s_pw[0], rows = s_pw[1];
+        bool done = false;
+        while (p < we) {  // (p < orig: checked per record)
+          if (p >= orig) { done = true; break; }
+          const uint32_t a1 = h1[p - wb], a2 = h2[p - wb];
+          if (a1 == kBadHop) { s_pst = OKV_BLK_PANIC; done = true; break; }  // :342-349
+          sm.f.rec[min(rows, uint32_t(kFastRows))] = p;
           ++rows;
-          p += 6 + kl + vl;
+          const uint32_t p1 = p + 6 + a1;
+          if (p1 < orig && a2 != kBadHop) {
+            sm.f.rec[min(rows, uint32_t(kFastRows))] = p1;
+            ++rows;
+            p += 12 + a2;
+          } else {
+            p = p1;
+          }
         }
+        s_pw[0] = p;
+        s_pw[1] = rows;
+        s_pw[2] = done;
+      } else if (tid >= 64 && k + 1 < nwin) {
+        const uint32_t nb0 = wb + kPointWin, ne = min(L, nb0 + kPointWin);
+        for (uint32_t q = nb0 + tid - 64; q < ne; q += kThreads - 64)
+          point_hops(sw, bias, L, q, s_hop1[(k + 1) & 1][q - nb0], s_hop2[(k + 1) & 1][q - nb0]);
       }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      int32_t st = s_pst;
+      uint32_t rows = s_pw[1], p = s_pw[0];
+      // a walk that reached the block end short of OriginalSize: the header read (:342-345)
+      if (st == OKV_BLK_OK && p < orig) st = OKV_BLK_PANIC;
       if (st != OKV_BLK_OK) rows = p = 0;  // a failed block has no rows
       s_walk[0] = rows;
       s_walk[3] = p;
@@ -1584,6 +1656,7 @@ __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Total
       P.blk_status[b] = st;
     }
     __syncthreads();
+    OKV_POINT_STAMP(2);
     const uint64_t rows = s_walk[0], pend = s_walk[3];
     const int32_t st = s_st;
     uint64_t kb = 0, vb = 0;
@@ -1634,6 +1707,7 @@ __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Total
         kb = ktot;
         vb = vtot;
         __syncthreads();
+        OKV_POINT_STAMP(3);
         emit_fast<3>(P, sm, bias, int(rows), kb, vb, row0, kb0, vb0);
       } else {
         // more rows than the row table holds: the byte totals by a second
@@ -1662,6 +1736,7 @@ __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Total
     vb0 += round16(vb);
     bad += st != OKV_BLK_OK;
     __syncthreads();  // the stage and the row table are reused by the next block
+    OKV_POINT_STAMP(4);
   }
   if (tid == 0) {
     P.row_start[P.nblk] = row0;

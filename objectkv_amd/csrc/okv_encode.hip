@@ -58,6 +58,8 @@ constexpr uint32_t kLook = 2048;                 // lookahead rows staged by E3
 constexpr uint32_t kPackRows = 512;              // rows per LDS batch in E10
 constexpr uint64_t kNone = ~uint64_t(0);
 
+constexpr uint32_t kFkCap = 32;  // FirstKey bytes kept per block for the meta kernel
+
 struct EncTotals {
   unsigned long long min_size;    // smallest record (6 + k + v)
   unsigned long long bad_row;     // first row with an empty key (kNone: none)
@@ -95,9 +97,12 @@ struct EncScratch {
   uint64_t* moff = nullptr;      // [nb] meta entry offsets (relative to the meta block)
   uint64_t* orig = nullptr;      // [nb] OriginalSize (the rows' record bytes) of each block
   uint16_t* fkl = nullptr;       // [nb] key length of each block's first row (its FirstKey)
+  uint8_t* fk = nullptr;         // [nb][kFkCap] its first kFkCap bytes (the LDS pack kernel)
   size_t cap_blocks = 0;
-  uint32_t* jts = nullptr;       // [ntiles][kCutS] level-0 chain table of the one-pass cut
+  uint32_t* jts = nullptr;       // [ntiles][kCutS] level-0 chain table of the tile cut
   uint32_t* jbs = nullptr;
+  uint32_t* tentry = nullptr;    // [ntiles] the tile's entry row, blocks before it
+  uint64_t* tkbase = nullptr;
   size_t cap_cut = 0;
   uint64_t* btile = nullptr;     // [4][nbtiles]: BlockSize tot/pre, entry tot/pre
   size_t cap_btiles = 0;
@@ -131,8 +136,8 @@ void enc_release(okv_ctx* ctx) {
   EncScratch* e = ctx->enc;
   if (!e) return;
   void* ps[] = {e->pl, e->nx, e->tile_tot, e->tile_pre, e->jt, e->jb, e->entry, e->kbase,
-                e->first, e->desc, e->hash, e->bsl, e->esl, e->moff, e->orig, e->fkl, e->jts,
-                e->jbs, e->btile,
+                e->first, e->desc, e->hash, e->bsl, e->esl, e->moff, e->orig, e->fkl, e->fk, e->jts,
+                e->jbs, e->tentry, e->tkbase, e->btile,
                 e->d_tot, e->d_in, e->d_outseg, e->p_flag, e->p_inc, e->p_tab, e->p_jlim,
                 e->p_ctr};
   for (void* p : ps)
@@ -253,13 +258,21 @@ __global__ __launch_bounds__(kThreads) void okv_enc_size_next_kernel(
   const uint64_t cs = uint64_t(blockIdx.x) * kETile;
   const uint64_t nwin = std::min<uint64_t>(n - cs, kFuseWin);
   uint64_t mn = kNone, bad = kNone;
+  uint32_t klv[kFuseItems], vlv[kFuseItems];  // (all loads in flight together)
+#pragma unroll
+  for (int i = 0; i < kFuseItems; ++i) {
+    const uint64_t r = cs + std::min<uint64_t>(i * kThreads + threadIdx.x, nwin - 1);
+    klv[i] = key_len[r];
+    vlv[i] = val_len[r];
+  }
+#pragma unroll
   for (int i = 0; i < kFuseItems; ++i) {  // coalesced loads
     const uint32_t j = i * kThreads + threadIdx.x;
     uint64_t sz = 0;
     if (j < nwin) {
       const uint64_t r = cs + j;
-      const uint32_t kl = key_len[r];
-      sz = 6u + uint64_t(kl) + uint64_t(val_len[r]);
+      const uint32_t kl = klv[i];
+      sz = 6u + uint64_t(kl) + uint64_t(vlv[i]);
       if (j < kETile) {
         if (kl == 0 && r < bad) bad = r;
         mn = sz < mn ? sz : mn;
@@ -668,13 +681,23 @@ __device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
   mn = kNone;
   bad = kNone;
   bool wide = false;
-  for (int i = 0; i < kFuseItems; ++i) {  // coalesced loads
+  // coalesced loads, all issued before the first is used (clamped addresses:
+  // a conditional load per item compiled to nine serial HBM round trips)
+  uint32_t klv[kFuseItems], vlv[kFuseItems];
+#pragma unroll
+  for (int i = 0; i < kFuseItems; ++i) {
+    const uint64_t r = cs + std::min<uint64_t>(i * kThreads + threadIdx.x, nwin - 1);
+    klv[i] = key_len[r];
+    vlv[i] = val_len[r];
+  }
+#pragma unroll
+  for (int i = 0; i < kFuseItems; ++i) {
     const uint32_t j = i * kThreads + threadIdx.x;
     uint64_t sz = 0;
     if (j < nwin) {
       const uint64_t r = cs + j;
-      const uint32_t kl = key_len[r];
-      sz = 6u + uint64_t(kl) + uint64_t(val_len[r]);
+      const uint32_t kl = klv[i];
+      sz = 6u + uint64_t(kl) + uint64_t(vlv[i]);
       if (j < kETile) {
         S.kl[j] = uint16_t(kl);
         if (kl == 0 && r < bad) bad = r;
@@ -698,7 +721,7 @@ __device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
   if (threadIdx.x == 0) S.W[0] = 0;
   __syncthreads();
   const uint32_t rows = uint32_t(std::min<uint64_t>(n - cs, kETile));
-  wide |= (total >> 32) != 0;
+  wide |= total >= 0xffffffffull;  // (so a saturated u32 target below exceeds every W)
   // next(a): first m > a - cs with W[m] >= W[a - cs] + T  (b = cs + m - 1)
   const uint32_t M = uint32_t(nwin) + 1;
   const bool complete = cs + nwin == n;
@@ -709,12 +732,13 @@ __device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
   for (int i = 0; i < kEItems; ++i) {
     const uint32_t ar = a0 + i;
     if (ar >= rows) break;
-    const uint64_t target = uint64_t(S.W[ar]) + T;
+    const uint32_t w0 = S.W[ar];
+    const uint32_t target = T >= uint64_t(0xffffffffu - w0) ? 0xffffffffu : w0 + uint32_t(T);
     if (i == 0) {
       uint32_t L = ar + 1, H = M;
       while (L < H) {
         const uint32_t m = (L + H) >> 1;
-        if (uint64_t(S.W[m]) >= target)
+        if (S.W[m] >= target)
           H = m;
         else
           L = m + 1;
@@ -722,7 +746,7 @@ __device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
       mb = L;
     } else {
       mb = std::max(mb, ar + 1);
-      while (mb < M && uint64_t(S.W[mb]) < target) ++mb;
+      while (mb < M && S.W[mb] < target) ++mb;
     }
     uint32_t d;
     if (mb < M)
@@ -810,15 +834,43 @@ __global__ __launch_bounds__(kThreads) void okv_enc_cut_kernel(
   if (threadIdx.x == 0) tile_raw[blockIdx.x] = w_rows;
 }
 
-// The level-0 table at the width the pointer doubling uses (W entries per tile).
-__global__ __launch_bounds__(kThreads) void okv_enc_restride_kernel(
-    const uint32_t* __restrict__ jts, const uint32_t* __restrict__ jbs, uint64_t nch, uint32_t W,
-    uint32_t* __restrict__ jt, uint32_t* __restrict__ jb) {
+// The pointer doubling's level-0 table over chunks of kCutTiles tiles (W
+// entries per chunk): the chunk's tiles' tables composed.  (One table per
+// tile made every doubling level 4x larger: 0.69 GB of C4's side traffic.)
+constexpr uint32_t kCutTiles = 4;
+__global__ __launch_bounds__(kThreads) void okv_enc_compose_kernel(
+    const uint32_t* __restrict__ jts, const uint32_t* __restrict__ jbs, uint64_t ntiles,
+    uint64_t nch, uint32_t W, uint32_t* __restrict__ jt, uint32_t* __restrict__ jb) {
   const uint64_t gid = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   const uint64_t c = gid / W, j = gid % W;
   if (c >= nch) return;
-  jt[gid] = jts[c * kCutS + j];
-  jb[gid] = jbs[c * kCutS + j];
+  uint32_t e = uint32_t(j), cnt = 0;
+  const uint64_t t1 = std::min<uint64_t>(ntiles, (c + 1) * kCutTiles);
+  for (uint64_t t = c * kCutTiles; t < t1; ++t) {  // (exit offsets are <= kFuseLook < kCutS)
+    cnt += jbs[t * kCutS + e];
+    e = jts[t * kCutS + e];
+  }
+  jt[gid] = e;
+  jb[gid] = cnt;
+}
+
+// Each tile's entry row and the blocks before it, from its chunk's (E6) and
+// the tables of the chunk's tiles before it.
+__global__ __launch_bounds__(kThreads) void okv_enc_tile_entry_kernel(
+    const uint32_t* __restrict__ jts, const uint32_t* __restrict__ jbs,
+    const uint32_t* __restrict__ entry, const uint64_t* __restrict__ kbase, uint64_t ntiles,
+    uint32_t* __restrict__ tentry, uint64_t* __restrict__ tkbase) {
+  const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (t >= ntiles) return;
+  const uint64_t c = t / kCutTiles;
+  uint32_t e = entry[c];
+  uint64_t kb = kbase[c];
+  for (uint64_t s = c * kCutTiles; s < t; ++s) {
+    kb += jbs[s * kCutS + e];
+    e = jts[s * kCutS + e];
+  }
+  tentry[t] = e;
+  tkbase[t] = kb;
 }
 
 // E7 per tile: the chain from the tile's entry row (E6) in LDS; each block
@@ -827,59 +879,23 @@ __global__ __launch_bounds__(kThreads) void okv_enc_emit_tile_kernel(
     const uint16_t* __restrict__ key_len, const uint32_t* __restrict__ val_len, uint64_t n,
     uint64_t T, const uint32_t* __restrict__ entry, const uint64_t* __restrict__ kbase,
     uint64_t* __restrict__ first, uint64_t* __restrict__ orig, uint16_t* __restrict__ fkl,
-    uint64_t nb, uint64_t nch, EncTotals* __restrict__ tot) {
+    uint64_t nb, uint64_t ntiles, EncTotals* __restrict__ tot) {
   __shared__ CutSmem S;
-  __shared__ uint16_t starts[kETile];  // (first the two-block table)
-  __shared__ uint16_t nx4[kETile];
-  __shared__ uint16_t coarse[kETile / 4 + 1];
-  __shared__ uint32_t s_m, s_q;
+  __shared__ uint16_t starts[kETile];
+  __shared__ uint32_t s_m;
   const uint64_t c = blockIdx.x, cs = c * kETile;
   uint64_t mn, bad, wmax;
   bool far;
   const uint32_t rows = cut_stage(key_len, val_len, n, T, cs, S, mn, bad, wmax, far);
-  // the jump tables (cut_jumps' rules; nx2 held in `starts` until the walk)
-  uint16_t* nx2 = starts;
-  for (int i = 0; i < kEItems; ++i) {
-    const uint32_t a = i * kThreads + threadIdx.x;
-    if (a < rows) {
-      const uint32_t b = a + S.nx[a];
-      nx2[a] = b < rows ? uint16_t(b - a + S.nx[b]) : kNoJump;
-    }
-  }
-  __syncthreads();
-  for (int i = 0; i < kEItems; ++i) {
-    const uint32_t a = i * kThreads + threadIdx.x;
-    if (a < rows) {
-      const uint32_t x = nx2[a];
-      const uint32_t q = a + x;
-      nx4[a] = x != kNoJump && q < rows && nx2[q] != kNoJump ? uint16_t(x + nx2[q]) : kNoJump;
-    }
-  }
-  __syncthreads();
-  // lane 0: the chain from the entry row four blocks a step (the last <= 3
-  // blocks one at a time); then lane i expands the i-th four-block step
+  // (lane 0 walks the chain; a four-block jump table and a parallel expansion
+  // measured slower: 504 vs 370 us per C4 launch)
   if (threadIdx.x == 0) {
-    uint32_t pos = entry[c], q = 0, m = 0;
-    while (pos < rows && nx4[pos] != kNoJump) {
-      coarse[q++] = uint16_t(pos);
-      pos += nx4[pos];
-    }
-    m = 4 * q;
+    uint32_t pos = entry[c], m = 0;
     while (pos < rows) {
       starts[m++] = uint16_t(pos);
       pos += S.nx[pos];
     }
     s_m = m;
-    s_q = q;
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < s_q; i += kThreads) {
-    uint32_t pos = coarse[i];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      starts[4 * i + k] = uint16_t(pos);
-      pos += S.nx[pos];
-    }
   }
   __syncthreads();
   const uint32_t m = s_m;
@@ -894,7 +910,7 @@ __global__ __launch_bounds__(kThreads) void okv_enc_emit_tile_kernel(
     orig[k0 + i] = S.W[a + S.nx[a]] - S.W[a];
     fkl[k0 + i] = S.kl[a];
   }
-  if (c == nch - 1 && threadIdx.x == 0) {
+  if (c == ntiles - 1 && threadIdx.x == 0) {
     if (k0 + m != nb) tot->fault = 1;
     first[nb] = n;
   }
@@ -923,13 +939,21 @@ __global__ __launch_bounds__(kThreads) void okv_enc_stat_kernel(StatParams P) {
   const uint64_t base = uint64_t(blockIdx.x) * kETile + uint64_t(threadIdx.x) * kEItems;
   uint64_t lb[kEItems], le[kEItems];
   uint64_t sb = 0, se = 0, bmax = 0;
+  uint64_t rawv[kEItems];  // loads first (clamped), so they are in flight together
+  uint32_t fklv[kEItems];
+#pragma unroll
+  for (int i = 0; i < kEItems; ++i) {
+    const uint64_t k = std::min<uint64_t>(base + i, P.nb - 1);
+    rawv[i] = P.orig[k];
+    fklv[i] = P.fkl[k];
+  }
 #pragma unroll
   for (int i = 0; i < kEItems; ++i) {
     const uint64_t k = base + i;
     if (k < P.nb) {
-      const uint64_t raw = P.orig[k];
+      const uint64_t raw = rawv[i];
       const uint64_t bs = (raw / P.D + 1) * P.D;
-      const uint64_t es = 42u + P.fkl[k];
+      const uint64_t es = 42u + fklv[i];
       Desc d;
       d.offset = 0;
       d.block_size = bs;
@@ -1017,6 +1041,7 @@ struct PackParams {
   uint8_t* meta;   // non-null: okv_enc_pack_lds_kernel also writes the blocks' meta
                    // index entries (BlockStat.toBytes, block_stat.go:27-42) here
   const uint64_t* moff;  // [nb] entry offsets within the meta block
+  uint8_t* fk = nullptr;  // non-null: the LDS kernel keeps each block's first kFkCap key bytes
 };
 
 struct __align__(16) PackSmem {
@@ -1344,16 +1369,21 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
   uint32_t* img = reinterpret_cast<uint32_t*>(img4);
   const uint64_t k0 = uint64_t(blockIdx.x) * G;
   const uint32_t g = uint32_t(std::min<uint64_t>(G, nb - k0));
+  // one HBM trip for everything that needs only the region's index: its
+  // blocks' first rows and descriptors (clamped addresses, issued together;
+  // round 4 waited for the region's extent before loading first[])
+  const uint64_t frow = P.first[k0 + std::min<uint32_t>(threadIdx.x, g)];
+  Desc dt{};
+  if (threadIdx.x < 64) dt = P.desc[k0 + std::min<uint32_t>(threadIdx.x, g - 1)];
   const uint64_t O0 = P.desc[k0].offset;
   const Desc dl = P.desc[k0 + g - 1];
   const uint32_t nq = uint32_t((dl.offset + dl.block_size - O0) >> 4);
+  if (threadIdx.x <= g) bfirst[threadIdx.x] = frow;
   for (uint32_t q = threadIdx.x; q < nq; q += kThreads) img4[q] = make_uint4(0, 0, 0, 0);
-  if (threadIdx.x <= g) bfirst[threadIdx.x] = P.first[k0 + threadIdx.x];
   if (threadIdx.x < 64) {  // g <= kMaxRegion = 64: wave 0
     const uint32_t t = threadIdx.x;
     uint64_t orig = 0;
-    if (t < g) {  // one trip with first[] (and the meta entry offset)
-      const Desc dt = P.desc[k0 + t];
+    if (t < g) {  // (with first[], and the meta entry offset)
       brel[t] = dt.offset - O0;
       blen[t] = uint32_t(dt.block_size);
       slim[t] = uint32_t(dt.offset - O0 + (dt.block_size & ~uint64_t(31)));
@@ -1412,6 +1442,15 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
         hi = m;
     }
     if (kMeta && r == bfirst[lo]) bfkl[lo] = kl;
+    if (P.fk && r == bfirst[lo]) {
+      // the block's first kFkCap key bytes (only the key's own are used), for
+      // the meta kernel -- which otherwise reads the block's first line from
+      // the segment, one scattered line per block (lines just loaded: L2 hits)
+      const Lines5 F = load_lines5(P.key_arena + ko, std::min<uint32_t>(kl, kFkCap));
+      uint4* o = reinterpret_cast<uint4*>(P.fk + (k0 + lo) * kFkCap);
+      o[0] = funnel32(F.l[0], F.l[1], F.s);
+      o[1] = funnel32(F.l[1], F.l[2], F.s);
+    }
     // (the other arms: the row's absolute row-stream position from the row
     // prefix, less the block's -- the region's first row's absolute position
     // abs0 plus the block's region-relative base)
@@ -1620,6 +1659,10 @@ struct MetaParams {
   // of through the row arrays (key_len, key_off and the key: three scattered
   // lines); null: through the row arrays
   const uint8_t* seg = nullptr;
+  // non-null: each block's FirstKey length and (when <= kFkCap) bytes, kept by
+  // the planner and the LDS pack kernel -- two coalesced reads per block
+  const uint8_t* fk = nullptr;
+  const uint16_t* fkl = nullptr;
 };
 
 __global__ __launch_bounds__(kThreads) void okv_enc_meta_kernel(MetaParams P) {
@@ -1663,7 +1706,10 @@ __global__ __launch_bounds__(kThreads) void okv_enc_meta_kernel(MetaParams P) {
 // Block k's FirstKey (block_stat.go:31-33): the key of its first record.
 __device__ __forceinline__ void first_key(const MetaParams& P, uint64_t k, const Desc& d,
                                           uint32_t& kl, const uint8_t*& key) {
-  if (P.seg) {  // [u16 LE kl][u32 LE vl][key] at the block's start
+  if (P.fk && P.fkl[k] <= kFkCap) {
+    kl = P.fkl[k];
+    key = P.fk + k * kFkCap;
+  } else if (P.seg) {  // [u16 LE kl][u32 LE vl][key] at the block's start
     const uint8_t* rec = P.seg + d.offset;
     kl = uint32_t(rec[0]) | (uint32_t(rec[1]) << 8);
     key = rec + 6;
@@ -1875,6 +1921,7 @@ int ensure_blocks_enc(okv_ctx* ctx, EncScratch* e, uint64_t nb) {
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->moff), c * 8))) return rc;
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->orig), c * 8))) return rc;
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->fkl), c * 2))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->fk), c * kFkCap))) return rc;
     e->cap_blocks = c;
   }
   if (nbt > e->cap_btiles || !e->btile) {
@@ -1937,6 +1984,8 @@ int ensure_cut(okv_ctx* ctx, EncScratch* e, uint64_t ntiles) {
   if (ntiles * kCutS > e->cap_cut || !e->jts) {
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->jts), ntiles * kCutS * 4))) return rc;
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->jbs), ntiles * kCutS * 4))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->tentry), ntiles * 4))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->tkbase), ntiles * 8))) return rc;
     e->cap_cut = ntiles * kCutS;
   }
   return OKV_OK;
@@ -1984,7 +2033,7 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   // entered at offsets <= kFuseLook, so its tables are at most kCutS wide)
   const uint64_t wmax = std::max<uint64_t>(1, e->h_tot->wmax);
   const uint64_t W = tile_cut ? std::min<uint64_t>(wmax, kCutS) : wmax;
-  uint64_t C = tile_cut ? kETile : 4096;
+  uint64_t C = tile_cut ? uint64_t(kETile) * kCutTiles : 4096;
   while (C < W) C <<= 1;
   const uint64_t nch = (n + C - 1) / C;
   uint32_t levels = 0;
@@ -1992,8 +2041,9 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   const uint64_t lv = nch * W;
   if ((rc = ensure_jump(ctx, e, lv * std::max<uint32_t>(levels, 1), nch))) return rc;
   if (tile_cut)
-    hipLaunchKernelGGL(okv_enc_restride_kernel, dim3(ceil_div(lv, kThreads)), dim3(kThreads), 0,
-                       ctx->stream, e->jts, e->jbs, nch, uint32_t(W), e->jt, e->jb);
+    hipLaunchKernelGGL(okv_enc_compose_kernel, dim3(ceil_div(lv, kThreads)), dim3(kThreads), 0,
+                       ctx->stream, e->jts, e->jbs, uint64_t(ntiles), nch, uint32_t(W), e->jt,
+                       e->jb);
   else
     hipLaunchKernelGGL(okv_enc_jump0_kernel, dim3(ceil_div(lv, kThreads)), dim3(kThreads), 0,
                        ctx->stream, e->nx, n, C, uint32_t(W), nch, e->jt, e->jb);
@@ -2015,10 +2065,14 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   uint64_t* bpre = e->btile + e->cap_btiles;
   uint64_t* etot = e->btile + 2 * e->cap_btiles;
   uint64_t* epre = e->btile + 3 * e->cap_btiles;
-  if (tile_cut)
-    hipLaunchKernelGGL(okv_enc_emit_tile_kernel, dim3(uint32_t(nch)), dim3(kThreads), 0,
-                       ctx->stream, R.kl, R.vl, n, T, e->entry, e->kbase, e->first, e->orig,
-                       e->fkl, nb, nch, e->d_tot);
+  if (tile_cut) {
+    hipLaunchKernelGGL(okv_enc_tile_entry_kernel, dim3(ceil_div(ntiles, kThreads)), dim3(kThreads),
+                       0, ctx->stream, e->jts, e->jbs, e->entry, e->kbase, uint64_t(ntiles),
+                       e->tentry, e->tkbase);
+    hipLaunchKernelGGL(okv_enc_emit_tile_kernel, dim3(ntiles), dim3(kThreads), 0, ctx->stream,
+                       R.kl, R.vl, n, T, e->tentry, e->tkbase, e->first, e->orig, e->fkl, nb,
+                       uint64_t(ntiles), e->d_tot);
+  }
   else
     hipLaunchKernelGGL(okv_enc_emit_kernel, dim3(ceil_div(nch, kThreads)), dim3(kThreads), 0,
                        ctx->stream, e->nx, n, C, nch, e->entry, e->kbase, e->first, nb, e->pl,
@@ -2069,7 +2123,7 @@ uint64_t pack_region_blocks(const Plan& pl) {
 // or a byte kernel when the segment is not 16-byte aligned.  *hashed: the
 // launch also wrote the block hashes.
 int enc_pack(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opts& o,
-             const Plan& pl, uint8_t* seg, const PackParams& pp, bool* hashed) {
+             const Plan& pl, uint8_t* seg, const PackParams& pp, bool* hashed, bool* fk_done) {
   // record-major LDS assembly pays off for small records (most chunks would
   // mix fields); large records take the chunk-major kernels, which read the
   // row prefix (E1-E2; a single-pass plan does not write it)
@@ -2078,10 +2132,13 @@ int enc_pack(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   const uint64_t G = pack_region_blocks(pl);
   int rc;
   if (aligned && GL >= 1 && pl.avg_rec <= 512) {
-    // small records: record-major LDS assembly and the block hashes
+    // small records: record-major LDS assembly, the block hashes and FirstKeys
+    PackParams q = pp;
+    q.fk = e->fk;
     hipLaunchKernelGGL((okv_enc_pack_lds_kernel<kImage, 7>), dim3(ceil_div(pl.nb, GL)),
-                       dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
+                       dim3(kThreads), 0, ctx->stream, q, pl.nb, uint32_t(GL));
     *hashed = true;
+    *fk_done = true;
     return OKV_OK;
   }
   // the other kernels read the row prefix: computed here (the tile cut writes
@@ -2127,14 +2184,14 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   pp.hash = e->hash;
   pp.meta = nullptr;
   pp.moff = e->moff;
-  bool hashed = false, meta_done = false;
+  bool hashed = false, meta_done = false, fk_done = false;
   int rc;
 #ifdef OKV_ABLATE
   bool handled = false;  // an ablation knob chose the pack launch
   if ((rc = enc_pack_ablate(ctx, e, R, o, pl, seg, pp, &hashed, &meta_done, &handled))) return rc;
   if (!handled)
 #endif
-    if ((rc = enc_pack(ctx, e, R, o, pl, seg, pp, &hashed))) return rc;
+    if ((rc = enc_pack(ctx, e, R, o, pl, seg, pp, &hashed, &fk_done))) return rc;
   enc_mark(ctx, e, 2);
   if (!hashed) launch_hash(ctx->stream, seg, pl.data_bytes, e->desc, uint32_t(pl.nb), e->hash);
   enc_mark(ctx, e, 3);
@@ -2153,6 +2210,8 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   mp.meta = seg + pl.data_bytes;
   mp.bloom_len = o.bloom ? o.bloom_len : ~uint64_t(0);
   mp.seg = o.compression == OKV_COMP_NONE ? seg : nullptr;
+  mp.fk = fk_done ? e->fk : nullptr;
+  mp.fkl = e->fkl;
   if (o.bloom && o.bloom_len)  // BloomFilter.WriteTo bytes at head - 10 - len (after flag + u64)
     OKV_HIP(hipMemcpyAsync(mp.meta + pl.head - 10 - o.bloom_len, o.bloom, o.bloom_len,
                            hipMemcpyHostToDevice, ctx->stream));

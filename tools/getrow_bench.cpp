@@ -7,7 +7,10 @@
 // GetRow (host probe, no GPU call).
 //
 // build: tools/build_getrow_bench.sh   run: tools/getrow_bench [calls]
-// prints one JSON line per block size.
+// prints one JSON line per block size.  Linked against the ablation build
+// (tools/getrow_bench_ablate), it also prints the point kernel's phase
+// times of one more GetRow (okv_debug_point_times: staged, walked,
+// prefixes, emitted, in microseconds from the block's start).
 #include <dlfcn.h>
 
 #include <algorithm>
@@ -100,6 +103,22 @@ int main(int argc, char** argv) {
       }
     }
     okv_reader_io_stats(r, &io1);
+    typedef int (*times_fn)(uint64_t*);
+    times_fn times = (times_fn)dlsym(RTLD_DEFAULT, "okv_debug_point_times");
+    if (times) {
+      double acc[4] = {0, 0, 0, 0};
+      const int reps = 50;
+      for (int i = 0; i < reps; ++i) {
+        key_of(rng() % c.rows, key);
+        okv_reader_get_row(r, key, 16, &row);
+        uint64_t t[5];
+        times(t);
+        for (int k = 0; k < 4; ++k) acc[k] += double(t[k + 1] - t[0]) / 100.0;
+      }
+      std::printf("{\"config\": \"%s\", \"point_phase_us\": {\"staged\": %.2f, \"walked\": %.2f, "
+                  "\"prefixes\": %.2f, \"emitted\": %.2f}}\n",
+                  c.name, acc[0] / reps, acc[1] / reps, acc[2] / reps, acc[3] / reps);
+    }
     // the CPU restatement's one-block decode of the same blocks
     std::vector<double> tc;
     const uint64_t nb = okv_writer_num_blocks(w);

@@ -31,11 +31,12 @@
 extern "C" {
 #endif
 
-#define OKV_ABI_VERSION 5 /* 2: okv_encode_opts.bloom / bloom_len, and okv_profile_read writes
+#define OKV_ABI_VERSION 6 /* 2: okv_encode_opts.bloom / bloom_len, and okv_profile_read writes
                              4 doubles (ms[4]: the zstd stage slot was added);
                              3: okv_open_ex / okv_open_opts
                              4: okv_decode_chain
-                             5: OKV_OPEN_NO_POINT / OKV_PATH_POINT (host-mode point path) */
+                             5: OKV_OPEN_NO_POINT / OKV_PATH_POINT (host-mode point path)
+                             6: okv_point_get (GetRow's block step, one row back) */
 
 /* ---- return codes (int) -------------------------------------------------- */
 #define OKV_OK 0
@@ -188,6 +189,32 @@ int okv_decode_blocks(okv_ctx *ctx, const uint8_t *seg, uint64_t seg_bytes,
  * okv_close of either unchains the pair.  The caller's current device is kept.
  */
 int okv_decode_chain(okv_ctx *ctx, okv_ctx *after);
+
+/*
+ * GetRow's block step (segment_reader.go:387-404) on one block, host memory:
+ * ReadBlockWithStat of the block -- every record walked with Go's checks --
+ * then the first row whose key equals `key` (bytes.Equal, :398), in one
+ * point-path launch (okv_point_kernel: the block and the key in, that one
+ * row out; no row arrays come back).
+ *   out->status : the block's OKV_BLK_* outcome (rows exist only when OK);
+ *   out->found  : 1 (key / val point at the row's bytes, valid until the next
+ *                 call on ctx), 0 (no such row), or -1 (the block is not a
+ *                 point-path block -- zstd, BlockSize > 64 KiB, a key longer
+ *                 than 8 KiB, or more than 1 024 rows: use okv_decode_blocks).
+ * Returns OKV_OK or a negative error.  (ABI 6.)
+ */
+typedef struct okv_point_row {
+  int32_t status;
+  int32_t found;
+  const uint8_t *key;
+  uint64_t key_len;
+  const uint8_t *val;
+  uint64_t val_len;
+} okv_point_row;
+
+int okv_point_get(okv_ctx *ctx, const uint8_t *seg, uint64_t seg_bytes,
+                  const okv_block_desc *desc, int compression, const uint8_t *key,
+                  uint64_t key_len, okv_point_row *out);
 
 /* After an OKV_F_ASYNC decode and okv_sync(): copy the device totals into out. */
 int okv_decode_totals(okv_ctx *ctx, okv_decode_out *out);

@@ -41,6 +41,7 @@ M_EOF = 1
 SYMBOLS = [
     "okv_open", "okv_open_on_stream", "okv_open_ex", "okv_close", "okv_last_error", "okv_stream", "okv_sync",
     "okv_abi_version", "okv_decode_plan", "okv_decode_blocks", "okv_decode_totals",
+    "okv_point_get",
     "okv_xxh64", "okv_hash_blocks", "okv_device_alloc", "okv_device_free", "okv_host_alloc",
     "okv_host_free", "okv_memcpy", "okv_profile", "okv_profile_read", "okv_last_path",
     "okv_decode_chain",
@@ -70,6 +71,12 @@ class Row(C.Structure):
 
 class ReaderIO(C.Structure):
     _fields_ = [("calls", C.c_uint64), ("blocks", C.c_uint64), ("bytes_staged", C.c_uint64)]
+
+
+class PointRow(C.Structure):
+    """okv_point_row (include/okv_sst.h, ABI 6)."""
+    _fields_ = [("status", C.c_int32), ("found", C.c_int32), ("key", C.c_void_p),
+                ("key_len", C.c_uint64), ("val", C.c_void_p), ("val_len", C.c_uint64)]
 
 
 class BlockDesc(C.Structure):
@@ -170,6 +177,8 @@ def lib():
                                   C.POINTER(u64)]),
         "okv_decode_blocks": (i32, [p, p, u64, p, u32, i32, C.POINTER(DecodeOut), u32]),
         "okv_decode_totals": (i32, [p, C.POINTER(DecodeOut)]),
+        "okv_point_get": (i32, [p, p, u64, C.POINTER(BlockDesc), i32, p, u64,
+                                C.POINTER(PointRow)]),
         "okv_xxh64": (u64, [p, C.c_size_t, u64]),
         "okv_hash_blocks": (i32, [p, p, u64, p, u32, p, u32]),
         "okv_device_alloc": (p, [p, C.c_size_t]),

@@ -1526,28 +1526,6 @@ __global__ __launch_bounds__(kThreads) void okv_copy_kernel(CopyParams P) {
 // blocks of more than kFastRows rows re-walk in batches, materialise).  The
 // host admits only batches whose OK blocks stage (BlockSize <= kStage).
 // ---------------------------------------------------------------------------
-constexpr uint32_t kPointWin = 8192;  // hop-table window (byte positions)
-constexpr uint16_t kBadHop = 0xffff;
-// Hop lengths from byte position q < L of a staged block: h1 = the record at
-// q's length - 6, h2 = that record's and the next one's - 12, kBadHop where
-// Go's checks (:342-349) fail at q (h1) or at either record (h2).  Branch-free:
-// header reads past the block end stay inside the stage's guard.
-__device__ __forceinline__ void point_hops(const uint32_t* sw, uint32_t bias, uint32_t L,
-                                           uint32_t q, uint16_t& h1, uint16_t& h2) {
-  uint32_t kl, vl;
-  header_lds(sw, bias + q, kl, vl);
-  const uint32_t room = L - q - 6;
-  const bool ok1 = (L - q >= 6) & (kl <= room) & (vl <= room - kl);
-  const uint32_t len = ok1 ? 6 + kl + vl : 0u;
-  const uint32_t q1 = q + len;  // <= L
-  uint32_t kl1, vl1;
-  header_lds(sw, bias + q1, kl1, vl1);
-  const uint32_t room1 = L - q1 - 6;
-  const bool ok2 = ok1 & (L - q1 >= 6) & (kl1 <= room1) & (vl1 <= room1 - kl1);
-  h1 = ok1 ? uint16_t(len - 6) : kBadHop;
-  h2 = ok2 ? uint16_t(len + kl1 + vl1 - 6) : kBadHop;
-}
-
 #ifdef OKV_ABLATE
 // (ablation build: wall-clock stamps of the point kernel's phases for the
 // last block of the last call -- start, staged, walked, prefixes, emitted;
@@ -1558,16 +1536,33 @@ __device__ uint64_t g_point_t[8];
 #else
 #define OKV_POINT_STAMP(i)
 #endif
-__global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Totals* tot) {
+// okv_point_get's search (GetRow :395-403): the key (<= kFindKey bytes, host
+// memory, 4-byte aligned) and the answer: found = 1 (the row's key and value
+// at key_arena / val_arena, lengths at key_len[0] / val_len[0]), 0, or -1
+// (more rows than the row table: the caller decodes the block in full).
+struct PointFind {
+  const uint8_t* key;
+  uint32_t klen;
+  int32_t* found;
+};
+constexpr uint32_t kFindKey = 8192;  // (held in the row table's prefix arrays)
+
+template <bool kFind>
+__global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Totals* tot,
+                                                             PointFind F) {
   __shared__ CopySmem sm;
   __shared__ uint64_t s_walk[4];  // rows, key bytes, value bytes, walk end
   __shared__ uint32_t s_wsum[2][kThreads / 64];
   __shared__ int32_t s_st, s_pst;
-  __shared__ uint32_t s_pw[3];
-  __shared__ uint16_t s_hop1[2][kPointWin], s_hop2[2][kPointWin];
+  __shared__ uint32_t s_pw[2];
   const uint32_t tid = threadIdx.x;
   const uint32_t* sw = reinterpret_cast<const uint32_t*>(sm.stage);
   uint64_t row0 = 0, kb0 = 0, vb0 = 0, bad = 0;  // exclusive prefixes (uniform)
+  if constexpr (kFind) {  // the key into LDS (the prefix arrays: unused by the search)
+    static_assert(2 * (kFastRows + 1) * 4 >= kFindKey, "key fits the prefix arrays");
+    const uint32_t* k4 = reinterpret_cast<const uint32_t*>(F.key);
+    for (uint32_t i = tid; i < (F.klen + 3) / 4; i += kThreads) sm.f.kpre[i] = k4[i];
+  }
   for (uint32_t b = 0; b < P.nblk; ++b) {
     OKV_POINT_STAMP(0);
     const Desc d = P.descs[b];
@@ -1590,57 +1585,66 @@ __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Total
     __syncthreads();
     OKV_POINT_STAMP(1);
     const uint32_t bias = 16u + shift;
-    // The header walk (Go's checks in its order) with the hop table: for every
-    // byte position q of an 8 KiB window, the length of the record at q and of
-    // the two records from q (or kBadHop where Go's checks fail), computed by
-    // all lanes; lane 0 then walks the window two records per LDS read while
-    // waves 1-3 fill the next window's table into the other slot.  (Lane 0
-    // alone, one dependent header decode per record: 120 ns a record, 80 us
-    // of a 64 KiB block's 116 us GetRow.)
+    // The header walk (Go's checks in its order) by wave 0 on a wave-uniform
+    // position, run-length speculated: from a record at p of length len, lane
+    // j reads the header at p + j * len -- a record start if every record
+    // before it was len long.  The first lane that breaks the run (past
+    // OriginalSize, a failed check, another length) ends the round; its
+    // position is a true record start, so a round confirms at least two
+    // records (the one at p and the next) and up to 64 when lengths repeat,
+    // for two dependent LDS reads.  (Lane 0 alone, one dependent header
+    // decode per record: 120 ns a record, 80 us of a 64 KiB block's GetRow.)
     const uint32_t L = st0 == OKV_BLK_OK ? uint32_t(len) : 0u;  // <= kStage
     const uint64_t orig = go_walk_bound(d.original_size);       // int(OriginalSize) (:340)
-    const uint32_t nwin = (L + kPointWin - 1) / kPointWin;
-    if (tid == 0) {
-      s_pw[0] = 0;          // position
-      s_pw[1] = 0;          // rows
-      s_pw[2] = orig == 0;  // done
-      s_pst = st0;
-    }
-    for (uint32_t q = tid; q < min(L, kPointWin); q += kThreads)
-      point_hops(sw, bias, L, q, s_hop1[0][q], s_hop2[0][q]);
-    __syncthreads();
-    for (uint32_t k = 0; k < nwin; ++k) {
-      const uint32_t wb = k * kPointWin, we = min(L, wb + kPointWin);
-      if (tid == 0 && !s_pw[2]) {
-        const uint16_t* h1 = s_hop1[k & 1];
-        const uint16_t* h2 = s_hop2[k & 1];
-        uint32_t p = s_pw[0], rows = s_pw[1];
-        bool done = false;
-        while (p < we) {  // (p < orig: checked per record)
-          if (p >= orig) { done = true; break; }
-          const uint32_t a1 = h1[p - wb], a2 = h2[p - wb];
-          if (a1 == kBadHop) { s_pst = OKV_BLK_PANIC; done = true; break; }  // :342-349
-          sm.f.rec[min(rows, uint32_t(kFastRows))] = p;
-          ++rows;
-          const uint32_t p1 = p + 6 + a1;
-          if (p1 < orig && a2 != kBadHop) {
-            sm.f.rec[min(rows, uint32_t(kFastRows))] = p1;
-            ++rows;
-            p += 12 + a2;
-          } else {
-            p = p1;
+    if (tid < 64) {
+      const uint32_t lane = tid;
+      const uint32_t o32 =
+          __builtin_amdgcn_readfirstlane(uint32_t(min<uint64_t>(orig, 0xffffffffull)));
+      uint32_t p = 0, rows = 0;
+      int32_t pst = st0;
+      if (st0 == OKV_BLK_OK) {
+        while (p < o32) {  // :340
+          uint32_t kl, vl;
+          header_lds(sw, bias + min(p, L), kl, vl);  // (one address: a broadcast)
+          kl = __builtin_amdgcn_readfirstlane(kl);
+          vl = __builtin_amdgcn_readfirstlane(vl);
+          const uint32_t room = L - p - 6;
+          // u16/u32 reads (:342-345), key/value reads (:346-349)
+          if (!((L - p >= 6) & (kl <= room) & (vl <= room - kl))) {
+            pst = OKV_BLK_PANIC;
+            break;
           }
+          const uint32_t rl = 6 + kl + vl;
+          const uint32_t q = p + lane * rl;  // (< 64 * 64 KiB)
+          uint32_t kj, vj;
+          header_lds(sw, bias + min(q, L), kj, vj);
+          const uint32_t rj = L - q - 6;
+          const bool okj = (q <= L) & (L - q >= 6) & (kj <= rj) & (vj <= rj - kj);
+          const bool brk = lane >= 1 && (q >= o32 || !okj || 6 + kj + vj != rl);
+          const uint64_t bm = __ballot(brk);
+          const uint32_t m = bm ? uint32_t(__builtin_ctzll(bm)) : 64u;  // (>= 1)
+          if (lane < m) sm.f.rec[min(rows + lane, uint32_t(kFastRows))] = q;
+          rows += m;
+          p += m * rl;  // the breaking lane's position: a true record start
+          if (m == 64 || p >= o32) continue;
+          const uint32_t okm = __builtin_amdgcn_readlane(uint32_t(okj), m);
+          const uint32_t lm = __builtin_amdgcn_readlane(6 + kj + vj, m);
+          if (!okm) {
+            pst = OKV_BLK_PANIC;
+            break;
+          }
+          if (lane == 0) sm.f.rec[min(rows, uint32_t(kFastRows))] = p;
+          ++rows;
+          p += lm;
         }
+      }
+      if (tid == 0) {
         s_pw[0] = p;
         s_pw[1] = rows;
-        s_pw[2] = done;
-      } else if (tid >= 64 && k + 1 < nwin) {
-        const uint32_t nb0 = wb + kPointWin, ne = min(L, nb0 + kPointWin);
-        for (uint32_t q = nb0 + tid - 64; q < ne; q += kThreads - 64)
-          point_hops(sw, bias, L, q, s_hop1[(k + 1) & 1][q - nb0], s_hop2[(k + 1) & 1][q - nb0]);
+        s_pst = pst;
       }
-      __syncthreads();
     }
+    __syncthreads();
     if (tid == 0) {
       int32_t st = s_pst;
       uint32_t rows = s_pw[1], p = s_pw[0];
@@ -1660,6 +1664,53 @@ __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Total
     const uint64_t rows = s_walk[0], pend = s_walk[3];
     const int32_t st = s_st;
     uint64_t kb = 0, vb = 0;
+    if constexpr (kFind) {
+      // the first row whose key equals F.key: one lane per row compares in
+      // LDS, the lowest index wins; only that row's bytes go back
+      __shared__ uint32_t s_hit;
+      if (tid == 0) s_hit = ~0u;
+      __syncthreads();
+      const bool listed = rows <= uint64_t(kFastRows);
+      if (st == OKV_BLK_OK && listed) {
+        const uint32_t* tk = sm.f.kpre;
+        for (uint32_t i = tid; i < uint32_t(rows); i += kThreads) {
+          uint32_t kl, vl;
+          header_lds(sw, bias + sm.f.rec[i], kl, vl);
+          if (kl != F.klen) continue;
+          const uint32_t kp = bias + sm.f.rec[i] + 6;
+          bool eq = true;
+          for (uint32_t j = 0; j < kl && eq; j += 4) {
+            const uint32_t bi = kp + j, sh = bi & 3;
+            const uint32_t a = funnel(sw[(bi >> 2) + 1], sw[bi >> 2], sh);
+            const uint32_t n = min(4u, kl - j);
+            const uint32_t m = n == 4 ? ~0u : (1u << (8 * n)) - 1u;
+            eq = ((a ^ tk[j >> 2]) & m) == 0;
+          }
+          if (eq) atomicMin(&s_hit, i);
+        }
+      }
+      __syncthreads();
+      OKV_POINT_STAMP(3);
+      const uint32_t hit = s_hit;
+      uint32_t kl = 0, vl = 0;
+      if (hit != ~0u) {
+        const uint32_t r0 = bias + sm.f.rec[hit];
+        header_lds(sw, r0, kl, vl);
+        uint4* ka = reinterpret_cast<uint4*>(P.key_arena);
+        uint4* va = reinterpret_cast<uint4*>(P.val_arena);
+        for (uint32_t c = tid; c < (kl + 15) / 16; c += kThreads) ka[c] = load16_lds(sw, r0 + 6 + 16 * c);
+        for (uint32_t c = tid; c < (vl + 15) / 16; c += kThreads)
+          va[c] = load16_lds(sw, r0 + 6 + kl + 16 * c);
+      }
+      if (tid == 0) {
+        *F.found = st != OKV_BLK_OK ? 0 : !listed ? -1 : hit != ~0u ? 1 : 0;
+        P.key_len[0] = uint16_t(kl);
+        P.val_len[0] = vl;
+        *tot = Totals{hit != ~0u ? 1u : 0u, kl, vl, uint64_t(st != OKV_BLK_OK)};
+      }
+      OKV_POINT_STAMP(4);
+      return;  // (one block)
+    }
     if (st == OKV_BLK_OK && rows) {
       if (rows <= uint64_t(kFastRows)) {
         // key / value lengths of the recorded rows, exclusive prefixes (4 rows a lane)
@@ -2513,7 +2564,8 @@ int decode_point(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv
   P.val_cap = A + 16;
   Totals* tot = reinterpret_cast<Totals*>(S + o_tot);
   ctx->last_path = OKV_PATH_POINT;
-  hipLaunchKernelGGL(okv_point_kernel, dim3(1), dim3(kThreads), 0, ctx->stream, P, tot);
+  hipLaunchKernelGGL(okv_point_kernel<false>, dim3(1), dim3(kThreads), 0, ctx->stream, P, tot,
+                     PointFind{nullptr, 0, nullptr});
   OKV_HIP(hipGetLastError());
   OKV_HIP(hipStreamSynchronize(ctx->stream));
   const Totals T = *tot;
@@ -2536,6 +2588,62 @@ int decode_point(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv
   out(o->val_len, P.val_len, T.rows * 4);
   out(o->key_arena, P.key_arena, T.kb);
   out(o->val_arena, P.val_arena, T.vb);
+  return OKV_OK;
+}
+
+// okv_point_get: GetRow's block step on one block in one launch (the block,
+// its descriptor and the key in the pinned slab; the row, if any, back).
+int point_get(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv_block_desc* desc,
+              int comp, const uint8_t* key, uint64_t klen, okv_point_row* out) {
+  out->status = OKV_BLK_OK;
+  out->found = -1;
+  out->key = out->val = nullptr;
+  out->key_len = out->val_len = 0;
+  if (!ctx->point || klen > kFindKey || !point_eligible(seg_bytes, desc, 1, comp, 0))
+    return OKV_OK;  // not a point-path block: the caller decodes it in full
+  const Desc& d = *reinterpret_cast<const Desc*>(desc);
+  const uint64_t A = go_read_status(d, seg_bytes) == OKV_BLK_OK ? round16(d.block_size) : 0;
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t o_desc = al(seg_bytes + 64), o_key = al(o_desc + sizeof(Desc)),
+               o_misc = al(o_key + klen + 16), o_tot = al(o_misc + 64), o_ka = al(o_tot + 64),
+               o_va = al(o_ka + A + 16), total = al(o_va + A + 16);
+  int rc = grow_host(ctx, &ctx->h_slab, &ctx->cap_slab, total);
+  if (rc) return rc;
+  uint8_t* S = ctx->h_slab;
+  if (seg_bytes) std::memcpy(S, seg, seg_bytes);
+  std::memcpy(S + o_desc, desc, sizeof(Desc));
+  if (klen) std::memcpy(S + o_key, key, klen);
+  CopyParams P;
+  std::memset(&P, 0, sizeof(P));
+  P.seg = S;
+  P.seg_bytes = seg_bytes;
+  P.descs = reinterpret_cast<const Desc*>(S + o_desc);
+  P.nblk = 1;
+  P.comp = comp;
+  uint64_t* misc = reinterpret_cast<uint64_t*>(S + o_misc);  // row_start[2], bases, status, lens
+  P.row_start = misc;
+  P.key_base = misc + 2;
+  P.val_base = misc + 3;
+  P.blk_status = reinterpret_cast<int32_t*>(misc + 4);
+  P.key_len = reinterpret_cast<uint16_t*>(misc + 5);
+  P.val_len = reinterpret_cast<uint32_t*>(misc + 6);
+  int32_t* found = reinterpret_cast<int32_t*>(misc + 7);
+  P.key_arena = S + o_ka;
+  P.val_arena = S + o_va;
+  Totals* tot = reinterpret_cast<Totals*>(S + o_tot);
+  ctx->last_path = OKV_PATH_POINT;
+  hipLaunchKernelGGL(okv_point_kernel<true>, dim3(1), dim3(kThreads), 0, ctx->stream, P, tot,
+                     PointFind{S + o_key, uint32_t(klen), found});
+  OKV_HIP(hipGetLastError());
+  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  out->status = *P.blk_status;
+  out->found = *found;
+  if (out->found == 1) {
+    out->key = P.key_arena;
+    out->key_len = *P.key_len;
+    out->val = P.val_arena;
+    out->val_len = *P.val_len;
+  }
   return OKV_OK;
 }
 
@@ -2893,6 +3001,16 @@ int okv_decode_blocks(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes,
     return decode_device(ctx, seg, seg_bytes, reinterpret_cast<const Desc*>(descs), nblk,
                          compression, out, flags);
   return decode_host(ctx, seg, seg_bytes, descs, nblk, compression, out, flags);
+}
+
+int okv_point_get(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes,
+                  const okv_block_desc* desc, int compression, const uint8_t* key,
+                  uint64_t key_len, okv_point_row* out) {
+  if (!ctx || !out || !desc || (!seg && seg_bytes) || (!key && key_len))
+    return set_err(ctx, OKV_E_ARG, "null argument");
+  if (compression < 0 || compression > 2) return set_err(ctx, OKV_E_ARG, "compression");
+  OKV_HIP(hipSetDevice(ctx->device));
+  return point_get(ctx, seg, seg_bytes, desc, compression, key, key_len, out);
 }
 
 int okv_decode_totals(okv_ctx* ctx, okv_decode_out* out) {

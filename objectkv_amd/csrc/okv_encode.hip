@@ -2133,12 +2133,10 @@ int enc_pack(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   int rc;
   if (aligned && GL >= 1 && pl.avg_rec <= 512) {
     // small records: record-major LDS assembly, the block hashes and FirstKeys
-    PackParams q = pp;
-    q.fk = e->fk;
     hipLaunchKernelGGL((okv_enc_pack_lds_kernel<kImage, 7>), dim3(ceil_div(pl.nb, GL)),
-                       dim3(kThreads), 0, ctx->stream, q, pl.nb, uint32_t(GL));
+                       dim3(kThreads), 0, ctx->stream, pp, pl.nb, uint32_t(GL));
     *hashed = true;
-    *fk_done = true;
+    *fk_done = pp.fk != nullptr;
     return OKV_OK;
   }
   // the other kernels read the row prefix: computed here (the tile cut writes
@@ -2184,6 +2182,7 @@ int enc_write(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_op
   pp.hash = e->hash;
   pp.meta = nullptr;
   pp.moff = e->moff;
+  pp.fk = e->fk;
   bool hashed = false, meta_done = false, fk_done = false;
   int rc;
 #ifdef OKV_ABLATE

@@ -111,6 +111,7 @@ struct okv_reader {
   BatchP last_read;    // the last ReadBlockWithStat batch outside the window (GetRow)
   BatchP range_batch;  // the last GetRange batch
   std::vector<okv_row> range_out;
+  std::vector<uint8_t> point_key, point_val;  // GetRow's row from okv_point_get
   okv_reader_io io{};  // GPU calls, blocks decoded, bytes staged
 };
 
@@ -191,12 +192,14 @@ int ensure_meta(okv_reader* r) {  // "Fetches the metadata if not already loaded
 
 // ReadBlocks: one GPU decode of the given file entries,
 // staging only their span of the storage.
-int decode_batch(okv_reader* r, const std::vector<uint32_t>& entries, BatchP* out) {
-  if (!r->ctx) return OKV_R_GPU;
+// The bytes a batch of these file entries stages: the span of the blocks with
+// a non-negative Offset inside the storage (the others fail before any read:
+// Seek error, or io.EOF at / past the end), and the descriptors rebased onto
+// it (offsets >= the storage end stay >= the span end -- io.EOF --, a
+// BlockSize past the end stays short; negative ones keep their sign).
+void stage_span(const okv_reader* r, const std::vector<uint32_t>& entries,
+                std::vector<okv_block_desc>* descs, const uint8_t** seg, uint64_t* n) {
   const uint64_t nbytes = r->data.size();
-  const uint32_t nb = uint32_t(entries.size());
-  // the span: blocks with a non-negative Offset inside the storage (the others
-  // fail before any read: Seek error, or io.EOF at / past the end)
   uint64_t lo = UINT64_MAX, hi = 0;
   for (uint32_t e : entries) {
     const okv_block_desc& d = r->file_entries[e].d;
@@ -205,15 +208,22 @@ int decode_batch(okv_reader* r, const std::vector<uint32_t>& entries, BatchP* ou
     hi = std::max(hi, d.offset + std::min(d.block_size, nbytes - d.offset));
   }
   if (lo > hi) lo = hi = 0;
-  std::vector<okv_block_desc> descs(nb);
-  for (uint32_t i = 0; i < nb; ++i) {
-    descs[i] = r->file_entries[entries[i]].d;
-    // rebased onto the span: offsets >= the storage end stay >= the span end
-    // (io.EOF), a BlockSize past the end stays short; negative ones keep their sign
-    if (int64_t(descs[i].offset) >= 0) descs[i].offset -= lo;
+  descs->resize(entries.size());
+  for (size_t i = 0; i < entries.size(); ++i) {
+    (*descs)[i] = r->file_entries[entries[i]].d;
+    if (int64_t((*descs)[i].offset) >= 0) (*descs)[i].offset -= lo;
   }
-  const uint8_t* seg = hi > lo ? r->data.data() + lo : nullptr;
-  const uint64_t n = hi - lo;
+  *seg = hi > lo ? r->data.data() + lo : nullptr;
+  *n = hi - lo;
+}
+
+int decode_batch(okv_reader* r, const std::vector<uint32_t>& entries, BatchP* out) {
+  if (!r->ctx) return OKV_R_GPU;
+  const uint32_t nb = uint32_t(entries.size());
+  std::vector<okv_block_desc> descs;
+  const uint8_t* seg;
+  uint64_t n;
+  stage_span(r, entries, &descs, &seg, &n);
   uint64_t rows = 0, kb = 0, vb = 0;
   int rc;
   // a small batch (GetRow's one block) sizes its outputs from bounds (one GPU
@@ -272,11 +282,11 @@ int decode_batch(okv_reader* r, const std::vector<uint32_t>& entries, BatchP* ou
   return OKV_OK;
 }
 
-// ReadBlockWithStat's outcome (segment_reader.go:295-355) for batch entry
-// `slot`: its rows, or the Go error / panic.
-int batch_rows(Batch& B, uint32_t slot, const std::vector<okv_row>** rows) {
-  switch (B.status[slot]) {
-    case OKV_BLK_OK: break;
+// A block's ReadBlockWithStat outcome (segment_reader.go:295-355) as the
+// reader's error: the Go error / panic, or OKV_OK.
+int block_rc(int32_t st) {
+  switch (st) {
+    case OKV_BLK_OK: return OKV_OK;
     case OKV_BLK_EOF: return OKV_R_BLOCK_EOF;
     case OKV_BLK_SHORT: return OKV_R_BLOCK_SHORT;
     case OKV_BLK_PANIC: return OKV_R_PANIC;
@@ -284,6 +294,12 @@ int batch_rows(Batch& B, uint32_t slot, const std::vector<okv_row>** rows) {
     case OKV_BLK_ZSTD_ERROR: return OKV_R_ZSTD;
     default: return OKV_R_GPU;  // (capacity: the plan sized every output)
   }
+}
+
+// ReadBlockWithStat's outcome for batch entry `slot`: its rows, or the Go
+// error / panic.
+int batch_rows(Batch& B, uint32_t slot, const std::vector<okv_row>** rows) {
+  if (const int rc = block_rc(B.status[slot])) return rc;
   if (!B.built[slot]) {
     std::vector<okv_row>& out = B.rows[slot];
     for (uint64_t g = B.row_start[slot]; g < B.row_start[slot + 1]; ++g) {
@@ -416,6 +432,32 @@ int okv_reader_get_row(okv_reader* r, const uint8_t* key, size_t klen, okv_row* 
   }
   const size_t up = upper(r, key, klen);  // DescendLessOrEqual first item (:381-385)
   if (up == 0) return OKV_R_NO_ROWS;
+  const uint32_t e = uint32_t(r->tree[up - 1].file_index);
+  if (r->ctx && !(r->window && r->window_slot[e] >= 0) && r->compression != OKV_COMP_ZSTD) {
+    // ReadBlockWithStat + the row loop (:387-403) in one point-path launch:
+    // only the matching row comes back (found == -1: not a point-path block)
+    std::vector<okv_block_desc> d;
+    const uint8_t* seg;
+    uint64_t n;
+    stage_span(r, {e}, &d, &seg, &n);
+    okv_point_row pr;
+    if (okv_point_get(r->ctx, seg, n, d.data(), r->compression, key, klen, &pr)) return OKV_R_GPU;
+    if (pr.found != -1) {
+      r->io.calls++;
+      r->io.blocks++;
+      r->io.bytes_staged += n;
+      if (const int brc = block_rc(pr.status)) return brc;
+      if (pr.found == 0) return OKV_R_NO_ROWS;  // "did not find row in block"
+      // (valid until the next read call, okv_host.h)
+      r->point_key.assign(pr.key, pr.key + pr.key_len);
+      r->point_val.assign(pr.val, pr.val + pr.val_len);
+      out->key_len = pr.key_len;
+      out->val_len = pr.val_len;
+      out->key = pr.key_len ? r->point_key.data() : nullptr;  // nil (Q4)
+      out->val = pr.val_len ? r->point_val.data() : nullptr;
+      return OKV_OK;
+    }
+  }
   const std::vector<okv_row>* rows = nullptr;
   BatchP keep;
   if ((rc = read_block(r, up - 1, &rows, &keep))) return rc;

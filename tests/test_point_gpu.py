@@ -5,6 +5,8 @@ GetRow's host bloom probe through the product reader
 (segment_reader.go:245-258, :362-404)."""
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -12,6 +14,7 @@ import objectkv_amd as okv
 from objectkv_amd import _lib
 from objectkv_amd import reader as R
 from tests.conftest import descs_of, unpack
+from oracle import coracle as CO
 from tests.test_decode_gpu import _assert_same_as_oracle
 
 pytestmark = pytest.mark.gpu
@@ -238,3 +241,85 @@ def test_getrow_bloom_negative_over_corrupt_block(decoder):
         pr.GetRow(member)
     with pytest.raises(P.GoPanic):
         orr.GetRow(member)
+
+
+def _point_get(decoder, seg, desc, comp, key):
+    """okv_point_get through ctypes: (status, found, key, value)."""
+    L = _lib.lib()
+    buf = np.frombuffer(bytes(seg), np.uint8) if len(seg) else np.zeros(1, np.uint8)
+    d = _lib.BlockDesc(*[int(x) for x in desc])
+    out = _lib.PointRow()
+    kb = bytes(key)
+    rc = L.okv_point_get(decoder._ctx, buf.ctypes.data, len(seg), C.byref(d), comp, kb, len(kb),
+                         C.byref(out))
+    assert rc == 0, decoder.error()
+    k = C.string_at(out.key, out.key_len) if out.found == 1 and out.key_len else b""
+    v = C.string_at(out.val, out.val_len) if out.found == 1 and out.val_len else b""
+    return out.status, out.found, k, v
+
+
+def _expect_get(ref, b, key):
+    """GetRow's row loop (segment_reader.go:395-403) on the oracle's rows of block b."""
+    st = int(ref["status"][b])
+    if st != 0:
+        return st, 0, b"", b""
+    r0, r1 = int(ref["row_start"][b]), int(ref["row_start"][b + 1])
+    ka, va = ref["key_arena"].tobytes(), ref["val_arena"].tobytes()
+    for g in range(r0, r1):
+        ko, kl = int(ref["key_off"][g]), int(ref["key_len"][g])
+        if ka[ko:ko + kl] == bytes(key):
+            vo, vl = int(ref["val_off"][g]), int(ref["val_len"][g])
+            return 0, 1, ka[ko:ko + kl], va[vo:vo + vl]
+    return 0, 0, b"", b""
+
+
+@pytest.mark.parametrize("comp", [_lib.COMP_NONE, _lib.COMP_LZ4])
+def test_point_get_matches_oracle_row_loop(decoder, golden, comp):
+    """okv_point_get (GetRow's block step, one row back) == the oracle's
+    ReadBlockWithStat + bytes.Equal loop: every key of every stageable
+    crafted and writer block (duplicates: the first row), absent keys, the
+    empty key, a key one byte longer, and every block status."""
+    cases = [golden["crafted_edges"]] + [c for c in golden.values()
+                                         if c["kind"] == "writer" and c["compression"] != 2]
+    checked = 0
+    for case in cases:
+        seg = unpack(case["segment_z"])
+        d = descs_of(case)
+        c = comp if case is golden["crafted_edges"] else case["compression"]
+        for b in range(d.shape[0]):
+            ref = CO.decode_soa(seg, CO.descs_array([tuple(int(x) for x in d[b])]), c, False)
+            keys = [b"", b"\x00", b"no-such-key"]
+            r0, r1 = int(ref["row_start"][0]), int(ref["row_start"][1])
+            ka = ref["key_arena"].tobytes()
+            for g in list(range(r0, r1))[:40] + list(range(max(r0, r1 - 5), r1)):
+                ko, kl = int(ref["key_off"][g]), int(ref["key_len"][g])
+                keys += [ka[ko:ko + kl], ka[ko:ko + kl] + b"\x01"]
+            for key in keys:
+                got = _point_get(decoder, seg, d[b], c, key)
+                if got[1] == -1:  # not a point-path block (> 64 KiB, > 1 024 rows, key > 8 KiB)
+                    continue
+                assert got == _expect_get(ref, 0, key), (b, key[:20])
+                checked += 1
+    assert checked > 200
+
+
+def test_point_get_reader_rows_and_fallback(decoder, nopoint):
+    """GetRow through the product reader takes okv_point_get and agrees with a
+    NO_POINT context's reader (full decode + host row loop) on present,
+    duplicate-free and absent keys, values (nil for empty) included; blocks of
+    more than 1 024 rows (tiny records) fall back to the full decode."""
+    from tests.test_reader_gpu import _segment
+    for nrows, vmax in ((3000, 300), (5000, 0)):
+        rows, data, flen, _meta = _segment(nrows=nrows, vmax=vmax)
+        ra = R.SegmentReader(data, flen, decoder)
+        rb = R.SegmentReader(data, flen, nopoint)
+        keys = [k for k, _v in rows[::97]] + [rows[-1][0], b"", b"\xff" * 9, rows[5][0] + b"\x00"]
+        for k in keys:
+            out = []
+            for rd in (ra, rb):
+                try:
+                    kv = rd.GetRow(k)
+                    out.append((kv.Key, kv.Value))
+                except Exception as e:  # noqa: BLE001
+                    out.append(type(e).__name__)
+            assert out[0] == out[1], (k, out)

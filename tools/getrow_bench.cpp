@@ -70,10 +70,18 @@ int main(int argc, char** argv) {
   rows_free_fn oref_free = oref ? (rows_free_fn)dlsym(oref, "oref_rows_free") : nullptr;
   struct Cfg {
     const char* name;
+    int kind;
     uint64_t rows, threshold, block;
-  } cfgs[] = {{"4KiB_blocks", 100000, 3584, 4096}, {"64KiB_blocks", 400000, 57344, 65536}};
+  } cfgs[] = {{"4KiB_blocks", OKV_SYNTH_FIXED, 100000, 3584, 4096},
+              {"64KiB_blocks", OKV_SYNTH_FIXED, 400000, 57344, 65536},
+              // C3-shaped rows (Zipf key 8-256 B, value 0-4096 B): no two
+              // neighbouring records need share a length; keys are the
+              // blocks' FirstKeys (the row loop still walks the whole block)
+              {"64KiB_zipf_blocks", OKV_SYNTH_ZIPF, 0, 57344, 65536}};
   for (const Cfg& c : cfgs) {
-    okv_writer* w = okv_synth_segment(OKV_SYNTH_FIXED, 3, c.rows, 0, c.threshold, c.block);
+    okv_writer* w = c.kind == OKV_SYNTH_FIXED
+                        ? okv_synth_segment(c.kind, 3, c.rows, 0, c.threshold, c.block)
+                        : okv_synth_segment(c.kind, 3, 0, 600, c.threshold, c.block);
     uint64_t dlen = 0;  // (a closed writer)
     const uint8_t* data = okv_writer_data(w, &dlen);
     okv_reader* r = okv_reader_open(ctx, data, dlen, int64_t(dlen));
@@ -82,23 +90,36 @@ int main(int argc, char** argv) {
       return 1;
     }
     std::mt19937_64 rng(7);
+    const uint64_t nblocks = okv_writer_num_blocks(w);
     uint8_t key[16];
+    const uint8_t* kp = key;
+    uint64_t kn = 16;
+    auto pick = [&]() {  // a key of the segment
+      if (c.kind == OKV_SYNTH_FIXED) {
+        key_of(rng() % c.rows, key);
+        kp = key;
+        kn = 16;
+      } else {
+        okv_block_desc d;
+        uint64_t h;
+        okv_writer_block(w, rng() % nblocks, &d, &h, &kp, &kn);
+      }
+    };
     okv_row row;
     for (int i = 0; i < 50; ++i) {  // warm (slab allocation, code objects)
-      key_of(rng() % c.rows, key);
-      okv_reader_get_row(r, key, 16, &row);
+      pick();
+      okv_reader_get_row(r, kp, kn, &row);
     }
     std::vector<double> t;
     okv_reader_io io0, io1;
     okv_reader_io_stats(r, &io0);
     for (int i = 0; i < calls; ++i) {
-      const uint64_t idx = rng() % c.rows;
-      key_of(idx, key);
+      pick();
       const double t0 = now_us();
-      const int rc = okv_reader_get_row(r, key, 16, &row);
+      const int rc = okv_reader_get_row(r, kp, kn, &row);
       t.push_back(now_us() - t0);
-      if (rc || row.key_len != 16 || std::memcmp(row.key, key, 16) != 0) {
-        std::fprintf(stderr, "GetRow(%llu) rc %d\n", (unsigned long long)idx, rc);
+      if (rc || row.key_len != kn || std::memcmp(row.key, kp, kn) != 0) {
+        std::fprintf(stderr, "GetRow rc %d\n", rc);
         return 1;
       }
     }
@@ -109,8 +130,8 @@ int main(int argc, char** argv) {
       double acc[4] = {0, 0, 0, 0};
       const int reps = 50;
       for (int i = 0; i < reps; ++i) {
-        key_of(rng() % c.rows, key);
-        okv_reader_get_row(r, key, 16, &row);
+        pick();
+        okv_reader_get_row(r, kp, kn, &row);
         uint64_t t[5];
         times(t);
         for (int k = 0; k < 4; ++k) acc[k] += double(t[k + 1] - t[0]) / 100.0;
@@ -121,7 +142,7 @@ int main(int argc, char** argv) {
     }
     // the CPU restatement's one-block decode of the same blocks
     std::vector<double> tc;
-    const uint64_t nb = okv_writer_num_blocks(w);
+    const uint64_t nb = nblocks;
     if (oref_read) {
       for (int i = 0; i < calls; ++i) {
         okv_block_desc d;

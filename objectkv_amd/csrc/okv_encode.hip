@@ -58,7 +58,12 @@ constexpr uint32_t kLook = 2048;                 // lookahead rows staged by E3
 constexpr uint32_t kPackRows = 512;              // rows per LDS batch in E10
 constexpr uint64_t kNone = ~uint64_t(0);
 
-constexpr uint32_t kFkCap = 32;  // FirstKey bytes kept per block for the meta kernel
+// Per block, the pack kernel keeps the first kFkStride bytes of the block
+// (u16 key length, u32 value length, then the FirstKey) for the meta kernel:
+// one whole 64-byte line per block (four chunk stores of consecutive lanes;
+// 48-byte entries, partial lines, cost the pack kernel 0.17 ms at C4).
+constexpr uint32_t kFkStride = 64;
+constexpr uint32_t kFkCap = kFkStride - 6;  // FirstKey bytes so kept
 
 struct EncTotals {
   unsigned long long min_size;    // smallest record (6 + k + v)
@@ -97,7 +102,7 @@ struct EncScratch {
   uint64_t* moff = nullptr;      // [nb] meta entry offsets (relative to the meta block)
   uint64_t* orig = nullptr;      // [nb] OriginalSize (the rows' record bytes) of each block
   uint16_t* fkl = nullptr;       // [nb] key length of each block's first row (its FirstKey)
-  uint8_t* fk = nullptr;         // [nb][kFkCap] its first kFkCap bytes (the LDS pack kernel)
+  uint8_t* fk = nullptr;         // [nb][kFkStride] the block's first bytes (the LDS pack kernel)
   size_t cap_blocks = 0;
   uint32_t* jts = nullptr;       // [ntiles][kCutS] level-0 chain table of the tile cut
   uint32_t* jbs = nullptr;
@@ -1041,7 +1046,7 @@ struct PackParams {
   uint8_t* meta;   // non-null: okv_enc_pack_lds_kernel also writes the blocks' meta
                    // index entries (BlockStat.toBytes, block_stat.go:27-42) here
   const uint64_t* moff;  // [nb] entry offsets within the meta block
-  uint8_t* fk = nullptr;  // non-null: the LDS kernel keeps each block's first kFkCap key bytes
+  uint8_t* fk = nullptr;  // non-null: the LDS kernel keeps each block's first kFkStride bytes
 };
 
 struct __align__(16) PackSmem {
@@ -1442,15 +1447,6 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
         hi = m;
     }
     if (kMeta && r == bfirst[lo]) bfkl[lo] = kl;
-    if (P.fk && r == bfirst[lo]) {
-      // the block's first kFkCap key bytes (only the key's own are used), for
-      // the meta kernel -- which otherwise reads the block's first line from
-      // the segment, one scattered line per block (lines just loaded: L2 hits)
-      const Lines5 F = load_lines5(P.key_arena + ko, std::min<uint32_t>(kl, kFkCap));
-      uint4* o = reinterpret_cast<uint4*>(P.fk + (k0 + lo) * kFkCap);
-      o[0] = funnel32(F.l[0], F.l[1], F.s);
-      o[1] = funnel32(F.l[1], F.l[2], F.s);
-    }
     // (the other arms: the row's absolute row-stream position from the row
     // prefix, less the block's -- the region's first row's absolute position
     // abs0 plus the block's region-relative base)
@@ -1503,6 +1499,12 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
       else
         hi = m;
     }
+    // the block's first kFkStride bytes (its first record's header and key),
+    // as stored, for the meta kernel -- which otherwise reads the block's first
+    // line from the segment, one scattered line per block (blocks start
+    // 16-byte aligned in the image: whole chunks; BlockSize >= 48 here)
+    if (P.fk && p < uint32_t(brel[lo]) + kFkStride && p + 16 <= uint32_t(brel[lo]) + blen[lo])
+      *reinterpret_cast<uint4*>(P.fk + (k0 + lo) * kFkStride + (p - uint32_t(brel[lo]))) = v;
     if constexpr (kMeta) {  // FirstKey bytes of the block's meta entry (block_stat.go:31-33)
       const uint32_t ks = uint32_t(brel[lo]) + 6, ke = ks + bfkl[lo];
       const uint32_t a0 = max(p, ks), a1 = min(p + 16, ke);
@@ -1706,9 +1708,9 @@ __global__ __launch_bounds__(kThreads) void okv_enc_meta_kernel(MetaParams P) {
 // Block k's FirstKey (block_stat.go:31-33): the key of its first record.
 __device__ __forceinline__ void first_key(const MetaParams& P, uint64_t k, const Desc& d,
                                           uint32_t& kl, const uint8_t*& key) {
-  if (P.fk && P.fkl[k] <= kFkCap) {
+  if (P.fk && P.fkl[k] <= kFkCap && d.block_size >= kFkStride) {
     kl = P.fkl[k];
-    key = P.fk + k * kFkCap;
+    key = P.fk + k * kFkStride + 6;
   } else if (P.seg) {  // [u16 LE kl][u32 LE vl][key] at the block's start
     const uint8_t* rec = P.seg + d.offset;
     kl = uint32_t(rec[0]) | (uint32_t(rec[1]) << 8);
@@ -1921,7 +1923,7 @@ int ensure_blocks_enc(okv_ctx* ctx, EncScratch* e, uint64_t nb) {
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->moff), c * 8))) return rc;
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->orig), c * 8))) return rc;
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->fkl), c * 2))) return rc;
-    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->fk), c * kFkCap))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->fk), c * kFkStride))) return rc;
     e->cap_blocks = c;
   }
   if (nbt > e->cap_btiles || !e->btile) {

@@ -104,8 +104,8 @@ struct EncScratch {
   uint16_t* fkl = nullptr;       // [nb] key length of each block's first row (its FirstKey)
   uint8_t* fk = nullptr;         // [nb][kFkStride] the block's first bytes (the LDS pack kernel)
   size_t cap_blocks = 0;
-  uint32_t* jts = nullptr;       // [ntiles][kCutS] level-0 chain table of the tile cut
-  uint32_t* jbs = nullptr;
+  uint16_t* jts = nullptr;       // [ntiles][kCutS] level-0 chain table of the tile cut
+  uint16_t* jbs = nullptr;       // (exit offsets <= 256, blocks <= 2 048: 16 bits each)
   uint32_t* tentry = nullptr;    // [ntiles] the tile's entry row, blocks before it
   uint64_t* tkbase = nullptr;
   size_t cap_cut = 0;
@@ -775,7 +775,7 @@ __device__ uint32_t cut_stage(const uint16_t* __restrict__ key_len,
 // the next one, <= kFuseLook) and how many blocks it starts on the way.
 __global__ __launch_bounds__(kThreads) void okv_enc_cut_kernel(
     const uint16_t* __restrict__ key_len, const uint32_t* __restrict__ val_len, uint64_t n,
-    uint64_t T, uint32_t* __restrict__ jts, uint32_t* __restrict__ jbs,
+    uint64_t T, uint16_t* __restrict__ jts, uint16_t* __restrict__ jbs,
     uint64_t* __restrict__ tile_raw, EncTotals* __restrict__ tot) {
   __shared__ CutSmem S;
   const uint64_t cs = uint64_t(blockIdx.x) * kETile;
@@ -819,8 +819,8 @@ __global__ __launch_bounds__(kThreads) void okv_enc_cut_kernel(
   }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < kCutS; j += kThreads) {
-    jts[uint64_t(blockIdx.x) * kCutS + j] = S.c.ex[j];
-    jbs[uint64_t(blockIdx.x) * kCutS + j] = S.c.nb[j];
+    jts[uint64_t(blockIdx.x) * kCutS + j] = uint16_t(S.c.ex[j]);
+    jbs[uint64_t(blockIdx.x) * kCutS + j] = uint16_t(S.c.nb[j]);
   }
   mn = wave_min64(mn);
   bad = wave_min64(bad);
@@ -844,7 +844,7 @@ __global__ __launch_bounds__(kThreads) void okv_enc_cut_kernel(
 // tile made every doubling level 4x larger: 0.69 GB of C4's side traffic.)
 constexpr uint32_t kCutTiles = 4;
 __global__ __launch_bounds__(kThreads) void okv_enc_compose_kernel(
-    const uint32_t* __restrict__ jts, const uint32_t* __restrict__ jbs, uint64_t ntiles,
+    const uint16_t* __restrict__ jts, const uint16_t* __restrict__ jbs, uint64_t ntiles,
     uint64_t nch, uint32_t W, uint32_t* __restrict__ jt, uint32_t* __restrict__ jb) {
   const uint64_t gid = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   const uint64_t c = gid / W, j = gid % W;
@@ -862,7 +862,7 @@ __global__ __launch_bounds__(kThreads) void okv_enc_compose_kernel(
 // Each tile's entry row and the blocks before it, from its chunk's (E6) and
 // the tables of the chunk's tiles before it.
 __global__ __launch_bounds__(kThreads) void okv_enc_tile_entry_kernel(
-    const uint32_t* __restrict__ jts, const uint32_t* __restrict__ jbs,
+    const uint16_t* __restrict__ jts, const uint16_t* __restrict__ jbs,
     const uint32_t* __restrict__ entry, const uint64_t* __restrict__ kbase, uint64_t ntiles,
     uint32_t* __restrict__ tentry, uint64_t* __restrict__ tkbase) {
   const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
@@ -1984,8 +1984,8 @@ int enc_row_prefix(okv_ctx* ctx, EncScratch* e, const DevRows& R, uint64_t T) {
 int ensure_cut(okv_ctx* ctx, EncScratch* e, uint64_t ntiles) {
   int rc;
   if (ntiles * kCutS > e->cap_cut || !e->jts) {
-    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->jts), ntiles * kCutS * 4))) return rc;
-    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->jbs), ntiles * kCutS * 4))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->jts), ntiles * kCutS * 2))) return rc;
+    if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->jbs), ntiles * kCutS * 2))) return rc;
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->tentry), ntiles * 4))) return rc;
     if ((rc = dev_realloc(ctx, reinterpret_cast<void**>(&e->tkbase), ntiles * 8))) return rc;
     e->cap_cut = ntiles * kCutS;

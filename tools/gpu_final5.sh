@@ -54,6 +54,14 @@ if [ "$PART" = a ]; then
   echo "final5 a done"
 else
   [ "$PART" = b2 ] && step bench_driver 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
+  if [ -n "$ENC_AGAIN" ]; then  # encode sources changed after part a: tests + C4 PMC again
+    step enc_tests 600 python -u -m pytest tests/test_encode_gpu.py tests/test_snapshot_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread
+    step pmc_c4 600 "$R/tools/pmc_run.sh" "$T/pmc_c4" bench.py --config c4 --steps 3 --warmup 1 \
+      --no-cpu --no-verify --c4-inflight 1
+    step pmc_c4_sum 60 python3 tools/pmc_summary.py "$O/pmc_c4" "$O/pmc_c4_encode.json" \
+      "{\"source_sha\": \"$ESHA\", \"config\": \"c4\", \"mode\": \"encode\", \"source\": \"gpurun_out/$T/pmc_c4\"}"
+    mkdir -p profiles/r5 && cp "$O/pmc_c4_encode.json" profiles/r5/
+  fi
   step bench_c4 600 python3 bench.py --config c4
   # the zstd stage: its 9 kernels per decode summed (cap, prologue, seq offsets, streams,
   # sequences, executor, general, regrow list, descriptors); untimed: plan, guard, 2 warmup

@@ -17,6 +17,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libokv_sst_ablate.so" if os.environ.get("OKV_ABLATE") == "1"
                         else "libokv_sst_ztrace.so" if os.environ.get("OKV_ZTRACE") == "1"
                         else "libokv_sst.so")
+# OKV_LIB=<path>: another build of the library (A/B runs of two builds on one
+# box, tools/gpu_*ab*.sh); never set by the product or the tests
+if os.environ.get("OKV_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["OKV_LIB"])
 
 # ---- constants (include/okv_sst.h) -------------------------------------------
 OKV_OK, OKV_E_ARG, OKV_E_HIP, OKV_E_CAPACITY, OKV_E_NOMEM, OKV_E_NODEV = 0, -1, -2, -3, -4, -5

@@ -785,17 +785,22 @@ __global__ __launch_bounds__(kThreads) void okv_enc_cut_kernel(
   const uint32_t w_rows = S.W[rows];  // (before the jump tables overwrite W)
   __syncthreads();
   cut_jumps(S, rows);
-  // entries 1..256, one lane each; entry 0 enters the chain of entry nx[0]
+  // entries 1..256, one lane each; entry 0 enters the chain of entry nx[0].
+  // A chain enters this tile at most nx[0] rows in (the block it was in when
+  // it crossed the tile start ends within the first nx[0] rows: bytes of rows
+  // [cs, cs + j - 1) < T), so only those entries are walked; the others are
+  // never reached and get an in-range placeholder.
+  const uint32_t lim = rows ? min(uint32_t(S.nx[0]), kCutS - 1) : 0u;
   {
     const uint32_t j = threadIdx.x + 1;
-    uint32_t pos = j, cnt = 0;
+    uint32_t pos = j > lim ? rows : j, cnt = 0;
     while (pos < rows) {
       const uint32_t j4 = S.c.nx4[pos], j1 = S.nx[pos];
       const bool four = j4 != kNoJump;
       pos += four ? j4 : j1;
       cnt += four ? 4u : 1u;
     }
-    S.c.ex[j] = pos - rows;
+    S.c.ex[j] = j > lim ? 0u : pos - rows;
     S.c.nb[j] = cnt;
   }
   __syncthreads();
@@ -1350,14 +1355,14 @@ __device__ __forceinline__ void lds_copy_field(uint32_t* img, uint32_t d, const 
   }
 }
 
-template <uint32_t IMG, int V = 0, bool kMeta = false>  // V: diagnostic ablation (OKV_ENC_VARIANT 4: no hash,
+template <uint32_t IMG, int V = 0, bool kMeta = false, uint32_t NT = kThreads>  // V: diagnostic ablation (OKV_ENC_VARIANT 4: no hash,
                                    // 5: headers only, 6: loads without LDS writes;
                                    // 7: row positions by a workgroup scan, no pl reads (the product);
                                    // 8: 7 with registers capped for 8 waves)
                                    // kMeta (ablation, OKV_ENC_META_FUSED=1): the meta index
                                    // entries written here too (measured slower: 5.16-5.30
                                    // vs 4.31-4.39 ms pack, + 0.23 ms meta kernel saved)
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(V == 8 ? 8 : 1)))
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(V == 8 ? 8 : 1)))
 void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
   // V == 7, the product form (70 registers, 7 waves per SIMD); V == 8
   // (ablation) is the same code capped at 64 registers for 8 waves: it spills
@@ -1384,7 +1389,7 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
   const Desc dl = P.desc[k0 + g - 1];
   const uint32_t nq = uint32_t((dl.offset + dl.block_size - O0) >> 4);
   if (threadIdx.x <= g) bfirst[threadIdx.x] = frow;
-  for (uint32_t q = threadIdx.x; q < nq; q += kThreads) img4[q] = make_uint4(0, 0, 0, 0);
+  for (uint32_t q = threadIdx.x; q < nq; q += NT) img4[q] = make_uint4(0, 0, 0, 0);
   if (threadIdx.x < 64) {  // g <= kMaxRegion = 64: wave 0
     const uint32_t t = threadIdx.x;
     uint64_t orig = 0;
@@ -1403,12 +1408,12 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
     const uint64_t incl = wave_incl_scan(orig, int(t));
     if (t < g) bbase[t] = incl - orig;
   }
-  __shared__ uint32_t s_wt[2][kThreads / 64];  // VL == 7: per-wave record-size totals
+  __shared__ uint32_t s_wt[2][NT / 64];  // VL == 7: per-wave record-size totals
   __syncthreads();
   const uint64_t R0 = bfirst[0], R1 = bfirst[g];
   const uint64_t abs0 = VL == 7 ? 0 : Pg(P.pl, P.tp, int64_t(R0) - 1);
   uint32_t carry = 0;  // VL == 7: image bytes of the rows before this pass
-  for (uint64_t base = R0; base < R1; base += kThreads) {  // uniform trip count (VL == 7 barriers)
+  for (uint64_t base = R0; base < R1; base += NT) {  // uniform trip count (VL == 7 barriers)
     const uint64_t r = base + threadIdx.x;
     const bool live = r < R1;
     uint32_t kl = 0, vl = 0;
@@ -1424,12 +1429,12 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
       // exclusive scan of the record sizes in row order (< IMG bytes: u32)
       const uint32_t sz = live ? 6 + kl + vl : 0u;
       const uint32_t inc = wave_scan_dpp(sz);
-      const uint32_t wave = threadIdx.x >> 6, par = uint32_t((base - R0) / kThreads) & 1;
+      const uint32_t wave = threadIdx.x >> 6, par = uint32_t((base - R0) / NT) & 1;
       if ((threadIdx.x & 63) == 63) s_wt[par][wave] = inc;
       __syncthreads();
       uint32_t before = carry, tot = 0;
 #pragma unroll
-      for (uint32_t w = 0; w < kThreads / 64; ++w) {
+      for (uint32_t w = 0; w < NT / 64; ++w) {
         const uint32_t t = s_wt[par][w];
         before += w < wave ? t : 0u;
         tot += t;
@@ -1478,7 +1483,7 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
   uint4* dst = reinterpret_cast<uint4*>(P.seg + O0);
   if constexpr (kOverlap) {
     if (threadIdx.x >= 64) {
-      for (uint32_t q = threadIdx.x - 64; q < nq; q += kThreads - 64) dst[q] = img4[q];
+      for (uint32_t q = threadIdx.x - 64; q < nq; q += NT - 64) dst[q] = img4[q];
       return;
     }
   } else {
@@ -1486,7 +1491,7 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
   // are then replaced in place (same lane, so no barrier between) by their two
   // XXH64 round inputs x * PRIME64_2, computed by all 256 lanes: the four
   // hashing lanes per block are left with add, rotate, multiply per round.
-  for (uint32_t q = threadIdx.x; q < nq; q += kThreads) {
+  for (uint32_t q = threadIdx.x; q < nq; q += NT) {
     const uint4 v = img4[q];
     dst[q] = v;
     if (VL == 4) continue;

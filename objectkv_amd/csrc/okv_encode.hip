@@ -170,11 +170,54 @@ __device__ __forceinline__ uint64_t Pg(const uint64_t* __restrict__ pl,
   return i < 0 ? 0 : v;
 }
 
+// v from the lane the DPP control names (id where there is none), 64 bits as
+// two v_mov_dpp: a reduction or scan step without an LDS round trip.
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v, uint64_t id) {
+  const uint32_t lo = __builtin_amdgcn_update_dpp(uint32_t(id), uint32_t(v), kCtrl, kRowMask, 0xf,
+                                                  false);
+  const uint32_t hi = __builtin_amdgcn_update_dpp(uint32_t(id >> 32), uint32_t(v >> 32), kCtrl,
+                                                  kRowMask, 0xf, false);
+  return uint64_t(lo) | (uint64_t(hi) << 32);
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  return uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), l))) |
+         (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), l))) << 32);
+}
+// Wave64 min / max (all lanes active; the result is wave-uniform): row_shr
+// 1, 2, 4, 8 leave each 16-lane row's result in its lane 15.
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
+  v = std::min(v, dpp64<0x111>(v, ~0ull));
+  v = std::min(v, dpp64<0x112>(v, ~0ull));
+  v = std::min(v, dpp64<0x114>(v, ~0ull));
+  v = std::min(v, dpp64<0x118>(v, ~0ull));
+  return std::min(std::min(readlane64(v, 15), readlane64(v, 31)),
+                  std::min(readlane64(v, 47), readlane64(v, 63)));
+}
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
+  v = std::max(v, dpp64<0x111>(v, 0));
+  v = std::max(v, dpp64<0x112>(v, 0));
+  v = std::max(v, dpp64<0x114>(v, 0));
+  v = std::max(v, dpp64<0x118>(v, 0));
+  return std::max(std::max(readlane64(v, 15), readlane64(v, 31)),
+                  std::max(readlane64(v, 47), readlane64(v, 63)));
+}
+// Wave64 inclusive scan of a 64-bit value by DPP (wave_scan_dpp's steps).
+__device__ __forceinline__ uint64_t wave_scan_dpp64(uint64_t x) {
+  x += dpp64<0x111>(x, 0);
+  x += dpp64<0x112>(x, 0);
+  x += dpp64<0x114>(x, 0);
+  x += dpp64<0x118>(x, 0);
+  x += dpp64<0x142, 0xa>(x, 0);  // row_bcast:15
+  x += dpp64<0x143, 0xc>(x, 0);  // row_bcast:31
+  return x;
+}
+
 // Workgroup exclusive scan of one u64 per thread (kThreads threads); also
 // returns the workgroup total.  `sm` holds kThreads/64 + 1 entries.
 __device__ __forceinline__ uint64_t wg_excl_scan(uint64_t v, uint64_t* sm, uint64_t& total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t inc = wave_incl_scan(v, lane);
+  const uint64_t inc = wave_scan_dpp64(v);  // (all lanes active)
   if (lane == 63) sm[wave] = inc;
   __syncthreads();
   uint64_t before = 0, tot = 0;
@@ -199,23 +242,6 @@ __device__ __forceinline__ uint64_t rotl31(uint64_t x) {
 // the accumulator chain is add, rotate, multiply.
 __device__ __forceinline__ uint64_t xround_pre(uint64_t acc, uint64_t xp) {
   return rotl31(acc + xp) * XP1;
-}
-
-__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint64_t o = __shfl_xor(v, d, 64);
-    v = o < v ? o : v;
-  }
-  return v;
-}
-__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint64_t o = __shfl_xor(v, d, 64);
-    v = o > v ? o : v;
-  }
-  return v;
 }
 
 __device__ __forceinline__ uint64_t wave_sum64_u(uint64_t v) {
@@ -543,7 +569,9 @@ __global__ __launch_bounds__(kThreads) void okv_enc_jump0_kernel(const uint32_t*
 __global__ __launch_bounds__(kThreads) void okv_enc_jump_kernel(
     const uint32_t* __restrict__ jt0, const uint32_t* __restrict__ jb0, uint32_t* __restrict__ jt1,
     uint32_t* __restrict__ jb1, uint32_t W, uint64_t nch, uint64_t h, EncTotals* tot) {
-  const uint64_t gid = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  // (the tables hold nch * W < 2^32 entries: 32-bit index arithmetic -- a
+  // 64-bit division by W was most of this kernel's instructions)
+  const uint32_t gid = blockIdx.x * kThreads + threadIdx.x;
   const uint64_t c = gid / W;
   if (c >= nch) return;
   uint32_t e = jt0[gid];
@@ -553,7 +581,7 @@ __global__ __launch_bounds__(kThreads) void okv_enc_jump_kernel(
     e = W - 1;
   }
   if (c + h < nch) {
-    const uint64_t g2 = (c + h) * W + e;
+    const uint32_t g2 = uint32_t(c + h) * W + e;
     jt1[gid] = jt0[g2];
     jb1[gid] = b + jb0[g2];
   } else {
@@ -635,45 +663,15 @@ struct CutSmem {
     uint32_t W[kFuseWin + 1];  // W[m] = record bytes of window rows [0, m) (a window of
                                // 2^32 bytes or more: tot->far, the general kernels)
     struct {                   // okv_enc_cut_kernel, once next(a) is known
-      uint16_t nx4[kETile];    // four blocks on (kNoJump: the chain leaves the tile first)
       uint32_t ex[kCutS];      // per entry: exit offset, blocks started
       uint32_t nb[kCutS];
     } c;
   };
   uint16_t nx[kETile];  // next(a) - a of the tile's rows
-  union {
-    uint16_t kl[kETile];   // their key lengths (okv_enc_emit_tile_kernel)
-    uint16_t nx2[kETile];  // two blocks on (okv_enc_cut_kernel)
-  };
+  uint16_t kl[kETile];  // their key lengths (okv_enc_emit_tile_kernel)
   uint64_t sm[kThreads / 64 + 1];
 };
-static_assert(sizeof(uint16_t) * kETile + 8 * kCutS <= sizeof(uint32_t) * (kFuseWin + 1),
-              "cut tables fit the prefix's LDS");
-constexpr uint16_t kNoJump = 0xffff;
-
-// nx2 / nx4: where the chain from row a is two / four blocks on, when every
-// block of those starts inside the tile (else kNoJump).  A chain walk then
-// takes four blocks per dependent LDS read (49 -> ~15 reads at C4's 42-row blocks).
-__device__ __forceinline__ void cut_jumps(CutSmem& S, uint32_t rows) {
-  for (int i = 0; i < kEItems; ++i) {
-    const uint32_t a = i * kThreads + threadIdx.x;
-    if (a < rows) {
-      const uint32_t b = a + S.nx[a];
-      S.nx2[a] = b < rows ? uint16_t(b - a + S.nx[b]) : kNoJump;
-    }
-  }
-  __syncthreads();
-  for (int i = 0; i < kEItems; ++i) {
-    const uint32_t a = i * kThreads + threadIdx.x;
-    if (a < rows) {
-      const uint32_t x = S.nx2[a];
-      const uint32_t c = a + x;
-      S.c.nx4[a] = x != kNoJump && c < rows && S.nx2[c] != kNoJump ? uint16_t(x + S.nx2[c])
-                                                                  : kNoJump;
-    }
-  }
-  __syncthreads();
-}
+static_assert(8 * kCutS <= sizeof(uint32_t) * (kFuseWin + 1), "cut tables fit the prefix's LDS");
 
 // The tile's window (its rows + kFuseLook lookahead rows): sizes, prefix and
 // next(a) for the tile's rows into S (okv_enc_size_next_kernel's rules).
@@ -782,10 +780,12 @@ __global__ __launch_bounds__(kThreads) void okv_enc_cut_kernel(
   uint64_t mn, bad, wmax;
   bool far;
   const uint32_t rows = cut_stage(key_len, val_len, n, T, cs, S, mn, bad, wmax, far);
-  const uint32_t w_rows = S.W[rows];  // (before the jump tables overwrite W)
+  const uint32_t w_rows = S.W[rows];  // (before the entry tables overwrite W)
   __syncthreads();
-  cut_jumps(S, rows);
-  // entries 1..256, one lane each; entry 0 enters the chain of entry nx[0].
+  // entries 1..256, one lane each, one LDS read per block (tables jumping two
+  // or four blocks per read cost more to build than the walks saved:
+  // profiles/r5/session/enc_cut_dpp_jumps_ab.log); entry 0 enters the chain
+  // of entry nx[0].
   // A chain enters this tile at most nx[0] rows in (the block it was in when
   // it crossed the tile start ends within the first nx[0] rows: bytes of rows
   // [cs, cs + j - 1) < T), so only those entries are walked; the others are
@@ -795,10 +795,8 @@ __global__ __launch_bounds__(kThreads) void okv_enc_cut_kernel(
     const uint32_t j = threadIdx.x + 1;
     uint32_t pos = j > lim ? rows : j, cnt = 0;
     while (pos < rows) {
-      const uint32_t j4 = S.c.nx4[pos], j1 = S.nx[pos];
-      const bool four = j4 != kNoJump;
-      pos += four ? j4 : j1;
-      cnt += four ? 4u : 1u;
+      pos += S.nx[pos];
+      ++cnt;
     }
     S.c.ex[j] = j > lim ? 0u : pos - rows;
     S.c.nb[j] = cnt;
@@ -851,8 +849,8 @@ constexpr uint32_t kCutTiles = 4;
 __global__ __launch_bounds__(kThreads) void okv_enc_compose_kernel(
     const uint16_t* __restrict__ jts, const uint16_t* __restrict__ jbs, uint64_t ntiles,
     uint64_t nch, uint32_t W, uint32_t* __restrict__ jt, uint32_t* __restrict__ jb) {
-  const uint64_t gid = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-  const uint64_t c = gid / W, j = gid % W;
+  const uint32_t gid = blockIdx.x * kThreads + threadIdx.x;  // (< nch * W < 2^32)
+  const uint32_t c = gid / W, j = gid - c * W;
   if (c >= nch) return;
   uint32_t e = uint32_t(j), cnt = 0;
   const uint64_t t1 = std::min<uint64_t>(ntiles, (c + 1) * kCutTiles);
@@ -935,6 +933,7 @@ struct StatParams {
   const uint64_t* orig;   // [nb] OriginalSize (the emit kernels)
   const uint16_t* fkl;    // [nb] FirstKey length
   uint64_t nb, D;
+  uint32_t dshift;  // log2(D) when D is a power of two, else 64
   int lz4;
   Desc* desc;
   uint64_t* bsl;
@@ -962,7 +961,12 @@ __global__ __launch_bounds__(kThreads) void okv_enc_stat_kernel(StatParams P) {
     const uint64_t k = base + i;
     if (k < P.nb) {
       const uint64_t raw = rawv[i];
-      const uint64_t bs = (raw / P.D + 1) * P.D;
+      // (Q2: len + DBS - len % DBS; a power-of-two DBS -- the usual case -- by
+      // shifts, else 32-bit division when both fit: a 64-bit division per
+      // block was most of this kernel's instructions)
+      const uint64_t bs = P.dshift < 64         ? ((raw >> P.dshift) + 1) << P.dshift
+                          : (raw | P.D) >> 32   ? (raw / P.D + 1) * P.D
+                                                : uint64_t(uint32_t(raw) / uint32_t(P.D) + 1) * P.D;
       const uint64_t es = 42u + fklv[i];
       Desc d;
       d.offset = 0;
@@ -2046,6 +2050,8 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   uint32_t levels = 0;
   while ((uint64_t(1) << levels) < nch) ++levels;  // 2^levels >= nch
   const uint64_t lv = nch * W;
+  if (lv >= (uint64_t(1) << 32))  // (the chain-table kernels index with 32 bits)
+    return set_err(ctx, OKV_E_ARG, "encode: too many rows for one call (chain table >= 2^32)");
   if ((rc = ensure_jump(ctx, e, lv * std::max<uint32_t>(levels, 1), nch))) return rc;
   if (tile_cut)
     hipLaunchKernelGGL(okv_enc_compose_kernel, dim3(ceil_div(lv, kThreads)), dim3(kThreads), 0,
@@ -2089,6 +2095,10 @@ int enc_plan(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   sp.fkl = e->fkl;
   sp.nb = nb;
   sp.D = D;
+  sp.dshift = 64;
+  if (D && (D & (D - 1)) == 0)
+    for (sp.dshift = 0; (uint64_t(1) << sp.dshift) != D; ++sp.dshift) {
+    }
   sp.lz4 = o.compression == OKV_COMP_LZ4;
   sp.desc = e->desc;
   sp.bsl = e->bsl;

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Builds an encode A/B variant of the product library: okv_encode.hip with
+# extra defines, linked with the other product objects from objectkv_amd/build,
+# into tools/ab/r5/lib_enc<NAME>.so (the tools/gpu_r5p.sh arms).
+# usage: tools/build_enc_variant.sh NAME [-DFOO=1 ...]
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+N=$1; shift
+B=$R/objectkv_amd/build; D=$R/tools/ab/r5; mkdir -p "$D"
+make -s -C "$R/objectkv_amd/csrc" >/dev/null
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I"$R/include" "$@" \
+  -c "$R/objectkv_amd/csrc/okv_encode.hip" -o "$D/enc_$N.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$D/lib_enc$N.so" \
+  "$B/okv_decode.o" "$D/enc_$N.o" "$B/okv_zstd.o" "$B/okv_merge.o" "$B/okv_host.o" "$B/okv_reader.o"
+echo "built $D/lib_enc$N.so"

@@ -4,7 +4,7 @@
 # (tools/ab/r5/lib_encA.so = before, lib_encB.so = after), C4 line alternating.
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r5p; mkdir -p $O
+O=gpurun_out/${AB_TAG:-r5p}; mkdir -p $O
 step() {
   local n=$1 s=$2; shift 2
   timeout -k 10 "$s" "$@" > "$O/$n.log" 2>&1

@@ -790,13 +790,35 @@ __global__ __launch_bounds__(kThreads) void okv_enc_cut_kernel(
   // it crossed the tile start ends within the first nx[0] rows: bytes of rows
   // [cs, cs + j - 1) < T), so only those entries are walked; the others are
   // never reached and get an in-range placeholder.
-  const uint32_t lim = rows ? min(uint32_t(S.nx[0]), kCutS - 1) : 0u;
+  const uint32_t L0 = rows ? S.nx[0] : 1u;
+  const uint32_t lim = rows ? min(L0, kCutS - 1) : 0u;
+  // A tile whose blocks all have one row count L (fixed-size rows, C4) needs
+  // no walks: the chain from j starts ceil((rows - j) / L) blocks here.
+  bool eq = true;
+  {
+    const uint32_t a0 = threadIdx.x * kEItems;
+    const uint32_t* n32 = reinterpret_cast<const uint32_t*>(S.nx + a0);
+#pragma unroll
+    for (int i = 0; i < kEItems / 2; ++i) {
+      const uint32_t v = n32[i];
+      if (a0 + 2 * i < rows) eq &= (v & 0xffffu) == L0;
+      if (a0 + 2 * i + 1 < rows) eq &= (v >> 16) == L0;
+    }
+  }
+  const bool uni = __syncthreads_and(eq);
   {
     const uint32_t j = threadIdx.x + 1;
     uint32_t pos = j > lim ? rows : j, cnt = 0;
-    while (pos < rows) {
-      pos += S.nx[pos];
-      ++cnt;
+    if (uni) {
+      if (pos < rows) {
+        cnt = (rows - pos + L0 - 1) / L0;
+        pos += cnt * L0;
+      }
+    } else {
+      while (pos < rows) {
+        pos += S.nx[pos];
+        ++cnt;
+      }
     }
     S.c.ex[j] = j > lim ? 0u : pos - rows;
     S.c.nb[j] = cnt;
@@ -895,15 +917,28 @@ __global__ __launch_bounds__(kThreads) void okv_enc_emit_tile_kernel(
   uint64_t mn, bad, wmax;
   bool far;
   const uint32_t rows = cut_stage(key_len, val_len, n, T, cs, S, mn, bad, wmax, far);
-  // (lane 0 walks the chain; a four-block jump table and a parallel expansion
-  // measured slower: 504 vs 370 us per C4 launch)
-  if (threadIdx.x == 0) {
+  // Wave 0 walks the chain from the tile's entry row, speculating on runs of
+  // equal block lengths: with L = next(pos) - pos, lane j reads next() at
+  // pos + j L; the lanes before the first whose block length differs (or that
+  // is past the tile) are confirmed block starts -- up to 64 per round of two
+  // LDS reads, one per round where every block differs.  (A four-block jump
+  // table and a parallel expansion measured slower: 504 vs 370 us per C4
+  // launch; so did a 64-row ballot search per block.)
+  if (threadIdx.x < 64) {
+    const uint32_t lane = threadIdx.x;
     uint32_t pos = entry[c], m = 0;
     while (pos < rows) {
-      starts[m++] = uint16_t(pos);
-      pos += S.nx[pos];
+      const uint32_t L = S.nx[pos];
+      const uint32_t q = pos + lane * L;
+      const bool in = q < rows;
+      const uint32_t lq = S.nx[in ? q : 0u];
+      const uint64_t brk = __ballot(!in || lq != L);
+      const uint32_t k = brk ? uint32_t(__builtin_ctzll(brk)) : 64u;  // >= 1: lane 0 is pos
+      if (lane < k) starts[m + lane] = uint16_t(q);
+      m += k;
+      pos += k * L;
     }
-    s_m = m;
+    if (lane == 0) s_m = m;
   }
   __syncthreads();
   const uint32_t m = s_m;

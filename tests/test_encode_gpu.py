@@ -374,6 +374,28 @@ def test_multi_chunk_encode(enc, T, vmax):
     assert got2.seg.tobytes() == got.seg.tobytes()
 
 
+@pytest.mark.parametrize("T", [14, 40, 3584, 5000])
+def test_tile_cut_uniform_tiles(enc, T):
+    """Tiles whose blocks all hold one row count (fixed 20-byte records: 1,
+    2, 180 and 250 rows per block): the cut kernel's arithmetic chains and the
+    emit kernel's speculated walk, beside a variable-size stretch (the walks)
+    and a short last block -- byte-equal to the oracle writer."""
+    rng = random.Random(T)
+    rows = [(b"%08d" % i, bytes([i & 255]) * (rng.randint(0, 12) if 12000 <= i < 13000 else 6))
+            for i in range(30001)]
+    rc, want, meta = oracle_segment(rows, T, 4096)
+    got = enc.encode(rows, T, 4096, strict_go=rc == 0)
+    if rc == 0:
+        assert got.seg.tobytes() == want
+        assert got.meta() == meta
+    else:  # the last row closed a block (Q1): compare with the host writer's footer
+        hw = okv.SegmentWriter(T, 4096, 0, False)
+        for k, v in rows:
+            hw.WriteRow(k, v)
+        hw.Close(strict_go=False)
+        assert got.seg.tobytes() == hw.data().tobytes()
+
+
 @pytest.mark.parametrize("T", [60, 3584, 4400, 5200, 20000])
 def test_tile_cut_boundaries_and_general_path(enc, T):
     """The greedy cut across many 2048-row tiles (okv_enc_cut_kernel /

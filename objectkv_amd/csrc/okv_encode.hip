@@ -1128,10 +1128,13 @@ __device__ __forceinline__ uint4 replace_from(const uint4& acc, const uint4& v, 
 __device__ __forceinline__ uint4 seg_window(const uint8_t* src, int64_t s, int64_t e) {
   const int64_t lo = s > 0 ? s : 0;
   const int64_t hi = e < 16 ? e : 16;
-  const uintptr_t v = reinterpret_cast<uintptr_t>(src) - uintptr_t(s);  // window byte 0
-  const uintptr_t a = v & ~uintptr_t(15);
-  const uint32_t sh = uint32_t(v & 15);
-  const uintptr_t safe = (v + uintptr_t(lo)) & ~uintptr_t(15);
+  // (pointer arithmetic, not integer casts: the loads keep the arena's global
+  // address space -- global_load, not flat_load, which also counts against
+  // lgkmcnt and so holds up every LDS wait behind it)
+  const uint8_t* v = src - s;  // window byte 0
+  const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(v) & 15);
+  const uint8_t* a = v - sh;
+  const uint8_t* safe = v + lo - (reinterpret_cast<uintptr_t>(v + lo) & 15);
   const bool n0 = int64_t(16 - sh) > lo;
   const bool n1 = sh != 0 && hi > int64_t(16 - sh);
   const uint4 x = *reinterpret_cast<const uint4*>(n0 ? a : safe);
@@ -1361,9 +1364,8 @@ struct Lines5 {
 };
 __device__ __forceinline__ Lines5 load_lines5(const uint8_t* src, uint32_t len) {
   Lines5 L;
-  const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
-  const uint4* line = reinterpret_cast<const uint4*>(sa & ~uintptr_t(15));
-  L.s = uint32_t(sa & 15);
+  L.s = uint32_t(reinterpret_cast<uintptr_t>(src) & 15);
+  const uint4* line = reinterpret_cast<const uint4*>(src - L.s);  // (global_load: seg_window)
   L.nwin = (len + 15) >> 4;
   const uint32_t nline = (L.s + len + 15) >> 4;
 #pragma unroll

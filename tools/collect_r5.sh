@@ -14,7 +14,7 @@ done
 for f in pmc_c3_full.json pmc_c4_encode.json trace_c3.json trace_cz.json; do
   [ -f $S/$f ] && cp $S/$f $D/
 done
-for t in trace_c3 trace_cz; do
+for t in trace_c3 trace_cz trace_c4; do
   k=$(find $S/$t -name 'run_kernel_stats.csv' 2>/dev/null | head -1)
   [ -n "$k" ] && cp "$k" $D/${t}_kernel_stats.csv
 done

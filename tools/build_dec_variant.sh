@@ -1,0 +1,16 @@
+#!/bin/bash
+# Builds a decode A/B variant of the product library: okv_decode.hip (or the
+# file given by DEC_SRC) with extra defines, linked with the other product
+# objects from objectkv_amd/build, into tools/ab/r5/lib_dec<NAME>.so.
+# usage: [DEC_SRC=path] tools/build_dec_variant.sh NAME [-DFOO=1 ...]
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+N=$1; shift
+B=$R/objectkv_amd/build; D=$R/tools/ab/r5; mkdir -p "$D"
+SRC=${DEC_SRC:-$R/objectkv_amd/csrc/okv_decode.hip}
+make -s -C "$R/objectkv_amd/csrc" >/dev/null
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I"$R/include" \
+  -I"$R/objectkv_amd/csrc" "$@" -c "$SRC" -o "$D/dec_$N.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$D/lib_dec$N.so" \
+  "$D/dec_$N.o" "$B/okv_encode.o" "$B/okv_zstd.o" "$B/okv_merge.o" "$B/okv_host.o" "$B/okv_reader.o"
+echo "built $D/lib_dec$N.so"

@@ -1532,9 +1532,12 @@ void okv_enc_pack_lds_kernel(PackParams P, uint64_t nb, uint32_t G) {
   // are then replaced in place (same lane, so no barrier between) by their two
   // XXH64 round inputs x * PRIME64_2, computed by all 256 lanes: the four
   // hashing lanes per block are left with add, rotate, multiply per round.
+  // (non-temporal stores: the segment is written once and read by no kernel
+  // of this encode -- pack 4.53-4.55 -> 4.44-4.47 ms, profiles/r5/session/
+  // enc_pack_nt_ab.log; non-temporal arena loads as well: 4.82-4.84 ms)
   for (uint32_t q = threadIdx.x; q < nq; q += NT) {
     const uint4 v = img4[q];
-    dst[q] = v;
+    store_nt16(&dst[q], v);
     if (VL == 4) continue;
     const uint32_t p = q << 4;
     uint32_t lo = 0, hi = g;  // block holding byte p

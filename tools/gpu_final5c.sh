@@ -21,5 +21,6 @@ step pmc_c4_sum 60 python3 tools/pmc_summary.py "$O/pmc_c4" "$O/pmc_c4_encode.js
 mkdir -p profiles/r5 && cp "$O/pmc_c4_encode.json" profiles/r5/
 step bench_c4 600 python3 bench.py --config c4
 step trace_c4 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c4 -o run -- python3 bench.py --config c4 --steps 3 --warmup 1 --no-cpu --c4-inflight 1 --no-verify
+step bench_cm 600 python3 bench.py --config cm
 step bench_driver 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
 echo "final5c done"

@@ -7,7 +7,12 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 N=$1; shift
 B=$R/objectkv_amd/build; D=$R/tools/ab/r5; mkdir -p "$D"
-make -s -C "$R/objectkv_amd/csrc" >/dev/null
+# (no make here: the working tree may hold the variant's source, and make would
+# rebuild the product library from it; the other objects come from the last
+# product build)
+for o in okv_decode okv_encode okv_zstd okv_merge okv_host okv_reader; do
+  [ -f "$B/$o.o" ] || { echo "missing $B/$o.o: run make -C objectkv_amd/csrc first" >&2; exit 1; }
+done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -I"$R/include" "$@" \
   -c "$R/objectkv_amd/csrc/okv_encode.hip" -o "$D/enc_$N.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$D/lib_enc$N.so" \

@@ -289,8 +289,8 @@ def main():
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the oracle comparison of the bench outputs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--c4-inflight", type=int, default=2,
-                    help="c4: segments in flight (Close of one overlaps the next's kernels)")
+    ap.add_argument("--c4-inflight", type=int, default=3,
+                    help="c4: segments in flight (the Closes of two overlap the next's kernels)")
     ap.add_argument("--decode-inflight", type=int, default=None,
                     help="decode configs: whole-segment decodes in flight, each on its own "
                          "context, stream, segment copy and output buffers (later decodes' "

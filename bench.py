@@ -230,7 +230,7 @@ class Dist:
         torch.cuda.set_device(self.local)
         self.dev = torch.device("cuda", self.local)
         self.dist = None
-        if self.world > 1:
+        if self.world > 1 or getattr(args, "dist_always", False):
             import torch.distributed as dist
             if self.backend == "nccl":
                 dist.init_process_group("nccl", device_id=self.dev)
@@ -299,8 +299,17 @@ def main():
                          "others (C2 at 4: 48.3 vs 55.3 GiB/s; DESIGN.md 13.11)")
     ap.add_argument("--e2e", action="store_true",
                     help="also time the pinned, pipelined host-buffer path (PCIe both ways)")
-    ap.add_argument("--dist-backend", default="nccl",
-                    help="control-plane backend (barrier, max time); gloo for rehearsals")
+    ap.add_argument("--dist-backend", default="gloo",
+                    help="control-plane backend (barrier, gather of the ranks' times).  The "
+                         "data path has no collective (each rank owns its segments), so the "
+                         "default keeps the control plane on the host: gloo, after "
+                         "torch.cuda.synchronize.  nccl (RCCL) is covered by "
+                         "tests/test_bench_gpu.py::test_rccl_control_plane_world1")
+    ap.add_argument("--pass3-chain", choices=["auto", "on", "off"], default="auto",
+                    help="decodes in flight: chain each pass 3 behind the previous decode's "
+                         "(auto: large uncompressed blocks)")
+    ap.add_argument("--dist-always", action="store_true",
+                    help="initialise the process group at world size 1 too (tests)")
     ap.add_argument("--device-mod", type=int, default=0,
                     help="rehearsal only: map LOCAL_RANK -> LOCAL_RANK %% N (ranks share a GPU)")
     args = ap.parse_args()
@@ -465,6 +474,8 @@ def run_decode(args, torch, okv, D):
     # for large blocks: small-block and zstd decodes are latency-bound and gain
     # from running side by side.
     chained = inflight > 1 and bs >= 32768 and kind != "zstd"
+    if args.pass3_chain != "auto":
+        chained = inflight > 1 and args.pass3_chain == "on"
     if chained:
         for i in range(inflight):
             decs[i].chain(decs[i - 1])

@@ -242,7 +242,11 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
   // reads every total with sc1 loads.  Round 4 made the add a release and
   // the last adder acquire: an L2 write-back per workgroup of the ~66 KB of
   // record table each has just written -- 6.5 us more per C3 count (A/B,
-  // profiles/r5/session/ab_count_arrival.log), and not needed by this row.
+  // profiles/r5/session/ab_count_arrival.log).  The totals travel write-
+  // through (sc1 stores, drained before the add), so no producer needs a
+  // release; the last adder still takes an agent-scope acquire before its
+  // loads (one L1 invalidate, in one workgroup), so the loads are ordered
+  // after the add by the memory model, not only by the sc1 load path.
   __shared__ uint32_t s_last;
   if (tid == kThreads - 1) {
     const Prefix t{inc[0] + v[0], inc[1] + v[1], inc[2] + v[2], inc[3] + v[3]};
@@ -266,6 +270,7 @@ __global__ __launch_bounds__(kThreads) void okv_count_kernel(
   }
   __syncthreads();
   if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // the last workgroup: exclusive scan of gridDim.x tile totals, 256 at a time
   // (from the totals of the blocks before this launch's, for a decode in pieces)
   uint64_t carry[4] = {0, 0, 0, 0};
@@ -688,7 +693,10 @@ __device__ __noinline__ uint4 tile_chunk_pieces(const uint8_t* seg, uint64_t seg
 // (The measured alternatives -- other tile sizes and widths, phase probes,
 // per-chunk lookups, direct global loads -- are tile_pass_diag in
 // okv_decode_ablate.inc, ablation build only.)
-template <uint32_t kT, uint32_t kNT, bool kXcd>
+// kSkip (ablation build only, okv_tile_kernel_skip): output classes left
+// unwritten, to attribute the pass's HBM write traffic -- 1 the SoA row index,
+// 2 value runs, 4 key chunks, 8 boundary value chunks, 16 partial chunks.
+template <uint32_t kT, uint32_t kNT, bool kXcd, uint32_t kSkip = 0>
 __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uint32_t ntile) {
   constexpr uint32_t kG = kT / 64 + 8;  // 64-byte destination granules of the key range
   __shared__ TileRows<kT> R;
@@ -884,7 +892,7 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
   __syncthreads();
   if (t == 0 && tid < 64) {  // the block outputs and SoA row index (from the LDS tables)
     block_outputs();
-    if (lane < rows) {
+    if (!(kSkip & 1) && lane < rows) {
       const uint64_t g = row0 + lane;
       const uint32_t kp = R.pre[0][lane], vp = R.pre[1][lane];
       P.key_len[g] = uint16_t(R.pre[0][lane + 1] - kp);
@@ -900,7 +908,7 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
     // value runs: one unit of <= 64 whole chunks of one row per wave iteration
     const uint32_t nunit = R.nunit, nbnd = R.nbnd;
     uint8_t* const varena = P.val_arena + vb0;
-    for (uint32_t u = tid >> 6; u < nunit; u += kNT / 64) {
+    for (uint32_t u = tid >> 6; u < ((kSkip & 2) ? 0u : nunit); u += kNT / 64) {
       const uint32_t c0 = __builtin_amdgcn_readfirstlane(R.unit[0][u]);
       const uint32_t sbyte = __builtin_amdgcn_readfirstlane(R.unit[1][u]);
       const uint32_t cnt = __builtin_amdgcn_readfirstlane(R.unit[2][u]);
@@ -913,6 +921,8 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
     // keys and the boundary value chunks: per-lane lookup
     for (uint32_t j = tid; j < nk + nbnd; j += kNT) {
       const uint32_t reg = j >= nk;
+      if ((kSkip & 4) && !reg) continue;
+      if ((kSkip & 8) && reg) continue;
       const uint32_t bv = reg ? R.bnd[j - nk] : 0u;
       if (reg && j > nk && (bv >> 8) == (R.bnd[j - nk - 1] >> 8)) continue;
       const uint32_t X0 = reg ? vx0 : kx0, X1 = reg ? vx1 : kx1;
@@ -935,7 +945,7 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
       }
       if (lo == x && hi == x + 16)
         *reinterpret_cast<uint4*>(dst) = out;
-      else
+      else if (!(kSkip & 16))
         store_partial(dst, out, lo - x, hi - x);
     }
   }
@@ -1061,6 +1071,13 @@ __device__ __forceinline__ void publish(uint32_t* f, Prefix* slot, const Prefix&
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(f, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void publish_payload(Prefix* slot, const Prefix& v) {
+  __hip_atomic_store(&slot->rows, v.rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&slot->kb, v.kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&slot->vb, v.vb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&slot->bad, v.bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 __device__ __forceinline__ uint32_t flag_peek(const uint32_t* f) {
   return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1085,17 +1102,46 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 // kernel (okv_decode_ablate_lb.inc); declared here, defined only there.
 __device__ Prefix fused_prefix_lookback(const CopyParams& P, const FusedParams& F, uint32_t b,
                                         uint32_t lane, uint32_t tag, const Prefix& mine);
+#ifdef OKV_ABLATE
+// (ablation build: wall-clock stamps of the fused kernel's phases per block --
+// start, staged, walked, prefix known, done; okv_debug_fused_times)
+__device__ uint64_t g_fused_t[kFusedMaxBlocks * 8];
+#define OKV_FUSED_STAMP(i) \
+  if (lane == 0 && b < kFusedMaxBlocks) g_fused_t[b * 8 + (i)] = wall_clock64()
+#else
+#define OKV_FUSED_STAMP(i)
+#endif
+
+// The fused kernel's look-back word per block: (epoch | 1 << 31) << 32 | its
+// counts packed in 30 bits -- rows (10), padded key bytes / 16 (9), padded
+// value bytes / 16 (9), failed (1), overflow (1: the counts do not fit and
+// are in F.agg[b], published before the word).  One 8-byte write-through
+// store is the payload and the flag at once.
+__device__ __forceinline__ bool fused_pack(const Prefix& v, uint32_t& w) {
+  if (v.rows >= 1024 || v.kb >= (512u << 4) || v.vb >= (512u << 4)) return false;
+  w = uint32_t(v.rows) | uint32_t(v.kb >> 4) << 10 | uint32_t(v.vb >> 4) << 19 |
+      uint32_t(v.bad) << 28;
+  return true;
+}
+
 template <bool kLB>  // (kLB: the ablation build's stream kernel only)
 __device__ __forceinline__ void fused_pass(const CopyParams& P, const FusedParams& F) {
   __shared__ GatherSmem sm;
   __shared__ uint4 stage[kSmallStage / 16 + 4];
-  __shared__ uint32_t s_b;
   const uint32_t lane = threadIdx.x;
-  if (lane == 0) s_b = uint32_t(atomicAdd(F.ctr, 1ull) - F.base);
-  __syncthreads();
-  const uint32_t b = s_b;
-  if (b >= P.nblk) return;
+  uint32_t b = blockIdx.x;
+  if constexpr (kLB) {  // blocks by arrival (the stream kernel's grid is not resident)
+    __shared__ uint32_t s_b;
+    if (lane == 0) s_b = uint32_t(atomicAdd(F.ctr, 1ull) - F.base);
+    __syncthreads();
+    b = s_b;
+    if (b >= P.nblk) return;
+  }
+  // (the product grid is all resident -- a quarter of the device's capacity
+  // -- and dispatched in index order, so a block waits only on lower indices
+  // that have started: no block-index counter)
   const uint32_t tag = F.epoch << 2;
+  OKV_FUSED_STAMP(0);
   if (b == 0 && lane == 0) *F.big_zero = 0;
   // ---- pass 1 for this block (okv_count_kernel's rules) ----
   const Desc d = P.descs[b];
@@ -1121,85 +1167,153 @@ __device__ __forceinline__ void fused_pass(const CopyParams& P, const FusedParam
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  __syncthreads();
+  OKV_FUSED_STAMP(1);
   const StageWin lsrc{stage, 16 + shift};
   uint64_t rows = 0, kb = 0, vb = 0, p = 0;
-  if (lane == 0 && st == OKV_BLK_OK) {
-    const uint64_t orig = go_walk_bound(d.original_size);
-    while (p < orig) {  // :340
-      if (len - p < 6) { st = OKV_BLK_PANIC; break; }  // :342-345
+  if (st == OKV_BLK_OK && staged) {
+    // The walk by the whole wave on a wave-uniform position, run-length
+    // speculated (okv_point_kernel's walk): from a record at p of length rl,
+    // lane j reads the header at p + j rl -- a record start if every record
+    // before it was rl long; the first lane that breaks the run (past
+    // OriginalSize, a failed check, another length) is itself a true record
+    // start.  A round of two dependent LDS reads confirms 2 to 64 records
+    // (C2's fixed 86-byte records: all 42 in one round); lane 0 alone paid
+    // one dependent header decode per record.
+    const uint32_t L = uint32_t(len);  // <= kSmallStage
+    const uint32_t o32 = __builtin_amdgcn_readfirstlane(
+        uint32_t(min<uint64_t>(go_walk_bound(d.original_size), 0xffffffffull)));  // (:340)
+    uint32_t pp = 0, nr = 0;
+    while (pp < o32) {  // :340
       uint32_t kl, vl;
-      if (staged) lsrc.header(uint32_t(p), kl, vl);
-      else header_global(P.seg, d.offset + p, kl, vl);
-      const uint64_t room = len - p - 6;
-      if (kl > room || vl > room - kl) { st = OKV_BLK_PANIC; break; }  // :346-349
-      if (rows < kRCap) sm.rec[rows] = uint32_t(p);
-      rows++;
-      kb += kl;
-      vb += vl;
-      p += 6 + uint64_t(kl) + uint64_t(vl);
+      lsrc.header(min(pp, L), kl, vl);  // (one address: a broadcast)
+      kl = __builtin_amdgcn_readfirstlane(kl);
+      vl = __builtin_amdgcn_readfirstlane(vl);
+      const uint32_t room = L - pp - 6;
+      // u16/u32 reads (:342-345), key/value reads (:346-349)
+      if (!((L - pp >= 6) & (kl <= room) & (vl <= room - kl))) {
+        st = OKV_BLK_PANIC;
+        break;
+      }
+      const uint32_t rl = 6 + kl + vl;
+      const uint32_t q = pp + lane * rl;  // (< 64 * 10 KiB)
+      uint32_t kj, vj;
+      lsrc.header(min(q, L), kj, vj);
+      const uint32_t rj = L - q - 6;
+      const bool okj = (q <= L) & (L - q >= 6) & (kj <= rj) & (vj <= rj - kj);
+      // (the run is of equal headers, not only equal lengths: the counts add
+      // m key and value lengths)
+      const bool brk = lane >= 1 && (q >= o32 || !okj || kj != kl || vj != vl);
+      const uint64_t bm = __ballot(brk);
+      const uint32_t m = bm ? uint32_t(__builtin_ctzll(bm)) : 64u;  // (>= 1)
+      if (lane < m && nr + lane < uint32_t(kRCap)) sm.rec[nr + lane] = q;
+      nr += m;
+      kb += uint64_t(m) * kl;
+      vb += uint64_t(m) * vl;
+      pp += m * rl;  // the breaking lane's position: a true record start
+      if (m == 64 || pp >= o32) continue;
+      const uint32_t okm = __builtin_amdgcn_readlane(uint32_t(okj), m);
+      const uint32_t km = __builtin_amdgcn_readlane(kj, m), vm = __builtin_amdgcn_readlane(vj, m);
+      if (!okm) {
+        st = OKV_BLK_PANIC;
+        break;
+      }
+      if (lane == 0 && nr < uint32_t(kRCap)) sm.rec[nr] = pp;
+      ++nr;
+      kb += km;
+      vb += vm;
+      pp += 6 + km + vm;
     }
+    rows = nr;
+    p = pp;
     if (st != OKV_BLK_OK) rows = kb = vb = 0;
+  } else if (st == OKV_BLK_OK) {  // not stageable: lane 0 walks the headers in HBM
+    if (lane == 0) {
+      const uint64_t orig = go_walk_bound(d.original_size);
+      while (p < orig) {  // :340
+        if (len - p < 6) { st = OKV_BLK_PANIC; break; }  // :342-345
+        uint32_t kl, vl;
+        header_global(P.seg, d.offset + p, kl, vl);
+        const uint64_t room = len - p - 6;
+        if (kl > room || vl > room - kl) { st = OKV_BLK_PANIC; break; }  // :346-349
+        if (rows < kRCap) sm.rec[rows] = uint32_t(p);
+        rows++;
+        kb += kl;
+        vb += vl;
+        p += 6 + uint64_t(kl) + uint64_t(vl);
+      }
+      if (st != OKV_BLK_OK) rows = kb = vb = 0;
+    }
+    st = __shfl(st, 0, 64);
+    rows = __shfl(rows, 0, 64);
+    kb = __shfl(kb, 0, 64);
+    vb = __shfl(vb, 0, 64);
+    p = __shfl(p, 0, 64);
   }
   __syncthreads();  // the walk's record positions (sm.rec) are read by every lane below
-  st = __shfl(st, 0, 64);
-  rows = __shfl(rows, 0, 64);
-  kb = __shfl(kb, 0, 64);
-  vb = __shfl(vb, 0, 64);
-  p = __shfl(p, 0, 64);
+  OKV_FUSED_STAMP(2);
   const Prefix mine{rows, round16(kb), round16(vb), uint64_t(st != OKV_BLK_OK)};
   Prefix ex{0, 0, 0, 0};
   if constexpr (kLB) {
     ex = fused_prefix_lookback(P, F, b, lane, tag, mine);  // ablation build only
   } else {
-  // ---- pass 2: the last block to arrive scans every block's counts ----
-  // (every block of the grid is resident: the fused form runs for small
-  // batches only, kFusedMaxBlocks << the chip's resident capacity)
-  uint32_t last_arrival = 0;
-  if (lane == 0) {
-    publish(&F.flag[b], &F.agg[b], mine, tag | 1u);  // sc1 payload, drained, then the flag
-    last_arrival = uint32_t(atomicAdd(F.arr, 1ull) - F.base) == P.nblk - 1;
-  }
-  if (__shfl(last_arrival, 0, 64)) {
-    // exclusive scan over all blocks, 64 at a time (sc1 loads: the adds that
-    // came before ours each followed their block's drained sc1 stores)
-    Prefix carry{0, 0, 0, 0};
-    for (uint32_t c0 = 0; c0 < P.nblk; c0 += 64) {
-      const uint32_t k = c0 + lane;
-      const Prefix v = k < P.nblk ? prefix_peek(&F.agg[k]) : Prefix{0, 0, 0, 0};
-      const uint64_t ir = wave_incl_scan(v.rows, lane), ik = wave_incl_scan(v.kb, lane);
-      const uint64_t iv = wave_incl_scan(v.vb, lane), ib = wave_incl_scan(v.bad, lane);
-      if (k < P.nblk)
-        __hip_atomic_store(&F.incl[k].rows, carry.rows + ir - v.rows, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      const Prefix ex_k{carry.rows + ir - v.rows, carry.kb + ik - v.kb, carry.vb + iv - v.vb,
-                        carry.bad + ib - v.bad};
-      if (k < P.nblk) {
-        __hip_atomic_store(&F.incl[k].kb, ex_k.kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&F.incl[k].vb, ex_k.vb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&F.incl[k].bad, ex_k.bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      carry.rows += __shfl(ir, 63, 64);
-      carry.kb += __shfl(ik, 63, 64);
-      carry.vb += __shfl(iv, 63, 64);
-      carry.bad += __shfl(ib, 63, 64);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (uint32_t k = lane; k < P.nblk; k += 64)
-      __hip_atomic_store(&F.flag[k], tag | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- pass 2: each block sums its predecessors' published counts ----
+    // One write-through 8-byte word per block carries its counts and the
+    // call's tag (fused_pack); every lane loads the words of up to
+    // kFusedMaxBlocks / 64 predecessors at once and re-polls only those not
+    // yet published.  (Round 5: the last block to arrive scanned every
+    // block's counts and published the prefixes behind a second flag -- a
+    // chain of dependent cross-XCD trips that every block waited out.)
+    uint64_t* word = reinterpret_cast<uint64_t*>(F.flag);
+    const uint32_t want = F.epoch | 0x80000000u;
     if (lane == 0) {
-      *F.tot = Totals{carry.rows, carry.kb, carry.vb, carry.bad};
-      P.row_start[P.nblk] = carry.rows;
+      uint32_t w = 0;
+      if (!fused_pack(mine, w)) {
+        publish_payload(&F.agg[b], mine);  // sc1 stores, drained
+        w = 1u << 29;
+      }
+      __hip_atomic_store(&word[b], uint64_t(want) << 32 | w, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    constexpr uint32_t kU = kFusedMaxBlocks / 64;
+    uint64_t wv[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t k = lane + 64 * u;
+      wv[u] = k < b ? __hip_atomic_load(&word[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : uint64_t(want) << 32;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t k = lane + 64 * u;
+      while (uint32_t(wv[u] >> 32) != want) {
+        __builtin_amdgcn_s_sleep(1);
+        wv[u] = __hip_atomic_load(&word[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const uint32_t w = uint32_t(wv[u]);
+      if (w >> 29 & 1u) {
+        const Prefix o = prefix_peek(&F.agg[k]);
+        ex.rows += o.rows;
+        ex.kb += o.kb;
+        ex.vb += o.vb;
+        ex.bad += o.bad;
+      } else {
+        ex.rows += w & 1023u;
+        ex.kb += uint64_t(w >> 10 & 511u) << 4;
+        ex.vb += uint64_t(w >> 19 & 511u) << 4;
+        ex.bad += w >> 28 & 1u;
+      }
+    }
+    ex.rows = wave_sum64(ex.rows);
+    ex.kb = wave_sum64(ex.kb);
+    ex.vb = wave_sum64(ex.vb);
+    ex.bad = wave_sum64(ex.bad);
+    if (b == P.nblk - 1 && lane == 0) {  // the totals
+      *F.tot = Totals{ex.rows + mine.rows, ex.kb + mine.kb, ex.vb + mine.vb, ex.bad + mine.bad};
+      P.row_start[P.nblk] = ex.rows + mine.rows;
     }
   }
-  // every block: wait for its exclusive prefix (F.incl holds exclusive values)
-  if (lane == 0)
-    while (flag_peek(&F.flag[b]) != (tag | 2u)) __builtin_amdgcn_s_sleep(1);
-  if (lane == 0) ex = prefix_peek(&F.incl[b]);
-  ex.rows = __shfl(ex.rows, 0, 64);
-  ex.kb = __shfl(ex.kb, 0, 64);
-  ex.vb = __shfl(ex.vb, 0, 64);
-  ex.bad = __shfl(ex.bad, 0, 64);
-  }
+  OKV_FUSED_STAMP(3);
   // ---- what passes 1-2 leave for okv_copy_kernel, and the totals ----
   if (lane == 0) {
     BlockCount c;
@@ -1220,7 +1334,10 @@ __device__ __forceinline__ void fused_pass(const CopyParams& P, const FusedParam
   m.c = BlockCount{rows, kb, vb, p, st, 0};
   m.B = block_base_of(P, m.c, ex, Prefix{0, 0, 0, 0});
   m.off = d.offset;
-  if (!block_head(P, b, m)) return;
+  if (!block_head(P, b, m)) {
+    OKV_FUSED_STAMP(4);
+    return;
+  }
   const int nr = int(rows);
   const uint32_t rec = int(lane) < nr ? sm.rec[lane] : 0u;
   if (staged) {
@@ -1239,6 +1356,7 @@ __device__ __forceinline__ void fused_pass(const CopyParams& P, const FusedParam
       gather_region<true>(gsrc, sm, nr, P.val_arena, m.B.vb0, 0, 1);
     }
   }
+  OKV_FUSED_STAMP(4);
 }
 
 __global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, FusedParams F) {
@@ -1261,11 +1379,20 @@ struct FastRows {               // fast path: block staged in LDS, <= kFastRows 
   uint32_t kpre[kFastRows + 1];   // exclusive prefix of key lengths
   uint32_t vpre[kFastRows + 1];   // exclusive prefix of value lengths
 };
+// okv_point_get's probe key (<= 8 KiB): over the fast row table's prefix
+// arrays, which its search does not use (the record positions stay live).
+struct FindRows {
+  uint32_t rec[kFastRows + 1];
+  uint32_t key[8192 / 4];
+};
+static_assert(offsetof(FindRows, key) == offsetof(FastRows, kpre), "key starts at kpre");
+static_assert(sizeof(FindRows) <= sizeof(FastRows), "the key adds no LDS");
 struct __align__(16) CopySmem {
   uint4 stage[(kStage + kStagePad) / 16];  // [16 B guard][block image][guard]
   union {
     SlowRows s;
     FastRows f;
+    FindRows k;
   };
 };
 
@@ -1559,9 +1686,9 @@ __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Total
   const uint32_t* sw = reinterpret_cast<const uint32_t*>(sm.stage);
   uint64_t row0 = 0, kb0 = 0, vb0 = 0, bad = 0;  // exclusive prefixes (uniform)
   if constexpr (kFind) {  // the key into LDS (the prefix arrays: unused by the search)
-    static_assert(2 * (kFastRows + 1) * 4 >= kFindKey, "key fits the prefix arrays");
+    static_assert(sizeof(sm.k.key) >= kFindKey, "the key fits its LDS array");
     const uint32_t* k4 = reinterpret_cast<const uint32_t*>(F.key);
-    for (uint32_t i = tid; i < (F.klen + 3) / 4; i += kThreads) sm.f.kpre[i] = k4[i];
+    for (uint32_t i = tid; i < (F.klen + 3) / 4; i += kThreads) sm.k.key[i] = k4[i];
   }
   for (uint32_t b = 0; b < P.nblk; ++b) {
     OKV_POINT_STAMP(0);
@@ -1672,7 +1799,7 @@ __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Total
       __syncthreads();
       const bool listed = rows <= uint64_t(kFastRows);
       if (st == OKV_BLK_OK && listed) {
-        const uint32_t* tk = sm.f.kpre;
+        const uint32_t* tk = sm.k.key;
         for (uint32_t i = tid; i < uint32_t(rows); i += kThreads) {
           uint32_t kl, vl;
           header_lds(sw, bias + sm.f.rec[i], kl, vl);
@@ -2096,6 +2223,10 @@ void launch_tile_t(hipStream_t s, const CopyParams& P, uint32_t tpb, uint32_t nt
     hipLaunchKernelGGL((okv_tile_kernel_w7<kT, kNT, kXcd>), dim3(grid), dim3(kNT), 0, s, P, tpb,
                        ntile);
     return;
+  } else if constexpr (kDiag >= 32) {
+    hipLaunchKernelGGL((okv_tile_kernel_skip<kT, kNT, kXcd, uint32_t(kDiag - 32)>), dim3(grid),
+                       dim3(kNT), 0, s, P, tpb, ntile);
+    return;
   }
   hipLaunchKernelGGL((okv_tile_kernel_diag<kT, kNT, kXcd, kDiag>), dim3(grid), dim3(kNT), 0, s, P,
                      tpb, ntile);
@@ -2123,7 +2254,12 @@ const TileForm kTileForms[] = {OKV_TILE_FORM(16, 256, 0), OKV_TILE_FORM(8, 256, 
                                OKV_TILE_FORM(16, 256, 7), OKV_TILE_FORM(16, 256, 8),
                                OKV_TILE_FORM(8, 256, 8), OKV_TILE_FORM(32, 512, 8),
                                OKV_TILE_FORM(16, 256, 9), OKV_TILE_FORM(64, 1024, 0),
-                               OKV_TILE_FORM(64, 512, 0)};
+                               OKV_TILE_FORM(64, 512, 0),
+                               // write attribution (okv_tile_kernel_skip): d32 + kSkip
+                               OKV_TILE_FORM(16, 256, 32), OKV_TILE_FORM(16, 256, 33),
+                               OKV_TILE_FORM(16, 256, 34), OKV_TILE_FORM(16, 256, 36),
+                               OKV_TILE_FORM(16, 256, 40), OKV_TILE_FORM(16, 256, 48),
+                               OKV_TILE_FORM(16, 256, 63)};
 const TileForm* tile_form(uint32_t kib, uint32_t threads, uint32_t diag) {
   for (const TileForm& f : kTileForms)
     if (f.kib == kib && f.threads == threads && f.diag == diag) return &f;
@@ -2159,8 +2295,10 @@ int ensure_fused(okv_ctx* ctx, uint32_t nblk) {
     (void)hipFree(ctx->f_agg);
     (void)hipFree(ctx->f_incl);
   }
-  OKV_HIP(hipMalloc(&ctx->f_flag, n * sizeof(uint32_t)));
-  OKV_HIP(hipMemsetAsync(ctx->f_flag, 0, n * sizeof(uint32_t), ctx->stream));
+  // (8 bytes per block: the fused kernel's look-back words; the ablation
+  // stream kernel uses the first 4 bytes per block as its flags)
+  OKV_HIP(hipMalloc(&ctx->f_flag, n * sizeof(uint64_t)));
+  OKV_HIP(hipMemsetAsync(ctx->f_flag, 0, n * sizeof(uint64_t), ctx->stream));
   OKV_HIP(hipMalloc(&ctx->f_agg, n * sizeof(Prefix)));
   OKV_HIP(hipMalloc(&ctx->f_incl, n * sizeof(Prefix)));
   if (!ctx->f_ctr) {
@@ -2354,7 +2492,9 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
         // nothing ran: the counters keep their value, so f_base must too
         return set_err(ctx, OKV_E_HIP, "okv_decode_fused_kernel launch", le);
       }
-      ctx->f_base += nblk;  // both counters advanced by nblk once the grid completes
+      // (the stream / block arms advance both counters by nblk once the grid
+      // completes; the product fused kernel uses none)
+      if (stream || block) ctx->f_base += nblk;
       if (!block) ctx->big_slot ^= 1u;  // the kernel zeroed the other slot (see big_counter)
     } else if (tile) {
       if ((ctx->tile_diag >= 3 && ctx->tile_diag <= 5) || ctx->tile_diag == 7) {

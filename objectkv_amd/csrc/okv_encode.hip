@@ -2202,6 +2202,11 @@ int enc_pack(okv_ctx* ctx, EncScratch* e, const DevRows& R, const okv_encode_opt
   PackParams q = pp;
   q.pl = e->pl;
   q.tp = e->tile_pre;
+  // precondition of every kernel below: the row prefix exists (round 5 launched
+  // them with a null prefix after the tile cut stopped writing it -- an illegal
+  // address on the device)
+  if (!e->have_pl || !q.pl || !q.tp || e->cap_rows < R.n)
+    return set_err(ctx, OKV_E_ARG, "enc_pack: row prefix missing for the chunk-major kernels");
   if (aligned && G >= 1) {  // large records: chunk-major regions
     hipLaunchKernelGGL(okv_enc_pack_region_kernel<0>, dim3(ceil_div(pl.nb, G)), dim3(kThreads), 0,
                        ctx->stream, q, pl.nb, uint32_t(G));

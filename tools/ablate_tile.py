@@ -72,12 +72,20 @@ for i, (a, dec) in enumerate(decs.items()):  # every arm on poisoned outputs, co
         dec.decode_device(seg_t, seg.nbytes, d_t, nblk, o, sync=True)
     if ref is None:
         ref = o
+        if os.environ.get("ABL_CLASSES") == "1":  # output-class bytes (write attribution arms)
+            vo = o["val_off"].cpu().numpy().astype(np.uint64)
+            vl = o["val_len"].cpu().numpy().view(np.uint32).astype(np.uint64)
+            e = (vo + vl)[(vl > 0) & ((vo + vl) % 16 != 0)]
+            nb = int(np.unique(e // 16).size)
+            print(f"classes soa={rows * 22} blocks={nblk * 28} keys={kb} vals={vb} "
+                  f"bnd_chunks={nb} bnd_bytes={nb * 16} runs_bytes~={vb - nb * 16} "
+                  f"read_orig={int(d[:, 2].sum())}", flush=True)
         if os.environ.get("ABL_VERIFY") == "1":
             sys.path.insert(0, ROOT)
             from bench import verify_decode
             print(verify_decode(o, seg, d, 0, False, True, torch), flush=True)
         continue
-    if re.search(r"d[1-5]$", a):
+    if re.search(r"d([1-5]|3[3-9]|[4-6][0-9])$", a):
         print(f"arm {a}: diagnostic (outputs not compared)", flush=True)
         del o
         continue

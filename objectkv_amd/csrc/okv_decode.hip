@@ -643,7 +643,7 @@ struct TileRowsT {
   // row piece {dest chunk, stage byte of its first chunk, count}, and the
   // value chunks that mix rows, padding or a neighbouring tile's bytes
   uint32_t unit[3][kUnits];
-  uint32_t bnd[kRCap + 2];
+  uint32_t bnd[2 * kRCap + 4];  // (sector form: up to two mixed sectors per row)
   uint32_t nunit, nbnd;
 };
 // value runs of a kT-byte tile: at most one partial run per row plus kT / 1 KiB
@@ -695,13 +695,18 @@ __device__ __noinline__ uint4 tile_chunk_pieces(const uint8_t* seg, uint64_t seg
 // okv_decode_ablate.inc, ablation build only.)
 // kSkip (ablation build only, okv_tile_kernel_skip): output classes left
 // unwritten, to attribute the pass's HBM write traffic -- 1 the SoA row index,
-// 2 value runs, 4 key chunks, 8 boundary value chunks, 16 partial chunks.
+// 2 value runs, 4 key chunks, 8 boundary value chunks, 16 partial chunks;
+// 64 (a form, not a skip): value-range cuts between a block's tiles moved to
+// 128-byte destination lines (kLineExt more source bytes staged per tile).
 template <uint32_t kT, uint32_t kNT, bool kXcd, uint32_t kSkip = 0>
 __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uint32_t ntile) {
   constexpr uint32_t kG = kT / 64 + 8;  // 64-byte destination granules of the key range
+  constexpr bool kLineCut = (kSkip & 64) != 0;
+  constexpr bool kSector = (kSkip & 128) != 0;
+  constexpr uint32_t kLineExt = kLineCut ? 512 : 0;
   __shared__ TileRows<kT> R;
   __shared__ uint8_t gt[1][kG];         // row holding key byte max(64 g, range start)
-  __shared__ uint4 stage[kT / 16 + 4];
+  __shared__ uint4 stage[(kT + kLineExt) / 16 + 4];
   uint32_t L = blockIdx.x;
   if constexpr (kXcd) L = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
   if (L >= ntile) return;
@@ -755,7 +760,7 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
   // first byte (a chunk's window begins up to 15 bytes before its first owned
   // byte) through the line after the one holding its last byte + 15
   const int64_t A = int64_t((off + P0) & ~uint64_t(15)) - 16;
-  const int64_t E = int64_t((off + P1 + 15) & ~uint64_t(15)) + 16;
+  const int64_t E = int64_t((off + P1 + 15) & ~uint64_t(15)) + 16 + (last_tile ? 0 : kLineExt);
   const uint32_t np = uint32_t((E - A) >> 4);
   // Waves 1.. issue the DMA; wave 0 builds the row table meanwhile.  (With a
   // share of the DMA in flight, wave 0's LDS row-table writes would wait for
@@ -813,6 +818,54 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
       X[1] = last_tile ? uint32_t(round16(KT)) : first_at(k, ks, kp, KT, P1, jx);
       X[2] = first_at(v, vs, vp, VT, P0, jv);
       X[3] = last_tile ? uint32_t(round16(VT)) : first_at(v, vs, vp, VT, P1, jx);
+      if constexpr (kLineCut) {
+        // a cut Y at source Q moves up to the next 128-byte line of the arena
+        // when the bytes it adds have their sources within kLineExt - 32 of Q
+        // (the tile before the cut stages that far); both tiles of a cut
+        // decide from the same row table, so they agree
+        auto line_cut = [&](uint32_t Y, uint32_t Q) -> uint32_t {
+          const uint32_t end = uint32_t(round16(VT));
+          uint32_t Yl = uint32_t(((vb0 + Y + 127) & ~uint64_t(127)) - vb0);
+          Yl = Yl > end ? end : Yl;
+          if (Yl <= Y || Y >= VT) return Yl <= Y ? Y : Yl;
+          const uint32_t y = min(Yl, VT) - 1;  // the last real byte the tile would add
+          const uint64_t mk = __ballot(live && v && vp <= y && y < vp + v);
+          if (!mk) return Y;
+          const uint32_t j = uint32_t(__ffsll(static_cast<unsigned long long>(mk)) - 1);
+          const uint32_t sy = __builtin_amdgcn_readlane(vs, j) + (y - __builtin_amdgcn_readlane(vp, j));
+          return sy + 32 <= Q + kLineExt ? Yl : Y;
+        };
+        if (t != 0) X[2] = line_cut(X[2], P0);
+        if (!last_tile) X[3] = line_cut(X[3], P1);
+        if (X[2] > X[3]) X[2] = X[3];
+        // the row holding X2 (head chunk: none when X2 is line-aligned)
+        const uint64_t mh = __ballot(live && v && vp <= X[2] && X[2] < vp + v);
+        jv = mh ? uint32_t(__ffsll(static_cast<unsigned long long>(mh)) - 1) : lastr;
+      }
+      // (sector form) the unrounded value cut at P1: value bytes before it
+      // have their sources in this tile's stage
+      const uint32_t Yv1 = X[3];
+      if constexpr (kSector) {
+        // every cut between two tiles of a block moves up to a 64-byte sector
+        // of the arena, so no destination sector is shared by two tiles; the
+        // few bytes this adds to the tile before the cut come from global
+        // windows when they lie past its stage
+        auto sector_up = [](uint32_t Y, uint64_t base, uint32_t tot) -> uint32_t {
+          const uint32_t end = uint32_t(round16(tot));
+          const uint32_t Ys = uint32_t(((base + Y + 63) & ~uint64_t(63)) - base);
+          return Ys > end ? end : Ys;
+        };
+        if (t != 0) {
+          X[0] = sector_up(X[0], kb0, KT);
+          X[2] = sector_up(X[2], vb0, VT);
+        }
+        if (!last_tile) {
+          X[1] = sector_up(X[1], kb0, KT);
+          X[3] = sector_up(X[3], vb0, VT);
+        }
+        X[0] = min(X[0], X[1]);
+        X[2] = min(X[2], X[3]);
+      }
       if (lane == 0) {
         R.x[0] = X[0];
         R.x[1] = X[1];
@@ -836,7 +889,48 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
           for (uint32_t g = gs; g <= ge; ++g) gt[reg][g - g0] = uint8_t(lane);
         }
       }
-      {
+      if constexpr (kSector) {
+        // row pieces of the owned value range: [a, e) = row r's bytes in [X2, X3).
+        // Runs: the whole 64-byte sectors inside a piece (and before Yv1), in
+        // units of <= 64 chunks -- one wave store writes whole sectors.  Every
+        // other sector a piece touches is a mixed sector: its four chunks are
+        // assembled by four adjacent lanes and stored by one instruction.
+        const uint32_t X2 = X[2], X3 = X[3];
+        const uint32_t a = max(vp, X2), e = min(vp + v, X3);
+        const bool piece = live && v && a < e;
+        const uint64_t va = vb0 + a, ve = vb0 + min(e, Yv1);
+        const uint64_t s0 = (va + 63) & ~uint64_t(63), s1 = ve & ~uint64_t(63);
+        const bool run = piece && s1 > s0;
+        const uint32_t cs = run ? uint32_t((s0 - vb0) >> 4) : 0u;
+        const uint32_t wc = run ? uint32_t((s1 - s0) >> 4) : 0u;
+        const uint32_t nu = (wc + 63) >> 6;
+        const uint32_t ui = wave_scan_dpp(nu);
+        const uint32_t sbias0 = uint32_t(int64_t(off) - A);
+        for (uint32_t q = 0; q < nu; ++q) {
+          const uint32_t u = ui - nu + q;
+          R.unit[0][u] = cs + 64 * q;
+          R.unit[1][u] = vs - vp + 16 * (cs + 64 * q) + sbias0;
+          R.unit[2][u] = min(64u, wc - 64 * q);
+        }
+        // mixed sectors, as (sector - the region's first sector) << 8 | the
+        // lowest row with bytes in it (rows in order, head before tail; equal
+        // neighbours skipped by the consumer)
+        const uint64_t vs0 = vb0 >> 6;
+        const uint32_t hsec = uint32_t(((vb0 + a) >> 6) - vs0);
+        const uint32_t tsec = uint32_t(((vb0 + e - 1) >> 6) - vs0);
+        const bool need_h = piece && (!run || s0 > va);
+        const bool need_t = piece && (run ? s1 < vb0 + e : tsec != hsec);
+        const uint32_t nme = uint32_t(need_h) + uint32_t(need_t);
+        const uint32_t mi = wave_scan_dpp(nme) - nme;
+        if (need_h) R.bnd[mi] = (hsec << 8) | lane;
+        if (need_t) R.bnd[mi + uint32_t(need_h)] = (tsec << 8) | lane;
+        const uint32_t nunit = __builtin_amdgcn_readlane(ui, 63);
+        const uint32_t nmix = __builtin_amdgcn_readlane(mi + nme, 63);
+        if (lane == 0) {
+          R.nbnd = nmix;
+          R.nunit = nunit;
+        }
+      } else {
         // row pieces of the owned value range: [a, e) = row r's bytes in [X2, X3)
         const uint32_t X2 = X[2], X3 = X[3];
         const uint32_t a = max(vp, X2), e = min(vp + v, X3);
@@ -917,6 +1011,58 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
         const uint4 w = funnel_u(stage[line], stage[line + 1], sbyte & 15);
         *reinterpret_cast<uint4*>(varena + (uint64_t(c0 + lane) << 4)) = w;
       }
+    }
+    if constexpr (kSector) {
+      // keys (from the first chunk of the range's first sector, so each wave
+      // store covers whole sectors) and the mixed value sectors, four lanes
+      // each: per-lane lookup; sources past the stage from global windows
+      const uint32_t kc0 = kx0 >> 4;
+      const uint32_t kph = uint32_t(((kb0 >> 4) + kc0) & 3u);
+      const uint32_t nk4 = nk ? (kph + nk + 3) & ~3u : 0u;
+      const uint32_t vph = uint32_t(vb0 & 63);
+      for (uint32_t j = tid; j < nk4 + 4 * nbnd; j += kNT) {
+        const uint32_t reg = j >= nk4;
+        if ((kSkip & 4) && !reg) continue;
+        uint32_t r;
+        int32_t xs;
+        if (reg) {
+          const uint32_t ei = (j - nk4) >> 2;
+          const uint32_t bv = R.bnd[ei];
+          if (ei && (bv >> 8) == (R.bnd[ei - 1] >> 8)) continue;
+          xs = int32_t((bv >> 8) * 64u) - int32_t(vph) + int32_t(16 * ((j - nk4) & 3u));
+          r = bv & 255u;
+        } else {
+          xs = int32_t(16 * (kc0 + j)) - int32_t(16 * kph);
+          r = 0;
+        }
+        const uint32_t X0 = reg ? vx0 : kx0, X1 = reg ? vx1 : kx1;
+        if (xs + 16 <= int32_t(X0) || xs >= int32_t(X1)) continue;
+        const uint32_t x = uint32_t(xs);
+        const uint32_t lo = max(x, X0), hi = min(x + 16, X1);
+        const uint32_t* pre = R.pre[reg];
+        const uint32_t* sb = R.sb[reg];
+        if (!reg) r = uint32_t(gt[0][(lo >> 6) - (X0 >> 6)]);
+        while (r < lastr && pre[r + 1] <= lo) ++r;
+        uint8_t* dst = (reg ? P.val_arena + vb0 : P.key_arena + kb0) + x;
+        const uint32_t dend = min(hi, pre[rows]);
+        uint4 out = make_uint4(0, 0, 0, 0);
+        for (uint32_t d = lo; d < dend; ++r) {
+          const uint32_t e = min(dend, pre[r + 1]);
+          if (e > d) {
+            const uint32_t bi = sb[r] + x + sbias;
+            const uint4 w = ((bi >> 4) + 1 < np)
+                                ? load16_lds_b128(stage, bi)
+                                : window16(P.seg, P.seg_bytes, int64_t(off) + sb[r] + x);
+            out = merge_bytes(out, w, int32_t(d - x), int32_t(e - x));
+            d = e;
+          }
+        }
+        if (lo == x && hi == x + 16)
+          *reinterpret_cast<uint4*>(dst) = out;
+        else
+          store_partial(dst, out, lo - x, hi - x);
+      }
+      return;
     }
     // keys and the boundary value chunks: per-lane lookup
     for (uint32_t j = tid; j < nk + nbnd; j += kNT) {
@@ -2226,10 +2372,10 @@ void launch_tile_t(hipStream_t s, const CopyParams& P, uint32_t tpb, uint32_t nt
   } else if constexpr (kDiag >= 32) {
     hipLaunchKernelGGL((okv_tile_kernel_skip<kT, kNT, kXcd, uint32_t(kDiag - 32)>), dim3(grid),
                        dim3(kNT), 0, s, P, tpb, ntile);
-    return;
+  } else {
+    hipLaunchKernelGGL((okv_tile_kernel_diag<kT, kNT, kXcd, kDiag>), dim3(grid), dim3(kNT), 0, s,
+                       P, tpb, ntile);
   }
-  hipLaunchKernelGGL((okv_tile_kernel_diag<kT, kNT, kXcd, kDiag>), dim3(grid), dim3(kNT), 0, s, P,
-                     tpb, ntile);
 #else
   static_assert(kDiag == 0, "the product library has no diagnostic arms");
   hipLaunchKernelGGL((okv_tile_kernel<kT, kNT, kXcd>), dim3(grid), dim3(kNT), 0, s, P, tpb, ntile);
@@ -2259,7 +2405,11 @@ const TileForm kTileForms[] = {OKV_TILE_FORM(16, 256, 0), OKV_TILE_FORM(8, 256, 
                                OKV_TILE_FORM(16, 256, 32), OKV_TILE_FORM(16, 256, 33),
                                OKV_TILE_FORM(16, 256, 34), OKV_TILE_FORM(16, 256, 36),
                                OKV_TILE_FORM(16, 256, 40), OKV_TILE_FORM(16, 256, 48),
-                               OKV_TILE_FORM(16, 256, 63)};
+                               OKV_TILE_FORM(16, 256, 63),
+                               // value cuts on 128-byte lines (tile_pass kSkip 64)
+                               OKV_TILE_FORM(16, 256, 96),
+                               // whole 64-byte sectors per store (tile_pass kSkip 128)
+                               OKV_TILE_FORM(16, 256, 160)};
 const TileForm* tile_form(uint32_t kib, uint32_t threads, uint32_t diag) {
   for (const TileForm& f : kTileForms)
     if (f.kib == kib && f.threads == threads && f.diag == diag) return &f;

@@ -701,9 +701,10 @@ __device__ __noinline__ uint4 tile_chunk_pieces(const uint8_t* seg, uint64_t seg
 template <uint32_t kT, uint32_t kNT, bool kXcd, uint32_t kSkip = 0>
 __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uint32_t ntile) {
   constexpr uint32_t kG = kT / 64 + 8;  // 64-byte destination granules of the key range
-  constexpr bool kLineCut = (kSkip & 64) != 0;
-  constexpr bool kSector = (kSkip & 128) != 0;
-  constexpr uint32_t kLineExt = kLineCut ? 512 : 0;
+  constexpr bool kSector = (kSkip & 128) != 0;       // whole 64-byte sectors per store
+  constexpr bool kLineCut = (kSkip & 64) != 0 && !kSector;
+  constexpr bool kKeyRound = kSector && !(kSkip & 256);  // (256: key cuts left as they are)
+  constexpr uint32_t kLineExt = (kSkip & (64 | 512)) ? 512 : 0;  // (512: stage extension)
   __shared__ TileRows<kT> R;
   __shared__ uint8_t gt[1][kG];         // row holding key byte max(64 g, range start)
   __shared__ uint4 stage[(kT + kLineExt) / 16 + 4];
@@ -856,11 +857,11 @@ __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uin
           return Ys > end ? end : Ys;
         };
         if (t != 0) {
-          X[0] = sector_up(X[0], kb0, KT);
+          if (kKeyRound) X[0] = sector_up(X[0], kb0, KT);
           X[2] = sector_up(X[2], vb0, VT);
         }
         if (!last_tile) {
-          X[1] = sector_up(X[1], kb0, KT);
+          if (kKeyRound) X[1] = sector_up(X[1], kb0, KT);
           X[3] = sector_up(X[3], vb0, VT);
         }
         X[0] = min(X[0], X[1]);
@@ -1400,27 +1401,44 @@ __device__ __forceinline__ void fused_pass(const CopyParams& P, const FusedParam
   OKV_FUSED_STAMP(2);
   const Prefix mine{rows, round16(kb), round16(vb), uint64_t(st != OKV_BLK_OK)};
   Prefix ex{0, 0, 0, 0};
+  // ---- pass 2: each block sums its predecessors' published counts ----
+  // One write-through 8-byte word per block carries its counts and the
+  // call's tag (fused_pack); every lane loads the words of up to
+  // kFusedMaxBlocks / 64 predecessors at once and re-polls only those not
+  // yet published.  (Round 5: the last block to arrive scanned every
+  // block's counts and published the prefixes behind a second flag -- a
+  // chain of dependent cross-XCD trips that every block waited out.)
+  uint64_t* word = reinterpret_cast<uint64_t*>(F.flag);
+  const uint32_t want = F.epoch | 0x80000000u;
+  if (!kLB && lane == 0) {
+    uint32_t w = 0;
+    if (!fused_pack(mine, w)) {
+      publish_payload(&F.agg[b], mine);  // sc1 stores, drained
+      w = 1u << 29;
+    }
+    __hip_atomic_store(&word[b], uint64_t(want) << 32 | w, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // Pass 3 up to the stores, while the predecessors' counts arrive: a staged
+  // block's key and value regions are assembled into an LDS image (block-
+  // local offsets); only the row index and the image's copy-out wait for the
+  // prefix.  (C2: the gather after the wait took 3.0 us of a 14 us kernel.)
+  __shared__ uint4 img[kSmallStage / 16 + 2];
+  const int nr = int(rows);
+  const bool pre_asm = !kLB && staged && st == OKV_BLK_OK && nr > 0 && rows <= uint64_t(kRCap) &&
+                       !P.index_only;
+  const uint32_t kreg = uint32_t(round16(kb)), vreg = uint32_t(round16(vb));
+  if (pre_asm) {
+    static_assert(sizeof(img) >= kSmallStage, "both regions fit the image");
+    const uint32_t rec = int(lane) < nr ? sm.rec[lane] : 0u;
+    build_row_table(lsrc, sm, nr, rec);
+    uint8_t* const im = reinterpret_cast<uint8_t*>(img);
+    gather_region<false>(lsrc, sm, nr, im, 0, 0, 1);
+    gather_region<true>(lsrc, sm, nr, im, kreg, 0, 1);
+  }
   if constexpr (kLB) {
     ex = fused_prefix_lookback(P, F, b, lane, tag, mine);  // ablation build only
   } else {
-    // ---- pass 2: each block sums its predecessors' published counts ----
-    // One write-through 8-byte word per block carries its counts and the
-    // call's tag (fused_pack); every lane loads the words of up to
-    // kFusedMaxBlocks / 64 predecessors at once and re-polls only those not
-    // yet published.  (Round 5: the last block to arrive scanned every
-    // block's counts and published the prefixes behind a second flag -- a
-    // chain of dependent cross-XCD trips that every block waited out.)
-    uint64_t* word = reinterpret_cast<uint64_t*>(F.flag);
-    const uint32_t want = F.epoch | 0x80000000u;
-    if (lane == 0) {
-      uint32_t w = 0;
-      if (!fused_pack(mine, w)) {
-        publish_payload(&F.agg[b], mine);  // sc1 stores, drained
-        w = 1u << 29;
-      }
-      __hip_atomic_store(&word[b], uint64_t(want) << 32 | w, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
     constexpr uint32_t kU = kFusedMaxBlocks / 64;
     uint64_t wv[kU];
 #pragma unroll
@@ -1484,7 +1502,15 @@ __device__ __forceinline__ void fused_pass(const CopyParams& P, const FusedParam
     OKV_FUSED_STAMP(4);
     return;
   }
-  const int nr = int(rows);
+  if (pre_asm) {  // the row index, then the image out in whole 16-byte chunks
+    write_row_index(P, sm, m, nr);
+    for (uint32_t c = lane; c < kreg / 16; c += 64)
+      *reinterpret_cast<uint4*>(P.key_arena + m.B.kb0 + 16ull * c) = img[c];
+    for (uint32_t c = lane; c < vreg / 16; c += 64)
+      *reinterpret_cast<uint4*>(P.val_arena + m.B.vb0 + 16ull * c) = img[kreg / 16 + c];
+    OKV_FUSED_STAMP(4);
+    return;
+  }
   const uint32_t rec = int(lane) < nr ? sm.rec[lane] : 0u;
   if (staged) {
     build_row_table(lsrc, sm, nr, rec);
@@ -2409,7 +2435,8 @@ const TileForm kTileForms[] = {OKV_TILE_FORM(16, 256, 0), OKV_TILE_FORM(8, 256, 
                                // value cuts on 128-byte lines (tile_pass kSkip 64)
                                OKV_TILE_FORM(16, 256, 96),
                                // whole 64-byte sectors per store (tile_pass kSkip 128)
-                               OKV_TILE_FORM(16, 256, 160)};
+                               OKV_TILE_FORM(16, 256, 160), OKV_TILE_FORM(16, 256, 672),
+                               OKV_TILE_FORM(16, 256, 928)};
 const TileForm* tile_form(uint32_t kib, uint32_t threads, uint32_t diag) {
   for (const TileForm& f : kTileForms)
     if (f.kib == kib && f.threads == threads && f.diag == diag) return &f;
@@ -2433,6 +2460,24 @@ int read_totals(okv_ctx* ctx, Totals* out) {
   *out = *ctx->h_tot;
   return OKV_OK;
 }
+
+// The context's stream replaced for a span of launches (pass 3 on a shared
+// queue), restored on every exit path.
+struct StreamSwap {
+  okv_ctx* c;
+  hipStream_t own = nullptr;
+  explicit StreamSwap(okv_ctx* x) : c(x) {}
+  void swap(hipStream_t s) {
+    own = c->stream;
+    c->stream = s;
+  }
+  bool swapped() const { return own != nullptr; }
+  void restore() {
+    if (own) c->stream = own;
+    own = nullptr;
+  }
+  ~StreamSwap() { restore(); }
+};
 
 // Scratch of the single-pass small-block decode (flags zeroed once; the epoch
 // tag makes every call's flags fresh).
@@ -2600,9 +2645,20 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
                                           ? OKV_PATH_STAGED
                                       : gt == 64 && ctx->gather_staged ? OKV_PATH_SMALL
                                                                        : OKV_PATH_GATHER));
-  // okv_decode_chain: pass 3 after the chained context's last pass 3
-  if (ctx->chain && ctx->chain->p3_rec)
+  // okv_decode_chain: pass 3 after the chained context's last pass 3.  With a
+  // shared pass-3 queue the kernels below go to the queue's stream behind
+  // this context's passes 1-2 (an event recorded long before the previous
+  // pass 3 ends), so consecutive pass 3s meet at a same-stream boundary;
+  // without one (or while profiling per-pass events), this stream waits for
+  // the chained context's pass-3 event.
+  StreamSwap s3(ctx);
+  if (ctx->p3q && !ctx->prof) {
+    OKV_HIP(hipEventRecord(ctx->ev_cnt, ctx->stream));
+    OKV_HIP(hipStreamWaitEvent(ctx->p3q->stream, ctx->ev_cnt, 0));
+    s3.swap(ctx->p3q->stream);
+  } else if (ctx->chain && ctx->chain->p3_rec) {
     OKV_HIP(hipStreamWaitEvent(ctx->stream, ctx->chain->p3_done, 0));
+  }
   if (nblk) {
     const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
 #ifdef OKV_ABLATE
@@ -2733,6 +2789,11 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   if (ctx->p3_done) {
     OKV_HIP(hipEventRecord(ctx->p3_done, ctx->stream));
     ctx->p3_rec = true;
+  }
+  if (s3.swapped()) {  // the context's stream continues after its pass 3
+    OKV_HIP(hipEventRecord(ctx->ev_p3, ctx->stream));
+    s3.restore();
+    OKV_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_p3, 0));
   }
   prof_mark(ctx, 4);
   if (flags & OKV_F_ASYNC) return OKV_OK;
@@ -3139,6 +3200,19 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
 
 okv_ctx* okv_open(int device) { return okv_open_on_stream(device, nullptr); }
 
+// Leave the shared pass-3 queue (its stream drained and destroyed with the
+// last member).
+static void p3q_leave(okv_ctx* ctx) {
+  P3Queue* q = ctx->p3q;
+  if (!q) return;
+  ctx->p3q = nullptr;
+  (void)hipStreamSynchronize(q->stream);
+  if (--q->refs == 0) {
+    (void)hipStreamDestroy(q->stream);
+    delete q;
+  }
+}
+
 void okv_close(okv_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
@@ -3158,6 +3232,9 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->d_big);
   (void)hipFree(ctx->d_ctr);
   if (ctx->p3_done) (void)hipEventDestroy(ctx->p3_done);
+  p3q_leave(ctx);
+  if (ctx->ev_cnt) (void)hipEventDestroy(ctx->ev_cnt);
+  if (ctx->ev_p3) (void)hipEventDestroy(ctx->ev_p3);
   (void)hipFree(ctx->f_flag);
   (void)hipFree(ctx->f_agg);
   (void)hipFree(ctx->f_incl);
@@ -3222,6 +3299,36 @@ int okv_decode_chain(okv_ctx* ctx, okv_ctx* after) {
         return set_err(ctx, OKV_E_HIP, "okv_decode_chain: event", e);
       }
     }
+  }
+  // the shared pass-3 queue: ctx joins after's (created with the first link)
+  if (after) {
+    if (!after->p3q || !ctx->ev_cnt || !after->ev_cnt) {
+      OKV_HIP(hipSetDevice(ctx->device));
+      for (okv_ctx* c : {ctx, after}) {
+        if (!c->ev_cnt && (hipEventCreateWithFlags(&c->ev_cnt, hipEventDisableTiming) != hipSuccess ||
+                           hipEventCreateWithFlags(&c->ev_p3, hipEventDisableTiming) != hipSuccess)) {
+          (void)hipSetDevice(prev);
+          return set_err(ctx, OKV_E_HIP, "okv_decode_chain: event");
+        }
+      }
+      if (!after->p3q) {
+        P3Queue* q = new P3Queue;
+        if (hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) != hipSuccess) {
+          delete q;
+          (void)hipSetDevice(prev);
+          return set_err(ctx, OKV_E_HIP, "okv_decode_chain: queue stream");
+        }
+        q->refs = 1;
+        after->p3q = q;
+      }
+    }
+    if (ctx->p3q != after->p3q) {
+      p3q_leave(ctx);
+      ctx->p3q = after->p3q;
+      ctx->p3q->refs++;
+    }
+  } else {
+    p3q_leave(ctx);
   }
   OKV_HIP(hipSetDevice(prev));  // the caller's current device is left as it was
   if (ctx->chain) {

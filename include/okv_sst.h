@@ -184,10 +184,7 @@ int okv_decode_blocks(okv_ctx *ctx, const uint8_t *seg, uint64_t seg_bytes,
  * once the pass 3 last enqueued on `after` has finished.  Two contexts chained
  * to each other, decoding alternate segments on their own streams, run each
  * decode's header walk (pass 1, latency-bound) under the other's pass 3,
- * while their pass-3 kernels never run concurrently.  Chained contexts share
- * one pass-3 stream (created with the first link): each decode's pass 3 is
- * enqueued there behind its own passes 1-2, in issue order, and its own
- * stream resumes after it.  after = NULL unchains.
+ * while their pass-3 kernels never run concurrently.  after = NULL unchains.
  * Both contexts must be on the same device and be driven from one host thread;
  * okv_close of either unchains the pair.  The caller's current device is kept.
  */

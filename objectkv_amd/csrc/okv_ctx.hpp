@@ -32,11 +32,6 @@ void launch_zstd_desc(hipStream_t s, const Desc* descs, uint32_t nblk, const uin
 constexpr uint32_t kZstdLitBytes = 1u << 17;  // per-wave literal scratch (Block_Maximum_Size)
 }  // namespace okv
 
-struct P3Queue {
-  hipStream_t stream = nullptr;
-  int refs = 0;
-};
-
 struct okv_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -69,12 +64,6 @@ struct okv_ctx {
   std::vector<okv_ctx*> chained_by;  // contexts whose chain is this one (unchained at close)
   hipEvent_t p3_done = nullptr;    // recorded after every pass 3 once created
   bool p3_rec = false;             // p3_done has been recorded
-  // chained contexts enqueue their pass 3 on one shared stream (in issue
-  // order), so one pass 3 follows the previous at a same-stream kernel
-  // boundary instead of behind a cross-stream event wait (okv_decode_chain)
-  struct P3Queue* p3q = nullptr;
-  hipEvent_t ev_cnt = nullptr;     // this context's passes 1-2 done (the queue waits on it)
-  hipEvent_t ev_p3 = nullptr;      // this context's pass 3 done (its stream waits on it)
   size_t f_cap = 0;
   okv::Totals* d_tot = nullptr;
   okv::Totals* h_tot = nullptr;  // pinned

@@ -625,6 +625,12 @@ __device__ __forceinline__ void sweep_handoff(const CopyParams& P, const GatherS
 //      window per row piece) and stored whole; the two chunks at a range's
 //      ends that the neighbouring tile shares are stored byte-exactly
 //      (store_partial: disjoint bytes, no read-modify-write).
+// The value-range cut between two tiles of a block moves up to the next
+// 128-byte line of the arena when the bytes it adds lie in the tile's staged
+// extension (kLineExt source bytes past its end): stores from two workgroups
+// never share that line.  (Every store instruction that covers part of a
+// 64-byte sector costs the HBM a whole 64-byte write request -- the L2 does
+// not merge separate stores into one; PMC by output class)
 // Tile 0 also writes the block's row index (SoA) and its block outputs.  The
 // last tile writes the zero padding of the block's arena regions.  Each
 // source byte is read once and each arena byte written once, so the pass
@@ -696,15 +702,15 @@ __device__ __noinline__ uint4 tile_chunk_pieces(const uint8_t* seg, uint64_t seg
 // kSkip (ablation build only, okv_tile_kernel_skip): output classes left
 // unwritten, to attribute the pass's HBM write traffic -- 1 the SoA row index,
 // 2 value runs, 4 key chunks, 8 boundary value chunks, 16 partial chunks;
-// 64 (a form, not a skip): value-range cuts between a block's tiles moved to
-// 128-byte destination lines (kLineExt more source bytes staged per tile).
+// forms: 64 the round-5 cuts (no line cut, below); 128 whole 64-byte sectors
+// per store (+ 256 key cuts unrounded, + 512 the stage extension).
 template <uint32_t kT, uint32_t kNT, bool kXcd, uint32_t kSkip = 0>
 __device__ __forceinline__ void tile_pass(const CopyParams& P, uint32_t tpb, uint32_t ntile) {
   constexpr uint32_t kG = kT / 64 + 8;  // 64-byte destination granules of the key range
   constexpr bool kSector = (kSkip & 128) != 0;       // whole 64-byte sectors per store
-  constexpr bool kLineCut = (kSkip & 64) != 0 && !kSector;
+  constexpr bool kLineCut = !(kSkip & 64) && !kSector;  // the product: value cuts on lines
   constexpr bool kKeyRound = kSector && !(kSkip & 256);  // (256: key cuts left as they are)
-  constexpr uint32_t kLineExt = (kSkip & (64 | 512)) ? 512 : 0;  // (512: stage extension)
+  constexpr uint32_t kLineExt = (kLineCut || (kSkip & 512)) ? 512 : 0;  // (512: stage extension)
   __shared__ TileRows<kT> R;
   __shared__ uint8_t gt[1][kG];         // row holding key byte max(64 g, range start)
   __shared__ uint4 stage[(kT + kLineExt) / 16 + 4];
@@ -2353,10 +2359,7 @@ int launch_plan(okv_ctx* ctx, const Work& w, uint32_t nblk, uint64_t* d_row_star
                      big_counter(ctx, 1), nullptr, 0u, span_max);
   OKV_HIP(hipGetLastError());
   ctx->big_slot ^= 1u;  // the launch zeroes the other slot: the next launch's counter
-  if (timed) {
-    prof_mark(ctx, 2);
-    prof_mark(ctx, 3);
-  }
+  if (timed) prof_mark(ctx, 2);  // (the caller marks 3: after the big-block kernel)
   return OKV_OK;
 }
 
@@ -2461,24 +2464,6 @@ int read_totals(okv_ctx* ctx, Totals* out) {
   return OKV_OK;
 }
 
-// The context's stream replaced for a span of launches (pass 3 on a shared
-// queue), restored on every exit path.
-struct StreamSwap {
-  okv_ctx* c;
-  hipStream_t own = nullptr;
-  explicit StreamSwap(okv_ctx* x) : c(x) {}
-  void swap(hipStream_t s) {
-    own = c->stream;
-    c->stream = s;
-  }
-  bool swapped() const { return own != nullptr; }
-  void restore() {
-    if (own) c->stream = own;
-    own = nullptr;
-  }
-  ~StreamSwap() { restore(); }
-};
-
 // Scratch of the single-pass small-block decode (flags zeroed once; the epoch
 // tag makes every call's flags fresh).
 int ensure_fused(okv_ctx* ctx, uint32_t nblk) {
@@ -2572,6 +2557,13 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
                                         ~uint32_t(kTile - 1));
   if (spn >= nblk) spn = 0;
 #endif
+  // the big-block kernel (okv_copy_kernel, okv_index_kernel) runs right after
+  // passes 1-2 when they are one count launch: before the chained context's
+  // pass-3 wait, so with decodes in flight it runs under the other decode's
+  // pass 3 (the list is empty on C1-C5: an empty launch cost 4.6 us + a
+  // kernel boundary in front of each pass 3), and before the pass-3 mark, so
+  // the pass-3 interval times the tile / gather kernel alone
+  bool early_big = false;
   if (fused || stream || (block && !block_diag)) {
     if ((rc = ensure_fused(ctx, nblk))) return rc;
     prof_mark(ctx, 2);
@@ -2588,6 +2580,8 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   } else {
     rc = launch_plan(ctx, w, nblk, o->row_start, true, rt_kl, geo.span_cap);
     if (rc) return rc;
+    early_big = nblk != 0;
+    if (!early_big) prof_mark(ctx, 3);
   }
   CopyParams P;
   P.seg = w.seg;
@@ -2645,20 +2639,25 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
                                           ? OKV_PATH_STAGED
                                       : gt == 64 && ctx->gather_staged ? OKV_PATH_SMALL
                                                                        : OKV_PATH_GATHER));
-  // okv_decode_chain: pass 3 after the chained context's last pass 3.  With a
-  // shared pass-3 queue the kernels below go to the queue's stream behind
-  // this context's passes 1-2 (an event recorded long before the previous
-  // pass 3 ends), so consecutive pass 3s meet at a same-stream boundary;
-  // without one (or while profiling per-pass events), this stream waits for
-  // the chained context's pass-3 event.
-  StreamSwap s3(ctx);
-  if (ctx->p3q && !ctx->prof) {
-    OKV_HIP(hipEventRecord(ctx->ev_cnt, ctx->stream));
-    OKV_HIP(hipStreamWaitEvent(ctx->p3q->stream, ctx->ev_cnt, 0));
-    s3.swap(ctx->p3q->stream);
-  } else if (ctx->chain && ctx->chain->p3_rec) {
-    OKV_HIP(hipStreamWaitEvent(ctx->stream, ctx->chain->p3_done, 0));
+  const uint32_t nbig_grid = std::min<uint32_t>(nblk, 512);
+  auto launch_big = [&]() {
+    if (index_only)
+      hipLaunchKernelGGL(okv_index_kernel, dim3((nbig_grid + kThreads - 1) / kThreads),
+                         dim3(kThreads), 0, ctx->stream, P);
+    else
+      hipLaunchKernelGGL(okv_copy_kernel, dim3(nbig_grid), dim3(kThreads), 0, ctx->stream, P);
+  };
+  if (early_big) {
+    launch_big();
+    OKV_HIP(hipGetLastError());
+    prof_mark(ctx, 3);
   }
+  // okv_decode_chain: pass 3 after the chained context's last pass 3.  (A
+  // shared pass-3 stream for chained contexts instead of this event wait
+  // measured slower: C5 0.407 vs 0.396 ms, C3 1.465 vs 1.449 ms per step with
+  // decodes in flight, profiles/r6/session/pass3_queue_ab.log.)
+  if (ctx->chain && ctx->chain->p3_rec)
+    OKV_HIP(hipStreamWaitEvent(ctx->stream, ctx->chain->p3_done, 0));
   if (nblk) {
     const dim3 g(ctx->gather_grid ? std::min<uint32_t>(nblk, ctx->gather_grid) : nblk);
 #ifdef OKV_ABLATE
@@ -2776,24 +2775,12 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       return set_err(ctx, OKV_E_ARG, "decode path");  // unreachable: large => tile
     }
 #endif
-    const uint32_t nbig_grid = std::min<uint32_t>(nblk, 512);
-    if (block) {
-      // (the block kernel decodes every block itself)
-    } else if (index_only)
-      hipLaunchKernelGGL(okv_index_kernel, dim3((nbig_grid + kThreads - 1) / kThreads),
-                         dim3(kThreads), 0, ctx->stream, P);
-    else
-      hipLaunchKernelGGL(okv_copy_kernel, dim3(nbig_grid), dim3(kThreads), 0, ctx->stream, P);
+    if (!block && !early_big) launch_big();  // (the block kernel decodes every block itself)
     OKV_HIP(hipGetLastError());
   }
   if (ctx->p3_done) {
     OKV_HIP(hipEventRecord(ctx->p3_done, ctx->stream));
     ctx->p3_rec = true;
-  }
-  if (s3.swapped()) {  // the context's stream continues after its pass 3
-    OKV_HIP(hipEventRecord(ctx->ev_p3, ctx->stream));
-    s3.restore();
-    OKV_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_p3, 0));
   }
   prof_mark(ctx, 4);
   if (flags & OKV_F_ASYNC) return OKV_OK;
@@ -3200,19 +3187,6 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
 
 okv_ctx* okv_open(int device) { return okv_open_on_stream(device, nullptr); }
 
-// Leave the shared pass-3 queue (its stream drained and destroyed with the
-// last member).
-static void p3q_leave(okv_ctx* ctx) {
-  P3Queue* q = ctx->p3q;
-  if (!q) return;
-  ctx->p3q = nullptr;
-  (void)hipStreamSynchronize(q->stream);
-  if (--q->refs == 0) {
-    (void)hipStreamDestroy(q->stream);
-    delete q;
-  }
-}
-
 void okv_close(okv_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
@@ -3232,9 +3206,6 @@ void okv_close(okv_ctx* ctx) {
   (void)hipFree(ctx->d_big);
   (void)hipFree(ctx->d_ctr);
   if (ctx->p3_done) (void)hipEventDestroy(ctx->p3_done);
-  p3q_leave(ctx);
-  if (ctx->ev_cnt) (void)hipEventDestroy(ctx->ev_cnt);
-  if (ctx->ev_p3) (void)hipEventDestroy(ctx->ev_p3);
   (void)hipFree(ctx->f_flag);
   (void)hipFree(ctx->f_agg);
   (void)hipFree(ctx->f_incl);
@@ -3299,36 +3270,6 @@ int okv_decode_chain(okv_ctx* ctx, okv_ctx* after) {
         return set_err(ctx, OKV_E_HIP, "okv_decode_chain: event", e);
       }
     }
-  }
-  // the shared pass-3 queue: ctx joins after's (created with the first link)
-  if (after) {
-    if (!after->p3q || !ctx->ev_cnt || !after->ev_cnt) {
-      OKV_HIP(hipSetDevice(ctx->device));
-      for (okv_ctx* c : {ctx, after}) {
-        if (!c->ev_cnt && (hipEventCreateWithFlags(&c->ev_cnt, hipEventDisableTiming) != hipSuccess ||
-                           hipEventCreateWithFlags(&c->ev_p3, hipEventDisableTiming) != hipSuccess)) {
-          (void)hipSetDevice(prev);
-          return set_err(ctx, OKV_E_HIP, "okv_decode_chain: event");
-        }
-      }
-      if (!after->p3q) {
-        P3Queue* q = new P3Queue;
-        if (hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) != hipSuccess) {
-          delete q;
-          (void)hipSetDevice(prev);
-          return set_err(ctx, OKV_E_HIP, "okv_decode_chain: queue stream");
-        }
-        q->refs = 1;
-        after->p3q = q;
-      }
-    }
-    if (ctx->p3q != after->p3q) {
-      p3q_leave(ctx);
-      ctx->p3q = after->p3q;
-      ctx->p3q->refs++;
-    }
-  } else {
-    p3q_leave(ctx);
   }
   OKV_HIP(hipSetDevice(prev));  // the caller's current device is left as it was
   if (ctx->chain) {

@@ -119,6 +119,8 @@ def sweep(run_once, budget_s):
             t_cpu += time.perf_counter() - t1
             n_pass += 1
         res[nth] = (units / t_cpu, n_pass, t_cpu)
+    from oracle import coracle
+    coracle.arena_trim()  # the arena pool back to the OS after the sweep
     return res
 
 
@@ -130,6 +132,9 @@ def sweep_summary(res, scale, unit, kind, sample):
             "single_thread_value": round(res[1][0] * scale, 4),
             "all_cores": {"cores": allc, "value": round(res[allc][0] * scale, 4)},
             "by_threads": {str(k): round(v[0] * scale, 4) for k, v in sorted(res.items())},
+            # (rounds 1-4 allocated with glibc malloc: their CPU lines are not
+            # comparable with these)
+            "allocator": "per-thread bump arena (Go per-P mcache analogue), since round 5",
             "sample": sample + f"; host CPU: {cpu_model()}, nproc={os.cpu_count()}, "
                                f"affinity={host_cores()}"}
 
@@ -600,8 +605,9 @@ def path_kernels(okv, lp):
              (L.PATH_STREAM, "okv_decode_stream_kernel (passes 1-3)"),
              (L.PATH_SMALL, "okv_gather_small_kernel"), (L.PATH_TILE, "okv_tile_kernel"),
              (L.PATH_SWEEP, "okv_rows_kernel + okv_value_sweep_kernel"),
-             (L.PATH_STAGED, "okv_gather_staged_kernel"), (L.PATH_GATHER, "okv_gather_kernel"),
-             (L.PATH_BIG, "okv_copy_kernel")]
+             (L.PATH_STAGED, "okv_gather_staged_kernel"), (L.PATH_GATHER, "okv_gather_kernel")]
+    # (the big-block kernel of these paths, okv_copy_kernel, runs before the
+    # pass-3 interval since round 6: after the count, ahead of the chain wait)
     return " + ".join(n for bit, n in names if lp & bit) or "none"
 
 

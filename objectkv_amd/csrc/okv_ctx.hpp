@@ -93,6 +93,7 @@ struct okv_ctx {
   // host-mode point reads (okv_point_kernel): one pinned slab holding the
   // staged blocks, their descriptors and every output
   uint8_t* h_slab = nullptr;
+  uint32_t point_seq = 0;          // point-kernel call number (its slab completion word)
   size_t cap_slab = 0;
   // per-pass event timing (okv_profile)
   uint32_t gather_grid = 0;  // 0: default grid; else workgroups (OKV_GATHER_GRID)

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1849,7 +1850,18 @@ struct PointFind {
   const uint8_t* key;
   uint32_t klen;
   int32_t* found;
+  uint32_t* done;  // non-null: the call's completion word in the pinned slab (point_wait)
+  uint32_t seq;    // ... the value the kernel writes there last
 };
+// The kernel's last act: every wave's slab writes pushed to system scope,
+// then one store of the call's sequence number, for which the host spins
+// (point_wait) instead of waiting in hipStreamSynchronize.
+__device__ __forceinline__ void point_done(const PointFind& F) {
+  if (!F.done) return;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(F.done, F.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 constexpr uint32_t kFindKey = 8192;  // (held in the row table's prefix arrays)
 
 template <bool kFind>
@@ -2014,6 +2026,7 @@ __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Total
         *tot = Totals{hit != ~0u ? 1u : 0u, kl, vl, uint64_t(st != OKV_BLK_OK)};
       }
       OKV_POINT_STAMP(4);
+      point_done(F);
       return;  // (one block)
     }
     if (st == OKV_BLK_OK && rows) {
@@ -2098,6 +2111,7 @@ __global__ __launch_bounds__(kThreads) void okv_point_kernel(CopyParams P, Total
     P.row_start[P.nblk] = row0;
     *tot = Totals{row0, kb0, vb0, bad};
   }
+  point_done(F);
 }
 
 // ---------------------------------------------------------------------------
@@ -2854,6 +2868,22 @@ int grow_host(okv_ctx* ctx, uint8_t** p, size_t* cap, size_t need) {
   return OKV_OK;
 }
 
+// Wait for a point-kernel call by spinning on its completion word in the
+// pinned slab (point_done), polling the stream every 1 024 spins so that a
+// failed launch ends the wait; hipStreamSynchronize then reports the error.
+// (A GetRow is one launch plus this wait; hipStreamSynchronize alone sleeps
+// through several microseconds after the kernel's last store.)
+int point_wait(okv_ctx* ctx, const volatile uint32_t* done, uint32_t seq) {
+  for (uint32_t n = 1; *done != seq; ++n) {
+    if ((n & 1023u) == 0 && hipStreamQuery(ctx->stream) != hipErrorNotReady) break;
+    __builtin_ia32_pause();
+  }
+  if (*done != seq) OKV_HIP(hipStreamSynchronize(ctx->stream));
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return OKV_OK;
+}
+
+
 // One launch, one synchronisation: the blocks and descriptors are copied into
 // the pinned slab, the kernel reads them there and writes every output there
 // (both over PCIe), and the outputs are copied into the caller's arrays.
@@ -2872,7 +2902,7 @@ int decode_point(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv
   const size_t n1 = size_t(nblk) + 1;
   const size_t o_desc = al(seg_bytes + 64), o_rs = al(o_desc + nblk * sizeof(Desc)),
                o_kb = al(o_rs + n1 * 8), o_vb = al(o_kb + n1 * 8), o_st = al(o_vb + n1 * 8),
-               o_tot = al(o_st + n1 * 4), o_ko = al(o_tot + sizeof(Totals)),
+               o_tot = al(o_st + n1 * 4), o_ko = al(o_tot + sizeof(Totals) + 16),
                o_kl = al(o_ko + R * 8), o_vo = al(o_kl + R * 2), o_vl = al(o_vo + R * 8),
                o_ka = al(o_vl + R * 4), o_va = al(o_ka + A + 16), total = al(o_va + A + 16);
   int rc = grow_host(ctx, &ctx->h_slab, &ctx->cap_slab, total);
@@ -2902,10 +2932,13 @@ int decode_point(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv
   P.val_cap = A + 16;
   Totals* tot = reinterpret_cast<Totals*>(S + o_tot);
   ctx->last_path = OKV_PATH_POINT;
+  uint32_t* done = reinterpret_cast<uint32_t*>(S + o_tot + sizeof(Totals));
+  *done = 0;
+  const uint32_t seq = ++ctx->point_seq ? ctx->point_seq : ++ctx->point_seq;  // (never 0)
   hipLaunchKernelGGL(okv_point_kernel<false>, dim3(1), dim3(kThreads), 0, ctx->stream, P, tot,
-                     PointFind{nullptr, 0, nullptr});
+                     PointFind{nullptr, 0, nullptr, done, seq});
   OKV_HIP(hipGetLastError());
-  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  if ((rc = point_wait(ctx, done, seq))) return rc;
   const Totals T = *tot;
   o->n_rows = T.rows;
   o->key_bytes = T.kb;
@@ -2937,13 +2970,14 @@ int point_get(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv_bl
   out->found = -1;
   out->key = out->val = nullptr;
   out->key_len = out->val_len = 0;
+  ctx->last_path = 0;  // (OKV_PATH_POINT once the kernel is launched: okv_last_path)
   if (!ctx->point || klen > kFindKey || !point_eligible(seg_bytes, desc, 1, comp, 0))
     return OKV_OK;  // not a point-path block: the caller decodes it in full
   const Desc& d = *reinterpret_cast<const Desc*>(desc);
   const uint64_t A = go_read_status(d, seg_bytes) == OKV_BLK_OK ? round16(d.block_size) : 0;
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t o_desc = al(seg_bytes + 64), o_key = al(o_desc + sizeof(Desc)),
-               o_misc = al(o_key + klen + 16), o_tot = al(o_misc + 64), o_ka = al(o_tot + 64),
+               o_misc = al(o_key + klen + 16), o_tot = al(o_misc + 72), o_ka = al(o_tot + 64),
                o_va = al(o_ka + A + 16), total = al(o_va + A + 16);
   int rc = grow_host(ctx, &ctx->h_slab, &ctx->cap_slab, total);
   if (rc) return rc;
@@ -2970,10 +3004,13 @@ int point_get(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const okv_bl
   P.val_arena = S + o_va;
   Totals* tot = reinterpret_cast<Totals*>(S + o_tot);
   ctx->last_path = OKV_PATH_POINT;
+  uint32_t* done = reinterpret_cast<uint32_t*>(misc + 8);
+  *done = 0;
+  const uint32_t seq = ++ctx->point_seq ? ctx->point_seq : ++ctx->point_seq;  // (never 0)
   hipLaunchKernelGGL(okv_point_kernel<true>, dim3(1), dim3(kThreads), 0, ctx->stream, P, tot,
-                     PointFind{S + o_key, uint32_t(klen), found});
+                     PointFind{S + o_key, uint32_t(klen), found, done, seq});
   OKV_HIP(hipGetLastError());
-  OKV_HIP(hipStreamSynchronize(ctx->stream));
+  if ((rc = point_wait(ctx, done, seq))) return rc;
   out->status = *P.blk_status;
   out->found = *found;
   if (out->found == 1) {

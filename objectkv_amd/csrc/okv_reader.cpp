@@ -442,10 +442,12 @@ int okv_reader_get_row(okv_reader* r, const uint8_t* key, size_t klen, okv_row* 
     stage_span(r, {e}, &d, &seg, &n);
     okv_point_row pr;
     if (okv_point_get(r->ctx, seg, n, d.data(), r->compression, key, klen, &pr)) return OKV_R_GPU;
-    if (pr.found != -1) {
+    if (okv_last_path(r->ctx) == OKV_PATH_POINT) {  // a launch, whatever it found
       r->io.calls++;
       r->io.blocks++;
       r->io.bytes_staged += n;
+    }
+    if (pr.found != -1) {
       if (const int brc = block_rc(pr.status)) return brc;
       if (pr.found == 0) return OKV_R_NO_ROWS;  // "did not find row in block"
       // (valid until the next read call, okv_host.h)

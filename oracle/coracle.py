@@ -79,6 +79,7 @@ def lib():
         L.oref_decode_range_go.argtypes = [p, u64, p, u64, C.c_int, C.c_int, C.POINTER(u64)]
         L.oref_block_counts.argtypes = [p, u64, p, u64, C.c_int, p, p, p, p]
         L.oref_decode_soa.argtypes = [p, u64, p, u64, C.c_int, C.c_int] + [p] * 10
+        L.oref_arena_trim.argtypes = []
         _lib = L
     return _lib
 
@@ -207,6 +208,11 @@ def decode_soa(seg, descs: np.ndarray, compression=0, index_only=False):
     for k in ("key_off", "key_len", "val_off", "val_len"):
         out[k] = out[k][:rows_out]
     return out
+
+
+def arena_trim():
+    """Free the baseline arena's pooled chunks (after a CPU baseline sweep)."""
+    lib().oref_arena_trim()
 
 
 def decode_go(seg, descs: np.ndarray, compression=0, threads=1):

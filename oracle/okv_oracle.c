@@ -604,8 +604,10 @@ static __thread size_t t_arena_since;  /* bytes handed out since the last reset 
 /* chunks of finished jobs, kept faulted-in for the next job (threads are
  * created per call; touching fresh pages would make every pass pay page faults) */
 static arena_chunk *g_pool;
+static size_t g_pool_n;  /* chunks pooled (capped: kPoolMax; the rest are freed) */
 static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
 static const size_t kArenaChunk = (size_t)16 << 20;
+static const size_t kPoolMax = 64; /* 1 GiB of faulted-in chunks kept across jobs */
 
 static void arena_begin(void) {
   t_arena_on = 1;
@@ -618,9 +620,32 @@ static void arena_release(arena_chunk *c) { /* to the pool (standard-size chunks
     return;
   }
   pthread_mutex_lock(&g_pool_mu);
-  c->next = g_pool;
-  g_pool = c;
+  if (g_pool_n < kPoolMax) {
+    c->next = g_pool;
+    g_pool = c;
+    g_pool_n++;
+    c = NULL;
+  }
   pthread_mutex_unlock(&g_pool_mu);
+  if (c) {
+    free(c->data);
+    free(c);
+  }
+}
+/* Free every pooled chunk (the CPU baselines call it after a sweep, so the
+ * process does not keep the sweep's peak arena memory). */
+void oref_arena_trim(void) {
+  pthread_mutex_lock(&g_pool_mu);
+  arena_chunk *c = g_pool;
+  g_pool = NULL;
+  g_pool_n = 0;
+  pthread_mutex_unlock(&g_pool_mu);
+  while (c) {
+    arena_chunk *n = c->next;
+    free(c->data);
+    free(c);
+    c = n;
+  }
 }
 static void arena_reset(void) {
   if (!t_arena) return;
@@ -647,7 +672,10 @@ static void *go_alloc(size_t n) {
     arena_chunk *c = NULL;
     if (n <= kArenaChunk) {
       pthread_mutex_lock(&g_pool_mu);
-      if ((c = g_pool)) g_pool = c->next;
+      if ((c = g_pool)) {
+        g_pool = c->next;
+        g_pool_n--;
+      }
       pthread_mutex_unlock(&g_pool_mu);
     }
     if (!c) {

@@ -323,3 +323,20 @@ def test_point_get_reader_rows_and_fallback(decoder, nopoint):
                 except Exception as e:  # noqa: BLE001
                     out.append(type(e).__name__)
             assert out[0] == out[1], (k, out)
+
+
+def test_getrow_counts_point_launch_before_full_decode(decoder):
+    """A block of more than 1 024 rows: okv_point_get walks it (one launch,
+    found == -1) and the reader then decodes it in full -- both GPU calls are
+    counted in the reader's I/O stats, and the row is Go's."""
+    rows = [(b"k%05d" % i, b"") for i in range(1500)]  # 12-byte records
+    w = okv.SegmentWriter(60000, 65536)
+    for k, v in rows:
+        w.WriteRow(k, v)
+    flen, _meta = w.Close()
+    r = R.SegmentReader(w.data().tobytes(), flen, decoder)
+    b = r.io_stats()
+    got = r.GetRow(rows[1234][0])
+    assert got.Key == rows[1234][0] and not got.Value
+    a = r.io_stats()
+    assert a["calls"] - b["calls"] == 2 and a["blocks"] - b["blocks"] == 2, (b, a)

@@ -602,6 +602,7 @@ def path_kernels(okv, lp):
     """The pass-3 kernels the last decode launched (okv_last_path bits)."""
     L = okv._lib
     names = [(L.PATH_FUSED, "okv_decode_fused_kernel (passes 1-3)"),
+             (L.PATH_GROUP, "okv_group_kernel (passes 1-3)"),
              (L.PATH_STREAM, "okv_decode_stream_kernel (passes 1-3)"),
              (L.PATH_SMALL, "okv_gather_small_kernel"), (L.PATH_TILE, "okv_tile_kernel"),
              (L.PATH_SWEEP, "okv_rows_kernel + okv_value_sweep_kernel"),
@@ -953,6 +954,9 @@ def run_compact(args, torch, okv, D):
         got = eout["seg"][b0 * bs:(b0 + 3) * bs].cpu().numpy().tobytes()
         assert got == want[:3 * bs], b0
     out_bytes = int(eo.data_bytes)
+    seg_t0, fb0, d_t0, nb0 = segs[0]  # which decode kernels the stage runs
+    enc.decode_device(seg_t0, fb0, d_t0, nb0, douts[0], sync=True)
+    dec_kernels = path_kernels(okv, enc.last_path())
 
     for _ in range(args.warmup):
         step()
@@ -967,8 +971,8 @@ def run_compact(args, torch, okv, D):
     for _ in range(2):
         step(ph)
     ph *= 1e3 / 2
-    # roofline of the decode stage's gather kernel (the largest kernel of the
-    # step): per step K launches over all input blocks
+    # roofline of the decode stage's pass-3 kernel (okv_group_kernel: passes
+    # 1-3 in one launch, since round 6): per step K launches over all input blocks
     gather_ms = kern_ms["copy"] / max(calls, 1) * K
     orig = 0
     for seg_t, fb, d_t, nb in segs:
@@ -999,7 +1003,7 @@ def run_compact(args, torch, okv, D):
                      "encode": round(ph[2], 4)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": f"okv_gather_kernel (decode stage, {K} launches per step)",
+                     "kernel": f"{dec_kernels} (decode stage, {K} launches per step)",
                      "algorithmic_bytes_per_launch": int(alg / K),
                      "kernel_ms_per_step": round(gather_ms, 4)},
         "cpu_baseline": cpu,

@@ -27,12 +27,12 @@ OKV_OK, OKV_E_ARG, OKV_E_HIP, OKV_E_CAPACITY, OKV_E_NOMEM, OKV_E_NODEV = 0, -1, 
 BLK_OK, BLK_EOF, BLK_SHORT, BLK_PANIC, BLK_UNSUPPORTED, BLK_CAPACITY = 0, 1, 2, 3, 4, 5
 COMP_NONE, COMP_ZSTD, COMP_LZ4 = 0, 1, 2
 F_DEVICE_PTRS, F_INDEX_ONLY, F_ASYNC, F_NO_CLOSE = 1, 2, 4, 8
-OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS, OPEN_NO_POINT = 1, 2, 4
+OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS, OPEN_NO_POINT, OPEN_NO_GROUP = 1, 2, 4, 8
 # okv_last_path bits (include/okv_sst.h OKV_PATH_*)
 PATH_FUSED, PATH_SMALL, PATH_TILE, PATH_SWEEP = 1, 2, 4, 8
 PATH_STAGED, PATH_GATHER, PATH_BIG, PATH_ZSTD = 16, 32, 64, 128
 PATH_ZSTD_REGROW, PATH_ENC_ONEPASS, PATH_STREAM = 256, 512, 1024
-PATH_POINT = 2048
+PATH_POINT, PATH_GROUP = 2048, 4096
 # SegmentWriter sentinels (okv_sst.h OKV_W_*)
 W_KEY_TOO_LARGE, W_VALUE_TOO_LARGE, W_CLOSED, W_INVALID_KEY = -101, -102, -103, -104
 W_NIL_WRITER, W_UNSUPPORTED, W_NO_ROWS = -105, -106, -107

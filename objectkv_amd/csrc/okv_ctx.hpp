@@ -58,6 +58,13 @@ struct okv_ctx {
   unsigned long long* f_ctr = nullptr;  // block-index counter, f_base at the next call
   unsigned long long f_base = 0;
   uint32_t f_epoch = 0;
+  // grouped single-pass small-block decode (okv_group_kernel; OKV_OPEN_NO_GROUP: off)
+  bool group = true;
+  uint32_t* g_flag = nullptr;      // [groups] look-back flags, tagged with g_epoch
+  okv::Prefix* g_agg = nullptr;
+  okv::Prefix* g_incl = nullptr;
+  size_t g_cap = 0;
+  uint32_t g_epoch = 0;
   uint32_t last_path = 0;          // OKV_PATH_* of the last decode (okv_last_path)
   // okv_decode_chain: this context's pass 3 waits for chain's last pass 3
   okv_ctx* chain = nullptr;

@@ -31,13 +31,12 @@
 extern "C" {
 #endif
 
-#define OKV_ABI_VERSION 7 /* 2: okv_encode_opts.bloom / bloom_len, and okv_profile_read writes
+#define OKV_ABI_VERSION 6 /* 2: okv_encode_opts.bloom / bloom_len, and okv_profile_read writes
                              4 doubles (ms[4]: the zstd stage slot was added);
                              3: okv_open_ex / okv_open_opts
                              4: okv_decode_chain
                              5: OKV_OPEN_NO_POINT / OKV_PATH_POINT (host-mode point path)
-                             6: okv_point_get (GetRow's block step, one row back)
-                             7: OKV_OPEN_NO_GROUP / OKV_PATH_GROUP (single-pass small blocks) */
+                             6: okv_point_get (GetRow's block step, one row back) */
 
 /* ---- return codes (int) -------------------------------------------------- */
 #define OKV_OK 0
@@ -143,9 +142,6 @@ okv_ctx *okv_open_on_stream(int device, void *stream);
                                      <= 16 small uncompressed blocks in one launch over pinned
                                      memory): every batch is staged to device memory and decoded
                                      by the device-resident kernels; outputs identical */
-#define OKV_OPEN_NO_GROUP 8u      /* large batches of small blocks decode in two passes (count,
-                                     then okv_gather_small_kernel re-reading every block) instead
-                                     of okv_group_kernel's single pass; outputs identical (ABI 7) */
 typedef struct okv_open_opts {
   uint32_t size;  /* sizeof(okv_open_opts) */
   uint32_t flags; /* OKV_OPEN_* */
@@ -425,9 +421,10 @@ int okv_profile_read(okv_ctx *ctx, double *ms, uint64_t *calls);
                                      builds only (OKV_ENC_ONEPASS=1); the product runs E1-E9 */
 #define OKV_PATH_ZSTD_REGROW 256u /* zstd frames outgrew their first output region and were
                                      measured and decoded again (io.Copy inflates them all) */
-#define OKV_PATH_GROUP 4096u /* okv_group_kernel: a large batch of small blocks in one pass,
-                                  16 blocks per workgroup, the prefix by decoupled look-back
-                                  (ABI 7) */
+#define OKV_PATH_GROUP 4096u /* okv_group_kernel (ablation builds only, OKV_DECODE_GROUP=1):
+                                  a large batch of small blocks in one pass, 16 blocks per
+                                  workgroup, the prefix by decoupled look-back; measured
+                                  slower than passes 1-3 */
 #define OKV_PATH_POINT 2048u /* okv_point_kernel: a host-mode call of a few small uncompressed
                                 blocks (GetRow, GetRange) in one launch over pinned memory */
 uint32_t okv_last_path(const okv_ctx *ctx);

@@ -27,7 +27,7 @@ OKV_OK, OKV_E_ARG, OKV_E_HIP, OKV_E_CAPACITY, OKV_E_NOMEM, OKV_E_NODEV = 0, -1, 
 BLK_OK, BLK_EOF, BLK_SHORT, BLK_PANIC, BLK_UNSUPPORTED, BLK_CAPACITY = 0, 1, 2, 3, 4, 5
 COMP_NONE, COMP_ZSTD, COMP_LZ4 = 0, 1, 2
 F_DEVICE_PTRS, F_INDEX_ONLY, F_ASYNC, F_NO_CLOSE = 1, 2, 4, 8
-OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS, OPEN_NO_POINT, OPEN_NO_GROUP = 1, 2, 4, 8
+OPEN_NO_FUSED, OPEN_ZSTD_ONE_PASS, OPEN_NO_POINT = 1, 2, 4
 # okv_last_path bits (include/okv_sst.h OKV_PATH_*)
 PATH_FUSED, PATH_SMALL, PATH_TILE, PATH_SWEEP = 1, 2, 4, 8
 PATH_STAGED, PATH_GATHER, PATH_BIG, PATH_ZSTD = 16, 32, 64, 128

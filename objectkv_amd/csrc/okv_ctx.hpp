@@ -58,8 +58,8 @@ struct okv_ctx {
   unsigned long long* f_ctr = nullptr;  // block-index counter, f_base at the next call
   unsigned long long f_base = 0;
   uint32_t f_epoch = 0;
-  // grouped single-pass small-block decode (okv_group_kernel; OKV_OPEN_NO_GROUP: off)
-  bool group = true;
+  // grouped single-pass small-block decode (ablation build, OKV_DECODE_GROUP=1)
+  bool group = false;
   uint32_t* g_flag = nullptr;      // [groups] look-back flags, tagged with g_epoch
   okv::Prefix* g_agg = nullptr;
   okv::Prefix* g_incl = nullptr;

@@ -1562,232 +1562,6 @@ __global__ __launch_bounds__(64) void okv_decode_fused_kernel(CopyParams P, Fuse
 }
 
 // ---------------------------------------------------------------------------
-// Single-pass decode of large batches of small blocks (OKV_PATH_GROUP; the CM
-// compaction feed's 386 K x 4 KiB segments): each block's bytes are read from
-// HBM once.  One 256-thread workgroup per group of kGroup consecutive blocks:
-//   1. every wave DMAs its four blocks into their LDS slots (64 KiB of the
-//      group in flight at once) and walks their headers there (walk_staged,
-//      Go's checks in Go's order);
-//   2. the group's counts go out as an aggregate, and wave 0 sums its
-//      predecessors' by a decoupled look-back over 64 groups per round
-//      (aggregate / inclusive flags tagged with the call's epoch; write-
-//      through payloads drained before their flag, read with sc1 loads after
-//      it -- the fused kernel's hand-off);
-//   3. every wave gathers its blocks' rows from their slots.
-// The prefix is what okv_count_kernel + its scan would give, so outputs are
-// identical to the two-pass form (count, then okv_gather_small_kernel
-// re-reading every block).  With kGroup blocks per look-back entry the
-// frontier spans 64 x kGroup blocks per round trip; round 4's one-block-per-
-// workgroup stream kernel advanced 64 blocks per round trip.
-// Blocks past the slot take the HBM walk and gather; blocks of more than
-// kRCap rows go on the big-block list (okv_copy_kernel) as from pass 1.
-#ifndef OKV_GROUP_BLOCKS  // (A/B builds: tools/build_dec_variant.sh -DOKV_GROUP_BLOCKS=8)
-#define OKV_GROUP_BLOCKS 16
-#endif
-constexpr uint32_t kGroup = OKV_GROUP_BLOCKS;  // blocks per workgroup (kGroup / 4 per wave)
-constexpr uint32_t kGroupPerWave = kGroup / 4;
-static_assert(kGroup % 4 == 0 && kGroup <= 64, "whole blocks per wave");
-constexpr uint32_t kGroupSlot = 4160;   // staged bytes per block: a 4 KiB block + lead-in + slack
-struct GroupParams {
-  const int32_t* pre;  // zstd-stage statuses or null
-  BlockCount* cnt;     // what passes 1-2 write, for okv_copy_kernel
-  Prefix* lp;
-  Prefix* tile_pre;
-  uint32_t* flag;      // [group] (epoch << 2) | 1 aggregate published, | 2 inclusive
-  Prefix* agg;         // [group]
-  Prefix* incl;        // [group] inclusive prefix
-  uint32_t epoch;      // per call, never 0 (the flags start zeroed)
-  Totals* tot;
-  uint32_t* big_zero;  // the other big-block counter slot: zeroed for the next launch
-};
-struct __align__(16) GroupSmem {
-  uint4 stage[kGroup][kGroupSlot / 16];
-  uint32_t rec[kGroup][kRCap + 1];
-  GatherSmem g[4];                 // row tables, one per wave
-  uint64_t cnt[kGroup][4];         // rows, key bytes, value bytes, walk end
-  uint64_t off[kGroup];
-  int32_t st[kGroup];
-  uint32_t staged[kGroup];
-  Prefix loc[kGroup];              // exclusive prefix within the group
-  Prefix ex;                       // the group's exclusive prefix
-};
-
-__global__ __launch_bounds__(kThreads) void okv_group_kernel(CopyParams P, GroupParams G) {
-  __shared__ GroupSmem sm;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t g = blockIdx.x, b0 = g * kGroup;
-  const uint32_t nb = min(kGroup, P.nblk - b0);
-  if (g == 0 && tid == 0) *G.big_zero = 0;
-  // ---- 1. descriptors, statuses, the DMA of the wave's blocks ----
-  const int64_t lim = int64_t(round16(P.seg_bytes));
-#pragma unroll
-  for (uint32_t i = 0; i < kGroupPerWave; ++i) {
-    const uint32_t lb = wave * kGroupPerWave + i;
-    if (lb >= nb) break;
-    const uint32_t b = b0 + lb;
-    const Desc d = P.descs[b];
-    int32_t st = OKV_BLK_OK;
-    const int32_t pre = G.pre ? G.pre[b] : int32_t(OKV_BLK_OK);
-    if (pre != OKV_BLK_OK) st = pre;  // outcome of the zstd stage
-    else if ((st = go_read_status(d, P.seg_bytes)) != OKV_BLK_OK) {}  // :303-316
-    else if (P.comp == OKV_COMP_ZSTD) st = OKV_BLK_UNSUPPORTED;
-    const uint64_t len = (P.comp == OKV_COMP_LZ4) ? 0 : d.block_size;  // Q7 (:331-333)
-    const uint32_t shift = uint32_t(d.offset & 15);
-    const bool staged = st == OKV_BLK_OK && len + 16 + shift + 32 <= kGroupSlot;
-    if (lane == 0) {
-      sm.off[lb] = d.offset;
-      sm.st[lb] = st;
-      sm.staged[lb] = staged;
-    }
-    if (staged && len) {  // [offset - shift - 16, offset + len + 32) into the slot
-      const int64_t D = int64_t(d.offset) - int64_t(shift) - 16;
-      const uint32_t n16 = uint32_t((16 + shift + len + 32 + 15) >> 4);
-      for (uint32_t c0 = 0; c0 < n16; c0 += 64) {
-        if (c0 + lane < n16) {  // (an inactive lane writes no LDS)
-          int64_t a = D + (int64_t(c0 + lane) << 4);
-          if (a < 0 || a + 16 > lim) a = int64_t(d.offset) & ~int64_t(15);  // bytes never used
-          __builtin_amdgcn_global_load_lds(P.seg + a, OKV_LDS_PTR(&sm.stage[lb][c0]), 16, 0, 0);
-        }
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // ---- the walks (each wave its own blocks: its own DMA, so no barrier) ----
-#pragma unroll
-  for (uint32_t i = 0; i < kGroupPerWave; ++i) {
-    const uint32_t lb = wave * kGroupPerWave + i;
-    if (lb >= nb) break;
-    const Desc d = P.descs[b0 + lb];
-    int32_t st = sm.st[lb];
-    uint64_t rows = 0, kb = 0, vb = 0, p = 0;
-    const uint64_t len = (P.comp == OKV_COMP_LZ4) ? 0 : d.block_size;
-    if (st == OKV_BLK_OK && sm.staged[lb]) {
-      const StageWin lsrc{&sm.stage[lb][0], 16 + uint32_t(d.offset & 15)};
-      walk_staged(lsrc, uint32_t(len), d.original_size, sm.rec[lb], lane, st, rows, kb, vb, p);
-    } else if (st == OKV_BLK_OK) {
-      walk_global(P.seg, d.offset, len, d.original_size, sm.rec[lb], lane, st, rows, kb, vb, p);
-    }
-    if (lane == 0) {
-      sm.st[lb] = st;
-      sm.cnt[lb][0] = rows;
-      sm.cnt[lb][1] = kb;
-      sm.cnt[lb][2] = vb;
-      sm.cnt[lb][3] = p;
-    }
-  }
-  __syncthreads();
-  // ---- 2. the group's prefix (wave 0) ----
-  if (wave == 0) {
-    const bool live = lane < nb;
-    uint64_t v[4] = {live ? sm.cnt[lane][0] : 0, live ? round16(sm.cnt[lane][1]) : 0,
-                     live ? round16(sm.cnt[lane][2]) : 0,
-                     uint64_t(live && sm.st[lane] != OKV_BLK_OK)};
-    uint64_t inc[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) inc[k] = wave_incl_scan(v[k], lane);
-    if (live) sm.loc[lane] = Prefix{inc[0] - v[0], inc[1] - v[1], inc[2] - v[2], inc[3] - v[3]};
-    const Prefix agg{__shfl(inc[0], 63, 64), __shfl(inc[1], 63, 64), __shfl(inc[2], 63, 64),
-                     __shfl(inc[3], 63, 64)};
-    const uint32_t tagA = (G.epoch << 2) | 1u, tagP = (G.epoch << 2) | 2u;
-    if (lane == 0) publish(&G.flag[g], &G.agg[g], agg, tagA);
-    Prefix ex{0, 0, 0, 0};
-    for (int64_t k_hi = int64_t(g) - 1; k_hi >= 0; k_hi -= 64) {
-      const int64_t k = k_hi - int64_t(lane);  // lane 0: the nearest predecessor
-      uint32_t f = k >= 0 ? flag_peek(&G.flag[k]) : tagP;
-      bool ready = k < 0 || f == tagA || f == tagP;
-      while (__ballot(!ready)) {
-        if (!ready) {
-          __builtin_amdgcn_s_sleep(1);
-          f = flag_peek(&G.flag[k]);
-          ready = f == tagA || f == tagP;
-        }
-      }
-      // the nearest inclusive prefix ends the look-back; the aggregates of
-      // the groups after it are added to it
-      const uint64_t pm = __ballot(k >= 0 && f == tagP);
-      const uint32_t stop = pm ? uint32_t(__builtin_ctzll(pm)) : 64u;
-      if (k >= 0 && lane <= stop) {
-        const Prefix o = lane == stop ? prefix_peek(&G.incl[k]) : prefix_peek(&G.agg[k]);
-        ex.rows += o.rows;
-        ex.kb += o.kb;
-        ex.vb += o.vb;
-        ex.bad += o.bad;
-      }
-      if (pm) break;
-    }
-    ex.rows = wave_sum64(ex.rows);
-    ex.kb = wave_sum64(ex.kb);
-    ex.vb = wave_sum64(ex.vb);
-    ex.bad = wave_sum64(ex.bad);
-    const Prefix in{ex.rows + agg.rows, ex.kb + agg.kb, ex.vb + agg.vb, ex.bad + agg.bad};
-    if (lane == 0) {
-      publish(&G.flag[g], &G.incl[g], in, tagP);
-      sm.ex = ex;
-      if (g == gridDim.x - 1) {  // the totals
-        *G.tot = Totals{in.rows, in.kb, in.vb, in.bad};
-        P.row_start[P.nblk] = in.rows;
-      }
-    }
-  }
-  __syncthreads();
-  // ---- 3. outputs and the gather, each wave its four blocks ----
-  GatherSmem& gs = sm.g[wave];
-#pragma unroll 1
-  for (uint32_t i = 0; i < kGroupPerWave; ++i) {
-    const uint32_t lb = wave * kGroupPerWave + i;
-    if (lb >= nb) break;
-    const uint32_t b = b0 + lb;
-    const Prefix l = sm.loc[lb];
-    const Prefix ex{sm.ex.rows + l.rows, sm.ex.kb + l.kb, sm.ex.vb + l.vb, sm.ex.bad + l.bad};
-    BlockMeta m;
-    m.c = BlockCount{sm.cnt[lb][0], sm.cnt[lb][1], sm.cnt[lb][2], sm.cnt[lb][3], sm.st[lb], 0};
-    m.B = block_base_of(P, m.c, ex, Prefix{0, 0, 0, 0});
-    m.off = sm.off[lb];
-    const uint64_t rows = m.c.rows;
-    if (lane == 0) {  // what passes 1-2 leave for okv_copy_kernel, and the block outputs
-      G.cnt[b] = m.c;
-      G.lp[b] = ex;
-      if (b % kTile == 0) G.tile_pre[b / kTile] = Prefix{0, 0, 0, 0};
-      if (m.c.status == OKV_BLK_OK && (rows > kRCap || m.c.pend >= (uint64_t(1) << 32)))
-        P.big_list[atomicAdd(P.big_count, 1u)] = b;
-      P.row_start[b] = m.B.row0;
-      if (P.key_base) P.key_base[b] = m.B.kb0;
-      if (P.val_base) P.val_base[b] = m.B.vb0;
-      P.blk_status[b] = m.B.st;
-    }
-    if (!(m.B.st == OKV_BLK_OK && rows != 0 && rows <= uint64_t(kRCap) &&
-          m.c.pend < (uint64_t(1) << 32)))
-      continue;
-    const int nr = int(rows);
-    const uint32_t rec = int(lane) < nr ? sm.rec[lb][lane] : 0u;
-    // the row index (lane r = row r)
-    auto row_index = [&]() {
-      if (int(lane) >= nr) return;
-      const uint64_t gr = m.B.row0 + lane;
-      const uint32_t kl = gs.kpre[lane + 1] - gs.kpre[lane], vl = gs.vpre[lane + 1] - gs.vpre[lane];
-      P.key_len[gr] = uint16_t(kl);
-      P.val_len[gr] = vl;
-      P.key_off[gr] = m.B.kb0 + gs.kpre[lane];
-      P.val_off[gr] = m.B.vb0 + gs.vpre[lane];
-    };
-    if (sm.staged[lb]) {
-      const StageWin src{&sm.stage[lb][0], 16 + uint32_t(m.off & 15)};
-      build_row_table(src, gs, nr, rec);
-      row_index();
-      gather_region<false>(src, gs, nr, P.key_arena, m.B.kb0, 0, 1);
-      gather_region<true>(src, gs, nr, P.val_arena, m.B.vb0, 0, 1);
-    } else {
-      const GlobalWin src{P.seg, P.seg_bytes, m.off};
-      build_row_table(src, gs, nr, rec);
-      row_index();
-      gather_region<false>(src, gs, nr, P.key_arena, m.B.kb0, 0, 1);
-      gather_region<true>(src, gs, nr, P.val_arena, m.B.vb0, 0, 1);
-    }
-  }
-}
-
-
-// ---------------------------------------------------------------------------
 // Pass 4 (big blocks only): LDS-staged decode with a serial header chase.
 // ---------------------------------------------------------------------------
 struct SlowRows {               // general path: 64-bit positions, batched rows
@@ -2748,26 +2522,6 @@ int ensure_fused(okv_ctx* ctx, uint32_t nblk) {
   return OKV_OK;
 }
 
-// Look-back scratch of the grouped single pass (flags zeroed once; the epoch
-// tag makes every call's flags fresh).
-int ensure_group(okv_ctx* ctx, uint32_t ngroups) {
-  const size_t n = std::max<size_t>(ngroups, 1);
-  if (n <= ctx->g_cap && ctx->g_flag) return OKV_OK;
-  if (ctx->g_flag) {
-    OKV_HIP(hipStreamSynchronize(ctx->stream));
-    (void)hipFree(ctx->g_flag);
-    (void)hipFree(ctx->g_agg);
-    (void)hipFree(ctx->g_incl);
-    ctx->g_flag = nullptr;
-  }
-  OKV_HIP(hipMalloc(&ctx->g_flag, n * sizeof(uint32_t)));
-  OKV_HIP(hipMemsetAsync(ctx->g_flag, 0, n * sizeof(uint32_t), ctx->stream));
-  OKV_HIP(hipMalloc(&ctx->g_agg, n * sizeof(Prefix)));
-  OKV_HIP(hipMalloc(&ctx->g_incl, n * sizeof(Prefix)));
-  ctx->g_cap = n;
-  return OKV_OK;
-}
-
 #ifdef OKV_ABLATE  // the measured alternative forms of round 4 (ablation build only)
 #include "okv_decode_ablate_host.inc"
 #endif
@@ -2801,8 +2555,14 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
   // large blocks: the source-tile pass (okv_tile_kernel); value_sweep 1-7 are
   // the round-2 forms (row pass + address-ordered value sweep)
   const bool large = nblk && !fused && !stream && gather_threads(ctx, w, nblk) == 256;
-  // small blocks past the fused batch: the grouped single pass (okv_group_kernel)
+  // (ablation build, OKV_DECODE_GROUP=1: small blocks past the fused batch in
+  // the grouped single pass, okv_group_kernel -- measured slower than passes
+  // 1-3: CM decode stage 5.9-6.8 vs 4.1 ms)
+#ifdef OKV_ABLATE
   const bool group = ctx->group && nblk && !fused && !stream && !large && !index_only;
+#else
+  constexpr bool group = false;
+#endif
 #ifdef OKV_ABLATE
   // OKV_VALUE_SWEEP=9: the one-launch per-block decode (okv_block_kernel)
   // (10: the same with 512-thread workgroups; 11: diagnostic, the prefix from
@@ -2849,10 +2609,12 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
     if ((rc = ensure_fused(ctx, nblk))) return rc;
     prof_mark(ctx, 2);
     prof_mark(ctx, 3);
+#ifdef OKV_ABLATE
   } else if (group) {
     if ((rc = ensure_group(ctx, (nblk + kGroup - 1) / kGroup))) return rc;
     prof_mark(ctx, 2);
     prof_mark(ctx, 3);
+#endif
 #ifdef OKV_ABLATE
   } else if (b0) {
     rc = launch_plan_pieces(ctx, w, nblk, b0, o->row_start, rt_kl, geo.span_cap);
@@ -2918,7 +2680,7 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
                    (!nblk ? 0u
                     : fused ? OKV_PATH_FUSED
                     : stream ? OKV_PATH_STREAM
-                    : group ? OKV_PATH_GROUP | OKV_PATH_BIG
+                    : group ? OKV_PATH_GROUP | OKV_PATH_BIG  // (ablation builds only)
                     : OKV_PATH_BIG | (tile ? OKV_PATH_TILE
                                       : sweep ? OKV_PATH_SWEEP | OKV_PATH_STAGED
                                       : gt == 256 && ctx->gather_staged && !index_only
@@ -2987,7 +2749,9 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
       // completes; the product fused kernel uses none)
       if (stream || block) ctx->f_base += nblk;
       if (!block) ctx->big_slot ^= 1u;  // the kernel zeroed the other slot (see big_counter)
-    } else if (group) {
+    }
+#ifdef OKV_ABLATE
+    else if (group) {
       GroupParams G;
       G.pre = w.pre;
       G.cnt = ctx->d_cnt;
@@ -3005,7 +2769,9 @@ int decode_device(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const De
                          ctx->stream, P, G);
       OKV_HIP(hipGetLastError());
       ctx->big_slot ^= 1u;  // the kernel zeroed the other slot (see big_counter)
-    } else if (tile) {
+    }
+#endif
+    else if (tile) {
       if ((ctx->tile_diag >= 3 && ctx->tile_diag <= 5) || ctx->tile_diag == 7) {
         // phase probe: 8 timestamps per 256th workgroup
         const size_t n = (size_t(nblk) * geo.tpb / 256 + 1) * 64;
@@ -3433,7 +3199,6 @@ okv_ctx* okv_open_ex(int device, void* stream, const okv_open_opts* opts) {
     if (opts->flags & OKV_OPEN_NO_FUSED) ctx->fused = false;
     ctx->zstd_one_pass = (opts->flags & OKV_OPEN_ZSTD_ONE_PASS) != 0;
     ctx->point = (opts->flags & OKV_OPEN_NO_POINT) == 0;
-    ctx->group = (opts->flags & OKV_OPEN_NO_GROUP) == 0;
   }
   return ctx;
 }
@@ -3470,6 +3235,7 @@ okv_ctx* okv_open_on_stream(int device, void* stream) {
   }
   if (const char* v = getenv("OKV_GATHER_GRID")) ctx->gather_grid = uint32_t(atoi(v));
   if (const char* v = getenv("OKV_DECODE_FUSED")) ctx->fused = atoi(v) != 0;
+  if (const char* v = getenv("OKV_DECODE_GROUP")) ctx->group = atoi(v) != 0;
   if (const char* v = getenv("OKV_DECODE_PIECES")) ctx->pieces = atoi(v) != 0;
   if (const char* v = getenv("OKV_DECODE_STREAM")) ctx->stream_lb = atoi(v) != 0;
   if (const char* v = getenv("OKV_SMALL_PIECE_MB")) ctx->small_piece = uint64_t(atoi(v)) << 20;

@@ -40,7 +40,7 @@ def test_library_exports_every_declared_symbol():
     L = _lib.lib()
     for name in declared:
         assert getattr(L, name)
-    assert L.okv_abi_version() == 7
+    assert L.okv_abi_version() == 6
 
 
 def test_library_has_gfx950_code_object():

@@ -293,10 +293,10 @@ def _mixed_segment(kinds, seed):
 
 @pytest.fixture(scope="module")
 def nofused_decoder():
-    """A context opened with OKV_OPEN_NO_FUSED (and NO_POINT, NO_GROUP): small
-    blocks take the two-pass path (count + scan in one launch, then
+    """A context opened with OKV_OPEN_NO_FUSED (and NO_POINT): small batches
+    of small blocks take the three-launch path (count, scan,
     okv_gather_small_kernel)."""
-    dec = okv.Decoder(0, flags=_lib.OPEN_NO_FUSED | _lib.OPEN_NO_POINT | _lib.OPEN_NO_GROUP)
+    dec = okv.Decoder(0, flags=_lib.OPEN_NO_FUSED | _lib.OPEN_NO_POINT)
     yield dec
     dec.close()
 
@@ -318,17 +318,7 @@ def nopoint_decoder():
 # kernels (<= 16 KiB) or the large-block tile pass; <= 512 small blocks run
 # the single-pass fused kernel unless the context was opened with NO_FUSED;
 # big blocks (> 64 rows, or past the tile span) go to okv_copy_kernel on either.
-# Past the fused batch, small blocks take the grouped single pass
-# (okv_group_kernel) unless the context was opened with NO_GROUP; "group"
-# forces it for any batch (a NO_FUSED context).
-PATHS = ["as_given", "fused", "nofused", "group", "large"]
-_GROUP_DEC = {}
-
-
-def _group_decoder():
-    if "d" not in _GROUP_DEC:
-        _GROUP_DEC["d"] = okv.Decoder(0, flags=_lib.OPEN_NO_FUSED | _lib.OPEN_NO_POINT)
-    return _GROUP_DEC["d"]
+PATHS = ["as_given", "fused", "nofused", "large"]
 
 
 def decode_path(path, decoder, nofused, seg, d, nopoint=None, **kw):
@@ -345,8 +335,6 @@ def decode_path(path, decoder, nofused, seg, d, nopoint=None, **kw):
     if path in ("fused", "large"):
         assert nopoint is not None
         dec = nopoint
-    elif path == "group":
-        dec = _group_decoder()
     else:
         dec = nofused if path == "nofused" else decoder
     got = dec.decode(seg, d, **kw)
@@ -355,12 +343,10 @@ def decode_path(path, decoder, nofused, seg, d, nopoint=None, **kw):
         if path != "as_given":
             assert not lp & _lib.PATH_POINT, lp
         if path == "nofused":
-            assert not lp & (_lib.PATH_FUSED | _lib.PATH_GROUP), lp
-        if path == "group" and not kw.get("index_only") and not lp & _lib.PATH_TILE:
-            assert lp & _lib.PATH_GROUP, lp
+            assert not lp & _lib.PATH_FUSED, lp
         if path == "large":
             # the large-block pass ran (not the small-block kernels)
-            assert not lp & (_lib.PATH_FUSED | _lib.PATH_SMALL | _lib.PATH_GROUP), lp
+            assert not lp & (_lib.PATH_FUSED | _lib.PATH_SMALL), lp
             if not kw.get("index_only"):
                 assert lp & (_lib.PATH_TILE | _lib.PATH_SWEEP), lp
     return got, seg
@@ -608,17 +594,16 @@ def test_large_batch_with_big_blocks(decoder, index_only):
 
 
 def test_large_batches_of_small_blocks(decoder, nofused_decoder, golden):
-    """More than 512 small blocks: the grouped single pass (okv_group_kernel;
-    index-only: count + okv_gather_small_kernel) -- 3 000 mixed blocks (4 KiB,
-    over-kRCap blocks for okv_copy_kernel), and the crafted edge blocks
-    repeated past 512 -- equal to the oracle and to the two-pass path of a
-    NO_FUSED | NO_GROUP context."""
+    """More than 512 small blocks: passes 1-3 as three launches (count, scan,
+    staged gather) -- 3 000 mixed blocks (4 KiB, over-kRCap blocks for
+    okv_copy_kernel), and the crafted edge blocks repeated past 512 -- equal
+    to the oracle and to the OKV_OPEN_NO_FUSED context."""
     rng = np.random.default_rng(5)
     kinds = list(rng.choice(["s"] * 12 + ["M"], size=3000))
     seg, d = _mixed_segment(kinds, 8)
     for index_only in (False, True):
         got = decoder.decode(seg, d, index_only=index_only)
-        assert decoder.last_path() & (_lib.PATH_GROUP if not index_only else _lib.PATH_SMALL)
+        assert decoder.last_path() & (_lib.PATH_SMALL | _lib.PATH_GATHER)
         assert not decoder.last_path() & (_lib.PATH_STREAM | _lib.PATH_FUSED)
         _assert_same_as_oracle(got, seg, d, 0, index_only)
         ref = nofused_decoder.decode(seg, d, index_only=index_only)

@@ -20,12 +20,14 @@ ABLATION_ONLY = [b"okv_value_sweep_kernel", b"okv_rows_kernel", b"okv_gather_sta
                  b"okv_gather_kernel", b"okv_tile_kernel_w7", b"okv_scan_kernel",
                  b"okv_tile_kernel_diag",
                  # round 4's measured-and-not-kept forms
-                 b"okv_decode_stream_kernel", b"okv_enc_plan_kernel", b"fused_prefix_lookback"]
+                 b"okv_decode_stream_kernel", b"okv_enc_plan_kernel", b"fused_prefix_lookback",
+                 # round 6's
+                 b"okv_group_kernel", b"okv_tile_kernel_skip"]
 KNOBS = [b"OKV_GATHER_THREADS", b"OKV_GATHER_GRID", b"OKV_DECODE_FUSED", b"OKV_GATHER_STAGED",
          b"OKV_VALUE_SWEEP", b"OKV_TILE", b"OKV_ZSTD_GENERAL", b"OKV_ZSTD_PROF",
          b"OKV_ENC_VARIANT", b"OKV_ENC_IMAGE", b"OKV_DECODE_PIECES", b"OKV_DECODE_STREAM",
          b"OKV_SMALL_PIECE_MB", b"OKV_COUNT_PREFETCH", b"OKV_ENC_ONEPASS", b"OKV_ENC_META_FUSED",
-         b"OKV_ZSTD_HUF_BLOCKS"]
+         b"OKV_ZSTD_HUF_BLOCKS", b"OKV_DECODE_GROUP"]
 
 
 def _bytes(path):
@@ -65,7 +67,7 @@ def test_product_source_holds_only_product_kernels():
         assert src.rfind("#ifdef OKV_ABLATE", 0, inc) > src.rfind("#endif", 0, inc), inc_name
     # round 4's arms are in the includes, not in the product translation units
     for name in ("okv_decode_stream_kernel", "launch_plan_pieces", "launch_count_piece",
-                 "piece_params"):
+                 "piece_params", "okv_group_kernel", "ensure_group"):
         assert not re.search(r"\b" + name + r"\s*\([^;]*\)\s*\{", src), name
     enc = open(os.path.join(ROOT, "objectkv_amd", "csrc", "okv_encode.hip")).read()
     for name in ("okv_enc_plan_kernel", "enc_plan_fast"):

@@ -37,7 +37,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s device-resident SST block decode + M rows/s, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_ROUND = "r5"  # profiles/<round>/pmc_<config>_<mode>.json (FETCH/WRITE_SIZE passes)
+PMC_ROUND = "r6"  # profiles/<round>/pmc_<config>_<mode>.json (FETCH/WRITE_SIZE passes)
 
 CONFIGS = {
     # name: (synth kind, seed, nblocks, threshold, block size, description)

@@ -144,19 +144,27 @@ def test_point_many_rows(decoder):
 
 
 def test_point_c3_blocks(decoder, nopoint):
-    """16 C3 (64 KiB Zipf) blocks and 16 C2 (4 KiB) blocks: point == device
-    path == oracle."""
-    for kind, th, bs in ((okv.sst.SYNTH_ZIPF, 57344, 65536), (okv.sst.SYNTH_FIXED, 3584, 4096)):
+    """8 C3 (64 KiB Zipf) blocks (512 KiB: the point path's byte cap) and 16 C2
+    (4 KiB) blocks: point == device path == oracle; 16 C3 blocks (1 MiB) take
+    the device path (measured faster past the cap)."""
+    for kind, th, bs, nb in ((okv.sst.SYNTH_ZIPF, 57344, 65536, 8),
+                             (okv.sst.SYNTH_FIXED, 3584, 4096, 16)):
         w = okv.synth_segment(kind, 12, nblocks=40, threshold=th, block_size=bs)
         seg, d = w.data(), w.descs()
         for b0 in (0, 16, 23):
-            dd = d[b0:b0 + 16].copy()
+            dd = d[b0:b0 + nb].copy()
             base = int(dd[0][0])
             span = seg.tobytes()[base:int(dd[-1][0] + dd[-1][1])]
             dd[:, 0] -= base
             got = _point(decoder, span, dd)
             _assert_same_as_oracle(got, span, dd, 0, False)
             _same(got, nopoint.decode(span, dd))
+        if kind == okv.sst.SYNTH_ZIPF:  # past the byte cap: the device path
+            dd = d[0:16].copy()
+            span = seg.tobytes()[:int(dd[-1][0] + dd[-1][1])]
+            got = decoder.decode(span, dd)
+            assert not decoder.last_path() & _lib.PATH_POINT, decoder.last_path()
+            _assert_same_as_oracle(got, span, dd, 0, False)
 
 
 def test_point_capacity_error(decoder, golden):

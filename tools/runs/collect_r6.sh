@@ -4,7 +4,7 @@
 #   tools/runs/collect_r6.sh <tag>
 set -e
 cd "$(dirname "$0")/../.."
-T=${1:-final6}
+T=${1:-r6fin}
 S=gpurun_out/$T
 D=profiles/r6
 mkdir -p $D

@@ -14,7 +14,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 export TMPDIR=/tmp
 PART=${1:-a}
-T=${2:-final6}
+T=${2:-r6fin}
 O="$R/gpurun_out/$T"
 mkdir -p "$O"
 step() {

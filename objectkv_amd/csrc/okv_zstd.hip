@@ -662,6 +662,8 @@ struct ZBlk {
   int32_t kind;           // kKindDone / kKindSeq / kKindSlow
   int32_t st;             // kOK / kErr / kCap of the stage that owns the block
   uint32_t nseq_ok;       // sequences the sequence stage decoded (all unless the stream overflowed)
+  uint32_t pfix;          // bit 31: the last one read past the stream's start: its position (bits
+                          // 0-20) and offset code (21-25)
   uint32_t bmax;          // Block_Maximum_Size of the block's frame (<= 128 KiB)
   // kFlagHuf: the Huffman literal streams are left to okv_zstd_huf_kernel
   uint64_t hq_off;        // the first stream (after the jump table), from the segment's start
@@ -1816,20 +1818,25 @@ __device__ __forceinline__ uint32_t lb_take(LaneBits& b, uint32_t k) {
 }
 
 // 128-bit window reader for the sequence stage.  The window holds aligned
-// dwords [wd, wd + 4); the three dwords below it are loaded unconditionally at
-// the end of every sequence and only read at the end of the next one, after the
-// next table gathers have drained the load queue -- so the stream never stalls
-// the lane chain.  One sequence reads <= 89 bits; the window always holds > 96.
+// dwords [wd, wd + 4); the three dwords below it are loaded (one 12-byte load)
+// unconditionally at the end of every sequence and only read at the end of the
+// next one, after the next table gathers have drained the load queue -- so the
+// stream never stalls the lane chain.  One sequence reads <= 89 bits; the
+// window always holds > 96.  Bits below the stream's start are not masked: the
+// chain reads them only as the state bits of a sequence that starts past the
+// stream (libzstd's overflow), which is not stored; the extra bits are read
+// by the executor (bits_below), which masks them.
+typedef uint32_t Dw3 __attribute__((ext_vector_type(3)));
 struct WinBits {
   LaneBits f;             // ab / s0 / n (masking), P
   int32_t wd;
   uint64_t lo, hi;        // dwords wd+1:wd, wd+3:wd+2 (masked)
-  uint32_t l0, l1, l2;    // raw dwords wd-1, wd-2, wd-3 (in flight)
+  Dw3 nx;                 // raw dwords from max(wd - 3, 0) (in flight)
 };
 __device__ __forceinline__ void wb_issue(WinBits& w) {
-  w.l0 = lb_raw(w.f, w.wd - 1);
-  w.l1 = lb_raw(w.f, w.wd - 2);
-  w.l2 = lb_raw(w.f, w.wd - 3);
+  // (clamped at the stream's first dword: a window that reaches below it
+  // takes its dwords from the clamped load, wb_slide)
+  w.nx = *(const __attribute__((address_space(1))) Dw3*)(w.f.ab + 4 * max(w.wd - 3, 0));
 }
 // k <= 31 bits at window bit pos: the two dwords around it (selects, no
 // branches) and one funnel shift.
@@ -1872,13 +1879,11 @@ __device__ __forceinline__ void wb_slide(WinBits& w) {
   const int32_t dtop = ((w.f.P + 31) >> 5) - 1;
   int32_t sft = w.wd + 3 - dtop;
   sft = sft < 0 ? 0 : (sft > 3 ? 3 : sft);
-  // dwords below the window only meet the stream's low end (its top was
-  // masked when the window was filled): clear the bytes below s0
-  auto low = [&](uint32_t v, int32_t d) {
-    const int32_t cut = min(max(w.f.s0 - 4 * d, 0), 4);
-    return cut >= 4 ? 0u : (v & (0xffffffffu << (8 * cut)));
-  };
-  const uint32_t c0 = low(w.l2, w.wd - 3), c1 = low(w.l1, w.wd - 2), c2 = low(w.l0, w.wd - 1);
+  // dwords wd - 3, wd - 2, wd - 1 (a load clamped at dword 0, wd < 3: dwords
+  // 0 and 1 from their places in it; the dwords before the stream are garbage)
+  const bool full = w.wd >= 3;
+  const uint32_t c0 = w.nx.x, c1 = full ? w.nx.y : w.nx.x,
+                 c2 = full ? w.nx.z : (w.wd == 2 ? w.nx.y : w.nx.x);
   // the last reads of the dwords in flight before the next loads: those then
   // reuse their registers (a load hoisted above these reads needs other
   // registers and a loop-carried copy, which waits for it)
@@ -1896,17 +1901,19 @@ __device__ __forceinline__ void wb_slide(WinBits& w) {
   wb_issue(w);
 }
 
-// Packed sequence, as the bitstream gives it: literal-length code (6 bits) |
+// A sequence as the sequence stage leaves it: literal-length code (6 bits) |
 // its extra bits (16) << 6 | match-length code (6) << 22 | extra bits (16) << 28
-// | offset (20, saturated) << 44.  The executor turns codes into lengths and
-// makes the execution checks (RFC 8878 3.1.1.4) in sequence order; an offset
-// past 2^20 - 1 is past any single-block frame's output, which the executor
-// holds to Block_Maximum_Size (<= 128 KiB, ZBlk::bmax) before the offset check,
-// so the saturated value fails the same check.
+// | the offset value (ofv = 2^code + extra bits, saturated at 2^20 - 1) << 44.
+// The executor resolves repeat offsets (a scan over its window of sequences),
+// turns codes into lengths and makes the execution checks (RFC 8878 3.1.1.4)
+// in sequence order.  An offset past 2^20 - 4 is past any single-block frame's
+// output, which the executor holds to Block_Maximum_Size (<= 128 KiB, ZBlk::bmax)
+// before the offset check, so the saturated value (and any repeat of it)
+// fails the same check.
 __device__ __forceinline__ uint64_t seq_pack(uint32_t llc, uint32_t llx, uint32_t mlc, uint32_t mlx,
-                                             uint32_t off) {
+                                             uint32_t ofv) {
   return uint64_t(llc | (llx << 6) | (mlc << 22)) | (uint64_t(mlx) << 28) |
-         (uint64_t(min(off, 0xfffffu)) << 44);
+         (uint64_t(min(ofv, 0xfffffu)) << 44);
 }
 }  // namespace zst
 
@@ -1983,12 +1990,14 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
   const zst::ZBlk z = zb[b];
   if (z.st != zst::kOK) {  // the literal streams failed (okv_zstd_huf_kernel): nothing to decode
     zb[b].nseq_ok = 0;
+    zb[b].pfix = 0;
     return;
   }
   const uint16_t* T = tl + lane * zst::kTabEnt;
   uint64_t* S = seqs + seq_off[b];
   int32_t st = zst::kOK;
   uint32_t nok = 0;  // sequences decoded before any overflow
+  uint32_t fix = 0;  // bit 31: the last stored sequence needs its extras masked (ZBlk::pfix)
   zst::WinBits br;
   {
     const uintptr_t a = reinterpret_cast<uintptr_t>(z.stream);
@@ -2011,10 +2020,10 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
     uint32_t sof = zst::wb_take(br, ofa);
     uint32_t sml = zst::wb_take(br, mla);
     zst::wb_slide(br);
-    uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
     const int32_t P0 = 8 * br.f.s0;
+    int32_t pl = 0, pfix = 0;
     // software-pipelined: sequence i + 1's three state lookups are issued as
-    // soon as its states are known, before sequence i's value work
+    // soon as its states are known, before the window slide
     uint32_t ell = T[sll & 511], eof = T[512 + (sof & 255)], eml = T[768 + (sml & 511)];
     // No breaks: a failed check sets st and the loop ends at its head.  An
     // early exit would make the window loads in flight at the latch
@@ -2030,9 +2039,10 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
       const bool over = br.f.P < P0;
       // Every field's position follows from the three states: offset extra
       // bits, then ML, then LL extra bits, then the LL / ML / OF state bits
-      // (read high to low).  The state bits and both length extras come out
-      // of ONE 64-bit window read (<= 26 + 16 + 16 bits), the offset extras of
-      // one 32-bit read.
+      // (read high to low).  Only the state bits feed the chain: the extra
+      // bits, the values and the repeat offsets are the executor's
+      // (okv_zstd_exec_kernel, a lane per sequence), which reads them at the
+      // stored stream position.
       const zst::St16 L = zst::st16(ell, lla), O = zst::st16(eof, ofa), M = zst::st16(eml, mla);
       const uint32_t ofs = O.sym, xml = zst::ml_xbits(M.sym), xll = zst::ll_xbits(L.sym);
       const uint32_t nsb = i + 1 < z.nseq ? L.nb + M.nb + O.nb : 0u;
@@ -2044,39 +2054,38 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
       const uint32_t llx = uint32_t(e >> nsb) & zst::lowmask(xll);
       const uint32_t mlx = uint32_t(e >> (nsb + xll)) & zst::lowmask(xml);
       // next states (an unused last update reads nothing: nsb = 0) and their
-      // entries, in flight during this sequence's value work
+      // entries, in flight during the window slide
       sll = L.base + (sbits >> (M.nb + O.nb));
       sml = M.base + ((sbits >> O.nb) & zst::lowmask(M.nb));
       sof = O.base + (sbits & zst::lowmask(O.nb));
       ell = T[sll & 511];
       eof = T[512 + (sof & 255)];
       eml = T[768 + (sml & 511)];
+      pend_seq = zst::seq_pack(L.sym, llx, M.sym, mlx, (1u << ofs) + ofx);
+      // the start (< 2^21) and offset code of the sequence stored at the top
+      // of this iteration, kept for the one that reads past the stream's
+      // start (below)
+      pfix = over ? pl : pfix;
+      pl = br.f.P | int32_t(ofs << 21);
       br.f.P -= int32_t(ofs + xml + xll + nsb);
       zst::wb_slide(br);
-      const uint32_t ofv = (1u << ofs) + ofx;
-      // repeat offsets (RFC 8878 3.1.1.5), branch-free: ofv > 3 is a new
-      // offset; else idx = ofv - 1 (+1 when ll == 0, i.e. literal-length
-      // code 0: every other code's baseline is >= 1) picks rep0/rep1/rep2/rep0-1
-      const bool fresh = ofv > 3;
-      const uint32_t idx = ofv - 1 + (L.sym == 0 ? 1u : 0u);  // 0..3 when !fresh
-      uint32_t t = idx == 3 ? rep0 - 1 : (idx == 1 ? rep1 : rep2);
-      t += t == 0;  // libzstd: offset 0 is corrupt input, forced to 1
-      const uint32_t off = fresh ? ofv - 3 : (idx == 0 ? rep0 : t);
-      const bool sh1 = fresh || idx != 0, sh2 = fresh || idx >= 2;
-      rep2 = sh2 ? rep1 : rep2;
-      rep1 = sh1 ? rep0 : rep1;
-      rep0 = sh1 ? off : rep0;
       // the stream overflowed before this sequence: it is not stored; the
       // execution checks of the sequences before it come first (executor)
       st = over ? zst::kErr : zst::kOK;
-      pend_seq = zst::seq_pack(L.sym, llx, M.sym, mlx, off);
       nok += over ? 0u : 1u;
     }
     if (st == zst::kOK && z.nseq) S[z.nseq - 1] = pend_seq;
+    // The last stored sequence may read extra bits past the stream's start
+    // (libzstd's overflow: the next sequence, if any, is not stored), which
+    // the window does not mask: the executor reads that one's extra bits
+    // again from the stream, those bits as 0 (bits_below).
+    if (st != zst::kOK) fix = uint32_t(pfix) | 0x80000000u;  // overflow before the next sequence
+    else if (z.nseq && br.f.P < P0) fix = uint32_t(pl) | 0x80000000u;
     if (st == zst::kOK && br.f.P > P0) st = zst::kErr;  // unread bits
   }
   zb[b].st = st;  // the executor ranks it after the sequences' own checks
   zb[b].nseq_ok = nok;
+  zb[b].pfix = fix;
 }
 
 // ---- stage 3: execution, one wave per segment block --------------------------------
@@ -2096,6 +2105,90 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
     }                             \
   } while (0)
 namespace zst {
+// Bits [P - 64, P) of a sequence stream (bytes outside it read as 0, as the
+// sequence stage reads them): bit 63 is stream bit P - 1.
+__device__ __forceinline__ uint64_t bits_below(const LaneBits& f, int32_t P) {
+  const int32_t a = P - 64;
+  const int32_t d0 = a >> 5;  // (arithmetic: a < 0 reads zero dwords)
+  const uint32_t s = uint32_t(a) & 31u;
+  const uint32_t w0 = lb_dw(f, d0), w1 = lb_dw(f, d0 + 1), w2 = lb_dw(f, d0 + 2);
+  return uint64_t(__builtin_amdgcn_alignbit(w1, w0, s)) |
+         (uint64_t(__builtin_amdgcn_alignbit(w2, w1, s)) << 32);
+}
+// The next k (<= 31) bits from the top of g.
+__device__ __forceinline__ uint32_t take_top(uint64_t& g, uint32_t k) {
+  const uint32_t v = k ? uint32_t(g >> (64u - k)) : 0u;
+  g <<= k;
+  return v;
+}
+
+// Repeat offsets (RFC 8878 3.1.1.5) as maps of the state (rep0, rep1, rep2),
+// so a wave resolves 256 sequences' offsets with one scan instead of a lane
+// chain.  Slot j of the new state is a constant, or max(r_src - k, 1) of the
+// old state; maps of that form compose into that form (max(max(x - a, 1) - b,
+// 1) = max(x - a - b, 1)), and every state value is >= 1.  A slot is one
+// dword: the constant or k (bits 0-23: offsets are saturated at 2^20 - 1, k
+// counts sequences of one window) | src << 24 | const << 26.
+struct RepMap {
+  uint32_t s0, s1, s2;
+};
+constexpr uint32_t kRepConst = 1u << 26;
+__device__ __forceinline__ RepMap rep_id() { return RepMap{0u, 1u << 24, 2u << 24}; }
+// One sequence's map: a new offset (ofv > 3) -> (ofv - 3, r0, r1); else idx =
+// ofv - 1 (+1 when the literal length is 0): 0 -> unchanged, 1 -> (r1, r0, r2),
+// 2 -> (r2, r0, r1), 3 -> (r0 - 1, r0, r1), where a 0 offset becomes 1 (libzstd).
+__device__ __forceinline__ RepMap rep_map(uint32_t ofv, bool ll0) {
+  const bool fresh = ofv > 3;
+  const uint32_t idx = ofv - 1 + (ll0 ? 1u : 0u);
+  const uint32_t a = fresh ? (kRepConst | (ofv - 3)) : idx == 1 ? (1u << 24) : idx == 2 ? (2u << 24)
+                                                                             : idx == 3 ? 1u : 0u;
+  return RepMap{a, (!fresh && idx == 0) ? (1u << 24) : 0u, (fresh || idx >= 2) ? (1u << 24) : (2u << 24)};
+}
+__device__ __forceinline__ uint32_t rep_sel(uint32_t j, uint32_t a, uint32_t b, uint32_t c) {
+  return j == 0 ? a : j == 1 ? b : c;
+}
+// slot j of (a, then b)
+__device__ __forceinline__ uint32_t rep_slot(const RepMap& a, uint32_t sb) {
+  const uint32_t sa = rep_sel((sb >> 24) & 3u, a.s0, a.s1, a.s2);
+  const uint32_t vb = sb & 0xffffffu, va = sa & 0xffffffu;
+  return (sb & kRepConst) ? sb : (sa & kRepConst) ? (kRepConst | (va > vb ? va - vb : 1u)) : sa + vb;
+}
+__device__ __forceinline__ RepMap rep_compose(const RepMap& a, const RepMap& b) {
+  return RepMap{rep_slot(a, b.s0), rep_slot(a, b.s1), rep_slot(a, b.s2)};
+}
+__device__ __forceinline__ uint32_t rep_val(uint32_t s, uint32_t r0, uint32_t r1, uint32_t r2) {
+  const uint32_t x = rep_sel((s >> 24) & 3u, r0, r1, r2), v = s & 0xffffffu;
+  return (s & kRepConst) ? v : (x > v ? x - v : 1u);
+}
+__device__ __forceinline__ void rep_apply(const RepMap& m, uint32_t& r0, uint32_t& r1, uint32_t& r2) {
+  const uint32_t n0 = rep_val(m.s0, r0, r1, r2), n1 = rep_val(m.s1, r0, r1, r2),
+                 n2 = rep_val(m.s2, r0, r1, r2);
+  r0 = n0;
+  r1 = n1;
+  r2 = n2;
+}
+// One DPP step of the wave scan of maps: lanes without a source keep the
+// identity (bound_ctrl off), so every lane composes.
+template <int kCtrl, int kRows>
+__device__ __forceinline__ RepMap rep_dpp(const RepMap& m) {
+  const RepMap id = rep_id();
+  const RepMap y{uint32_t(__builtin_amdgcn_update_dpp(int(id.s0), int(m.s0), kCtrl, kRows, 0xf, false)),
+                 uint32_t(__builtin_amdgcn_update_dpp(int(id.s1), int(m.s1), kCtrl, kRows, 0xf, false)),
+                 uint32_t(__builtin_amdgcn_update_dpp(int(id.s2), int(m.s2), kCtrl, kRows, 0xf, false))};
+  return rep_compose(y, m);
+}
+// Inclusive scan of the lanes' maps (lane order = sequence order), DPP as
+// wave_scan_dpp.  All 64 lanes active.
+__device__ __forceinline__ RepMap rep_scan(RepMap m) {
+  m = rep_dpp<0x111, 0xf>(m);  // row_shr:1
+  m = rep_dpp<0x112, 0xf>(m);  // row_shr:2
+  m = rep_dpp<0x114, 0xf>(m);  // row_shr:4
+  m = rep_dpp<0x118, 0xf>(m);  // row_shr:8
+  m = rep_dpp<0x142, 0xa>(m);  // row_bcast:15
+  m = rep_dpp<0x143, 0xc>(m);  // row_bcast:31
+  return m;
+}
+
 constexpr uint32_t kTerm = 0x80000000u, kLit = 0x40000000u, kIdx = 0x3fffffffu;
 // a global (not flat) byte load: the literal pointer comes from a ZBlk field, so
 // the compiler cannot tell its address space; flat loads would count in lgkmcnt
@@ -2180,6 +2273,17 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
     // execution checks (3.1.1.4) in sequence order, before anything runs; the
     // block's totals for the end checks.  A failed block executes nothing.
     uint32_t O = 0, lp = 0;
+    // the last sequence's extra bits when it read past the stream's start
+    // (okv_zstd_seq_kernel leaves those unmasked): read again, masked
+    const uint32_t pfix = zst::rfl(zb[b].pfix);
+    zst::LaneBits sb;
+    {
+      const uintptr_t a = reinterpret_cast<uintptr_t>(zst::rflp(zb[b].stream));
+      sb.ab = reinterpret_cast<const uint8_t*>(a & ~uintptr_t(3));
+      sb.s0 = int32_t(a & 3);
+      sb.n = int32_t(zst::rfl(zb[b].stream_len));
+    }
+    uint32_t rep0 = 1, rep1 = 4, rep2 = 8;  // repeat offsets before the window
     // (the next window's sequences are loaded while this one is checked: the
     // pass is a chain of windows per block)
     uint64_t nx[4];
@@ -2193,22 +2297,57 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
         cur[u] = nx[u];
         nx[u] = S[min(i0 + 256 + 4u * lane + u, nseq - 1)];
       }
-      uint32_t lt = 0, ot = 0, ll[4], ml[4], of[4];
+      uint32_t lt = 0, ot = 0, ll[4], ml[4], of[4], ofv[4];
+      bool ll0[4];
+      zst::RepMap m = zst::rep_id();
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const uint32_t k = 4 * lane + u;
         const uint64_t vr = cur[u];
         const uint32_t lo = uint32_t(vr), hi = uint32_t(vr >> 32);
         const bool live = k < nrem;
+        const uint32_t lc = lo & 63u, mc = (lo >> 22) & 63u;
+        uint32_t llx = (lo >> 6) & 0xffffu, mlx = ((lo >> 28) | (hi << 4)) & 0xffffu, ov = hi >> 12;
+        if ((pfix >> 31) && i0 + k == nseq - 1) {  // (one lane of one block, rarely)
+          const uint32_t oc = (pfix >> 21) & 31u;
+          uint64_t g = zst::bits_below(sb, int32_t(pfix & 0x1fffffu));
+          const uint32_t ofx = zst::take_top(g, oc);
+          mlx = zst::take_top(g, zst::ml_xbits(mc));
+          llx = zst::take_top(g, zst::ll_xbits(lc));
+          ov = min((1u << oc) + ofx, 0xfffffu);
+        }
         // (baselines computed, not looked up: an LDS table would cost this
         // kernel a workgroup per CU, 11 -> 10)
-        ll[u] = live ? zst::ll_base(lo & 63u) + ((lo >> 6) & 0xffffu) : 0u;
-        ml[u] = live ? zst::ml_base((lo >> 22) & 63u) + (((lo >> 28) | (hi << 4)) & 0xffffu) : 0u;
-        of[u] = live ? hi >> 12 : 0u;
+        ll[u] = live ? zst::ll_base(lc) + llx : 0u;
+        ml[u] = live ? zst::ml_base(mc) + mlx : 0u;
+        ofv[u] = live ? ov : 1u;  // a dead sequence: the identity map
+        ll0[u] = live && lc == 0;
+        m = zst::rep_compose(m, zst::rep_map(ofv[u], ll0[u]));
         lt += ll[u];
         ot += ll[u] + ml[u];
       }
-      uint32_t lpx = wave_incl_scan32(lt, lane) - lt, opx = wave_incl_scan32(ot, lane) - ot;
+      // repeat offsets: the maps of the lanes before this one, applied to the
+      // state before the window, then this lane's sequences in order
+      m = zst::rep_scan(m);
+      {
+        zst::RepMap ex{uint32_t(__shfl_up(int(m.s0), 1, 64)), uint32_t(__shfl_up(int(m.s1), 1, 64)),
+                       uint32_t(__shfl_up(int(m.s2), 1, 64))};
+        if (lane == 0) ex = zst::rep_id();
+        uint32_t r0 = rep0, r1 = rep1, r2 = rep2;
+        zst::rep_apply(ex, r0, r1, r2);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          zst::rep_apply(zst::rep_map(ofv[u], ll0[u]), r0, r1, r2);
+          // (an offset past 2^20 - 1 is past any single-block frame's output,
+          // which is held to Block_Maximum_Size (<= 128 KiB) before the offset
+          // check below, so the saturated value fails the same check)
+          of[u] = 4 * lane + u < nrem ? min(r0, 0xfffffu) : 0u;
+        }
+        rep0 = __builtin_amdgcn_readlane(r0, 63);
+        rep1 = __builtin_amdgcn_readlane(r1, 63);
+        rep2 = __builtin_amdgcn_readlane(r2, 63);
+      }
+      uint32_t lpx = wave_scan_dpp(lt) - lt, opx = wave_scan_dpp(ot) - ot;
       // the lengths back in place for the execution pass: ll (18 bits) | ml (18)
       // << 18 | offset (28) << 36 (lengths < 2^18; a block that fails a check
       // below is never executed)
@@ -2275,7 +2414,7 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
         lt += ll[u];
         ot += ll[u] + ml[u];
       }
-      uint32_t lpx = wave_incl_scan32(lt, lane) - lt, opx = wave_incl_scan32(ot, lane) - ot;
+      uint32_t lpx = wave_scan_dpp(lt) - lt, opx = wave_scan_dpp(ot) - ot;
       uint32_t fit = 0;  // sequences of this lane that end within the byte map
 #pragma unroll
       for (int u = 0; u < kSU; ++u) {

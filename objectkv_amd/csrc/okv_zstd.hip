@@ -1901,6 +1901,36 @@ __device__ __forceinline__ void wb_slide(WinBits& w) {
   wb_issue(w);
 }
 
+// The same slide in two halves, for a window whose dwords below arrive two
+// sequences after their load (okv_zstd_seq_kernel): the shift for the position
+// Pn after the sequence, known early in it; the load of the dwords below the
+// window at wd (issued as soon as wd is known); the shift itself, with the
+// dwords of the load issued a sequence earlier.
+__device__ __forceinline__ int32_t wb_sft(const WinBits& w, int32_t Pn) {
+  const int32_t sft = w.wd + 3 - (((Pn + 31) >> 5) - 1);
+  return sft < 0 ? 0 : (sft > 3 ? 3 : sft);
+}
+__device__ __forceinline__ Dw3 wb_load(const WinBits& w, int32_t wd) {
+  return *(const __attribute__((address_space(1))) Dw3*)(w.f.ab + 4 * max(wd - 3, 0));
+}
+__device__ __forceinline__ void wb_shift(WinBits& w, const Dw3& nx, int32_t sft) {
+  // (the load's first use here, after the sequence's other memory operations:
+  // selects on it hoisted to the sequence's top would wait for it there)
+  uint32_t x = nx.x, y = nx.y, z = nx.z;
+  asm volatile("" : "+v"(x), "+v"(y), "+v"(z)::"memory");
+  const bool full = w.wd >= 3;  // (as wb_slide)
+  const uint32_t c0 = x, c1 = full ? y : x, c2 = full ? z : (w.wd == 2 ? y : x);
+  const uint32_t w0 = uint32_t(w.lo), w1 = uint32_t(w.lo >> 32), w2 = uint32_t(w.hi),
+                 w3 = uint32_t(w.hi >> 32);
+  const uint32_t n0 = sft == 0 ? w0 : sft == 1 ? c2 : sft == 2 ? c1 : c0;
+  const uint32_t n1 = sft == 0 ? w1 : sft == 1 ? w0 : sft == 2 ? c2 : c1;
+  const uint32_t n2 = sft == 0 ? w2 : sft == 1 ? w1 : sft == 2 ? w0 : c2;
+  const uint32_t n3 = sft == 0 ? w3 : sft == 1 ? w2 : sft == 2 ? w1 : w0;
+  w.lo = uint64_t(n0) | (uint64_t(n1) << 32);
+  w.hi = uint64_t(n2) | (uint64_t(n3) << 32);
+  w.wd -= sft;
+}
+
 // A sequence as the sequence stage leaves it: literal-length code (6 bits) |
 // its extra bits (16) << 6 | match-length code (6) << 22 | extra bits (16) << 28
 // | the offset value (ofv = 2^code + extra bits, saturated at 2^20 - 1) << 44.
@@ -2033,19 +2063,29 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
     // iteration: every wait for the window loads also waits for older stores
     // (vmcnt), so the store is issued a whole sequence before that wait.
     uint64_t pend_seq = 0;
-    for (uint32_t i = 0; i < z.nseq && st == zst::kOK; ++i) {
-      if (i) S[i - 1] = pend_seq;
+    // One sequence.  The dwords below the window are loaded as soon as the
+    // sequence's length in bits is known and shifted in at the end of the NEXT
+    // sequence (two load sets, alternating: the loop runs two sequences per
+    // trip), so a load has about two sequences to arrive -- an L2 hit, which
+    // a lane whose window enters a new 64-byte piece takes about every 50
+    // sequences, no longer stalls the wave (profiles/r6/session/zstd_seq_chain_ab.log).
+    // act: the lane still decodes (the second sequence of a trip runs on every
+    // lane of the trip; a lane that ended with the first keeps its state)
+    auto step = [&](uint32_t i, const zst::Dw3& cur, zst::Dw3& nxt, bool act) {
+      if (i && act) S[i - 1] = pend_seq;
       // libzstd: the stream overflowed before this sequence
       const bool over = br.f.P < P0;
       // Every field's position follows from the three states: offset extra
       // bits, then ML, then LL extra bits, then the LL / ML / OF state bits
-      // (read high to low).  Only the state bits feed the chain: the extra
-      // bits, the values and the repeat offsets are the executor's
-      // (okv_zstd_exec_kernel, a lane per sequence), which reads them at the
-      // stored stream position.
+      // (read high to low).  The state bits and both length extras come out
+      // of one 64-bit window read (<= 26 + 16 + 16 bits), the offset extras of
+      // one 32-bit read; the repeat offsets are the executor's (a scan).
       const zst::St16 L = zst::st16(ell, lla), O = zst::st16(eof, ofa), M = zst::st16(eml, mla);
       const uint32_t ofs = O.sym, xml = zst::ml_xbits(M.sym), xll = zst::ll_xbits(L.sym);
       const uint32_t nsb = i + 1 < z.nseq ? L.nb + M.nb + O.nb : 0u;
+      const int32_t Pn = br.f.P - int32_t(ofs + xml + xll + nsb);
+      const int32_t sft = zst::wb_sft(br, Pn);
+      nxt = zst::wb_load(br, br.wd - sft);  // for the next sequence's shift
       const uint32_t p1 = uint32_t(br.f.P - 32 * br.wd) - ofs;  // offset extras at [p1, p1 + ofs)
       const uint32_t p4 = p1 - xml - xll - nsb;                 // state bits at [p4, p4 + nsb)
       const uint64_t e = zst::wb_get64(br, p4);
@@ -2054,25 +2094,37 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
       const uint32_t llx = uint32_t(e >> nsb) & zst::lowmask(xll);
       const uint32_t mlx = uint32_t(e >> (nsb + xll)) & zst::lowmask(xml);
       // next states (an unused last update reads nothing: nsb = 0) and their
-      // entries, in flight during the window slide
+      // entries, in flight during the window shift
       sll = L.base + (sbits >> (M.nb + O.nb));
       sml = M.base + ((sbits >> O.nb) & zst::lowmask(M.nb));
       sof = O.base + (sbits & zst::lowmask(O.nb));
-      ell = T[sll & 511];
-      eof = T[512 + (sof & 255)];
-      eml = T[768 + (sml & 511)];
-      pend_seq = zst::seq_pack(L.sym, llx, M.sym, mlx, (1u << ofs) + ofx);
+      const uint32_t e0 = T[sll & 511], e1 = T[512 + (sof & 255)], e2 = T[768 + (sml & 511)];
+      ell = act ? e0 : ell;
+      eof = act ? e1 : eof;
+      eml = act ? e2 : eml;
+      pend_seq = act ? zst::seq_pack(L.sym, llx, M.sym, mlx, (1u << ofs) + ofx) : pend_seq;
       // the start (< 2^21) and offset code of the sequence stored at the top
       // of this iteration, kept for the one that reads past the stream's
       // start (below)
-      pfix = over ? pl : pfix;
-      pl = br.f.P | int32_t(ofs << 21);
-      br.f.P -= int32_t(ofs + xml + xll + nsb);
-      zst::wb_slide(br);
+      pfix = (act && over) ? pl : pfix;
+      pl = act ? (br.f.P | int32_t(ofs << 21)) : pl;
+      br.f.P = act ? Pn : br.f.P;
+      zst::wb_shift(br, cur, act ? sft : 0);
       // the stream overflowed before this sequence: it is not stored; the
       // execution checks of the sequences before it come first (executor)
-      st = over ? zst::kErr : zst::kOK;
-      nok += over ? 0u : 1u;
+      st = act ? (over ? zst::kErr : zst::kOK) : st;
+      nok += (act && !over) ? 1u : 0u;
+    };
+    zst::Dw3 nb2;
+    // (the first window loads complete before the loop: a load pending at its
+    // head would make the head wait on the loop's own loads every trip)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (no exit between a trip's two sequences: a trip that could end after the
+    // first would leave that one's load pending at the loop's head, and the
+    // head would wait on the loop's own loads every trip)
+    for (uint32_t i = 0; i < z.nseq && st == zst::kOK; i += 2) {
+      step(i, br.nx, nb2, true);
+      step(i + 1, nb2, br.nx, i + 1 < z.nseq && st == zst::kOK);
     }
     if (st == zst::kOK && z.nseq) S[z.nseq - 1] = pend_seq;
     // The last stored sequence may read extra bits past the stream's start

@@ -686,6 +686,7 @@ struct Pro {
   uint16_t* htab;     // kHufSlot entries: this block's Huffman decoding table for the stream stage
   const uint8_t* hq;  // deferred literal streams (huf_on)
   uint32_t hlen[4], hmb, hns, huf_on;
+  uint32_t nseq;      // out: the deferred block's sequence count (lane 0)
 };
 
 __device__ __forceinline__ void prof_add(const Out& o, int k, unsigned long long v) {
@@ -1069,6 +1070,7 @@ sequences:
       z.stream_len = uint32_t(n - at);
       z.lits = rle ? nullptr : lits;
       z.nseq = nseq;
+      pro->nseq = nseq;
       z.lit_total = regen;
       z.cap = uint32_t(min<uint64_t>(o.cap, 0x7fffffffu));
       z.fcs = pro->fcs;
@@ -1622,7 +1624,7 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
     uint32_t nblk, const uint64_t* __restrict__ cap_off, uint8_t* __restrict__ dec,
     uint64_t* __restrict__ dec_len, int32_t* __restrict__ zstatus, uint8_t* __restrict__ lits,
     uint16_t* __restrict__ tabs, uint16_t* __restrict__ htab, zst::ZBlk* __restrict__ zb,
-    unsigned long long* __restrict__ prof) {
+    uint64_t* __restrict__ seq_n, unsigned long long* __restrict__ prof) {
   __shared__ zst::SmemCore sm;
   const int lane = threadIdx.x & 63;
   for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
@@ -1630,6 +1632,7 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
     const Desc d = descs[b];
     int32_t st = OKV_BLK_OK;
     int32_t kind = zst::kKindDone;
+    uint32_t nseq = 0;
     zst::Out o;
     o.prof = prof;  // diagnostics (ablation build, OKV_ZSTD_PROF); null in the product
     o.base = dec + cap_off[b];
@@ -1651,11 +1654,13 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
       pro.htab = htab + uint64_t(b) * zst::kHufSlot;
       pro.seg = seg;
       pro.huf_on = 0;
+      pro.nseq = 0;
       const int32_t r = zst::decode_frames<true>(sm, seg + d.offset, int64_t(d.compressed_size), o,
                                                  nullptr, &pro);
       __syncthreads();
       if (r == zst::kDefer) {
         kind = zst::kKindSeq;
+        nseq = pro.nseq;
       } else if (r == zst::kSlow) {
         kind = zst::kKindSlow;
       } else {
@@ -1665,6 +1670,7 @@ __global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
     if (lane == 0) {
       zb[b].kind = kind;
       zb[b].st = zst::kOK;
+      seq_n[b] = nseq;  // (scanned in place by okv_zstd_seqoff_kernel)
       if (kind == zst::kKindDone) {
         zstatus[b] = st;
         dec_len[b] = st == OKV_BLK_OK ? o.pos : 0;
@@ -1742,17 +1748,26 @@ __global__ __launch_bounds__(64) void okv_zstd_huf_kernel(zst::ZBlk* __restrict_
 #endif
 constexpr uint32_t kHufBlocks = OKV_ZSTD_HUF_BLOCKS;  // blocks per wave of the stream stage
 
-// Exclusive scan of the deferred blocks' sequence counts -> seq_off[nblk + 1].
-__global__ __launch_bounds__(1024) void okv_zstd_seqoff_kernel(const zst::ZBlk* __restrict__ zb,
-                                                               uint32_t nblk,
-                                                               uint64_t* __restrict__ seq_off) {
+namespace zst {
+// One-workgroup exclusive scan of v(i), i < n -> out[i], out[n] = total: each
+// thread owns kScanPer consecutive elements of a tile, their loads all in
+// flight before one block scan per tile (an element per thread per round
+// left a chain of dependent HBM trips: 80 us for CZ's 16 384 blocks).
+constexpr uint32_t kScanPer = 16;
+template <class V>
+__device__ __forceinline__ void block_excl_scan(uint32_t n, V v_of, uint64_t* __restrict__ out) {
   __shared__ uint64_t sm[16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint64_t carry = 0;
-  for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
-    const uint32_t i = b0 + threadIdx.x;
-    const uint64_t v = (i < nblk && zb[i].kind == zst::kKindSeq) ? zb[i].nseq : 0;
-    const uint64_t inc = wave_incl_scan(v, lane);
+  for (uint32_t t0 = 0; t0 < n; t0 += 1024 * kScanPer) {
+    const uint32_t base = t0 + threadIdx.x * kScanPer;
+    uint64_t v[kScanPer];
+    uint64_t sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) v[k] = base + k < n ? v_of(base + k) : 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) sum += v[k];
+    const uint64_t inc = wave_incl_scan(sum, lane);
     if (lane == 63) sm[wave] = inc;
     __syncthreads();
     uint64_t before = 0, tot = 0;
@@ -1760,11 +1775,26 @@ __global__ __launch_bounds__(1024) void okv_zstd_seqoff_kernel(const zst::ZBlk* 
       before += w < wave ? sm[w] : 0;
       tot += sm[w];
     }
-    if (i < nblk) seq_off[i] = carry + before + inc - v;
+    uint64_t run = carry + before + inc - sum;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+      if (base + k < n) out[base + k] = run;
+      run += v[k];
+    }
     carry += tot;
     __syncthreads();
   }
-  if (threadIdx.x == 0) seq_off[nblk] = carry;
+  if (threadIdx.x == 0) out[n] = carry;
+}
+}  // namespace zst
+
+// Exclusive scan of the deferred blocks' sequence counts, in place: seq_off[b]
+// holds block b's count (okv_zstd_pro_kernel: 0 unless deferred) -> its offset,
+// seq_off[nblk] the total.  (A compact array: the ZBlk fields are a line per
+// block, and one workgroup reading 16 384 lines took 80 us.)
+__global__ __launch_bounds__(1024) void okv_zstd_seqoff_kernel(uint32_t nblk,
+                                                               uint64_t* __restrict__ seq_off) {
+  zst::block_excl_scan(nblk, [&](uint32_t i) -> uint64_t { return seq_off[i]; }, seq_off);
 }
 
 namespace zst {
@@ -2157,6 +2187,17 @@ __global__ __launch_bounds__(64) void okv_zstd_seq_kernel(zst::ZBlk* __restrict_
     }                             \
   } while (0)
 namespace zst {
+// Wave64 inclusive max-scan by DPP (wave_scan_dpp's pattern; 0 is the
+// identity: unsigned values).  All 64 lanes active.
+__device__ __forceinline__ uint32_t wave_max_scan_dpp(uint32_t x) {
+  x = max(x, uint32_t(__builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, true)));   // row_shr:1
+  x = max(x, uint32_t(__builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, true)));   // row_shr:2
+  x = max(x, uint32_t(__builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, true)));   // row_shr:4
+  x = max(x, uint32_t(__builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, true)));   // row_shr:8
+  x = max(x, uint32_t(__builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false)));  // row_bcast:15
+  x = max(x, uint32_t(__builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false)));  // row_bcast:31
+  return x;
+}
 // Bits [P - 64, P) of a sequence stream (bytes outside it read as 0, as the
 // sequence stage reads them): bit 63 is stream bit P - 1.
 __device__ __forceinline__ uint64_t bits_below(const LaneBits& f, int32_t P) {
@@ -2260,7 +2301,7 @@ __device__ __forceinline__ uint32_t gload_u8(const uint8_t* p) {
 constexpr uint32_t kExecOut = OKV_ZSTD_EXEC_OUT;
 constexpr int kEU = int(kExecOut / 1024);
 #ifndef OKV_ZSTD_GQ
-#define OKV_ZSTD_GQ 1
+#define OKV_ZSTD_GQ 2
 #endif
 #ifndef OKV_ZSTD_GB
 #define OKV_ZSTD_GB 4
@@ -2273,8 +2314,10 @@ constexpr int kEU = int(kExecOut / 1024);
 constexpr int kSU = OKV_ZSTD_SU;
 constexpr uint32_t kSW = 64u * kSU;
 static_assert(kSW <= zst::kSeqChunk, "sequence window (byte map entries are 8-bit)");
-constexpr int kGQ = OKV_ZSTD_GQ;  // gather: output dwords per lane per step (1: 96 registers at the
-                                  // 5-wave cap; 2: 128; 4: 163 -- slower, profiles/r3/r3v, r3z)
+constexpr int kGQ = OKV_ZSTD_GQ;  // gather: output dwords per lane per step (2 since round 6: at
+                                  // the 5-wave cap with 12 B of scratch, executor -2 % against 1,
+                                  // profiles/r6/session/zstd_seq_chain_ab.log; round 3 uncapped:
+                                  // 2: 128 registers, 4: 163 -- slower, profiles/r3/r3v, r3z)
 constexpr int kGB = OKV_ZSTD_GB;  // source resolution: 64-byte groups per batch
 static_assert(kExecOut <= zst::kChunkOut && kExecOut % 1024 == 0 && (kExecOut & (kExecOut - 1)) == 0,
               "exec chunk");
@@ -2467,17 +2510,16 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
         ot += ll[u] + ml[u];
       }
       uint32_t lpx = wave_scan_dpp(lt) - lt, opx = wave_scan_dpp(ot) - ot;
-      uint32_t fit = 0;  // sequences of this lane that end within the byte map
+      uint32_t fit = 0;  // sequences that end within the byte map (a prefix: ballots)
 #pragma unroll
       for (int u = 0; u < kSU; ++u) {
         const uint32_t k = kSU * lane + u;
         rec[k] = make_uint4(opx, ll[u], of[u], lpx);
         lpx += ll[u];
         opx += ll[u] + ml[u];
-        fit += (k < nrem && opx <= kExecOut) ? 1u : 0u;
+        fit += uint32_t(__builtin_popcountll(__ballot(k < nrem && opx <= kExecOut)));
       }
       if (lane == 63) rec[kSW] = make_uint4(opx, 0, 0, lpx);
-      for (int d = 32; d; d >>= 1) fit += __shfl_xor(fit, d, 64);
       const uint32_t cnt = fit ? fit : 1;  // a single long sequence when none fits
       __syncthreads();
       const uint32_t osum = zst::rfl(rec[cnt].x), lsum = zst::rfl(rec[cnt].w);
@@ -2501,12 +2543,7 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
 #pragma unroll
             for (int t = 0; t < 4; ++t) mx = max(mx, (w4[q] >> (8 * t)) & 0xffu);
         }
-        uint32_t run = mx;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const uint32_t y = __shfl_up(run, d, 64);
-          if (lane >= d) run = max(run, y);
-        }
+        uint32_t run = zst::wave_max_scan_dpp(mx);
         run = __shfl_up(run, 1, 64);
         if (lane == 0) run = 0;
 #pragma unroll
@@ -2751,25 +2788,7 @@ __device__ __forceinline__ uint64_t first_region(const Desc& d) {
 __global__ __launch_bounds__(1024) void okv_zstd_cap_kernel(const Desc* __restrict__ descs,
                                                             uint32_t nblk,
                                                             uint64_t* __restrict__ cap_off) {
-  __shared__ uint64_t sm[16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint64_t carry = 0;
-  for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
-    const uint32_t i = b0 + threadIdx.x;
-    const uint64_t v = i < nblk ? first_region(descs[i]) : 0;
-    const uint64_t inc = wave_incl_scan(v, lane);
-    if (lane == 63) sm[wave] = inc;
-    __syncthreads();
-    uint64_t before = 0, tot = 0;
-    for (int w = 0; w < 16; ++w) {
-      before += w < wave ? sm[w] : 0;
-      tot += sm[w];
-    }
-    if (i < nblk) cap_off[i] = carry + before + inc - v;
-    carry += tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) cap_off[nblk] = carry;
+  zst::block_excl_scan(nblk, [&](uint32_t i) -> uint64_t { return first_region(descs[i]); }, cap_off);
 }
 
 // Descriptors of the decompressed blocks for the record walk (passes 1-3):
@@ -2897,9 +2916,8 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
     hipLaunchKernelGGL(okv_zstd_pro_kernel, dim3(std::max(1u, std::min(nblk, pgrid))), dim3(64), 0, s,
                        seg, seg_bytes, descs, nblk, ctx->z_cap_off, ctx->z_dec, ctx->z_dec_len,
                        ctx->z_status, ctx->z_blit, reinterpret_cast<uint16_t*>(ctx->z_tabs), htab, zb,
-                       pprof);
-    hipLaunchKernelGGL(okv_zstd_seqoff_kernel, dim3(1), dim3(1024), 0, s, zb, nblk,
-                       ctx->z_seq_off);
+                       ctx->z_seq_off, pprof);
+    hipLaunchKernelGGL(okv_zstd_seqoff_kernel, dim3(1), dim3(1024), 0, s, nblk, ctx->z_seq_off);
     uint64_t nseq_total = 0;
     OKV_HIP(hipMemcpyAsync(&nseq_total, ctx->z_seq_off + nblk, 8, hipMemcpyDeviceToHost, s));
     if (!ctx->z_ev) OKV_HIP(hipEventCreateWithFlags(&ctx->z_ev, hipEventDisableTiming));
@@ -2936,7 +2954,11 @@ int zstd_run(okv_ctx* ctx, const uint8_t* seg, uint64_t seg_bytes, const Desc* d
                                                   : nblk;
     if (prof) egrid = std::min(egrid, kExecGridMax);
     egrid = std::max(egrid, 1u);
-    hipLaunchKernelGGL(okv_zstd_exec_kernel, dim3(std::min<uint32_t>(nblk, egrid)), dim3(64), 0, s,
+#ifndef OKV_ZSTD_EXEC_PAD  // A/B builds: dynamic LDS per workgroup to lower the executor's occupancy
+#define OKV_ZSTD_EXEC_PAD 0  // (18 / 16 / 11 per CU: slower, zstd_seq_chain_ab.log)
+#endif
+    hipLaunchKernelGGL(okv_zstd_exec_kernel, dim3(std::min<uint32_t>(nblk, egrid)), dim3(64),
+                       OKV_ZSTD_EXEC_PAD, s,
                        zb, nblk, ctx->z_seq_off, ctx->z_seqs, ctx->z_cap_off, ctx->z_dec,
                        ctx->z_dec_len, ctx->z_status, eprof);
   }

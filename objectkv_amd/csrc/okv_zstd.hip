@@ -595,25 +595,36 @@ __device__ __forceinline__ bool huf_stream(const uint16_t* huf, uint32_t mb, con
       r[7] = raw(cd - 8);
     }
   };
-  auto literal = [&](uint32_t i) {
+  auto literal = [&]() {
     const int32_t p0 = P - int32_t(mb);
     const uint32_t idx = uint32_t(c >> uint32_t(p0 - 32 * cd)) & ((1u << mb) - 1u);
     const uint32_t e = huf[idx];
-    out[i] = uint8_t(e & 0xff);
     P -= int32_t(e >> 8);
+    return e & 0xffu;
   };
   // invariant: 32 cd <= P < 32 cd + 64; a literal takes <= mb <= 11 bits, so
   // one refill check (at most one dword) covers two literals: the lanes are
-  // different streams, and each check is a divergent branch
+  // different streams, and each check is a divergent branch.  Literals are
+  // stored four to a dword store once the output is aligned (a byte store per
+  // literal was a store instruction per literal).
   uint32_t i = 0;
-  for (; i + 1 < cnt; i += 2) {
-    refill(2 * int32_t(mb));
-    literal(i);
-    literal(i + 1);
-  }
-  if (i < cnt) {
+  const uint32_t head = min(cnt, (4u - uint32_t(reinterpret_cast<uintptr_t>(out) & 3)) & 3u);
+  for (; i < head; ++i) {
     refill(int32_t(mb));
-    literal(i);
+    out[i] = uint8_t(literal());
+  }
+  for (; i + 3 < cnt; i += 4) {
+    refill(2 * int32_t(mb));
+    const uint32_t b0 = literal();
+    const uint32_t b1 = literal();
+    refill(2 * int32_t(mb));
+    const uint32_t b2 = literal();
+    const uint32_t b3 = literal();
+    *reinterpret_cast<uint32_t*>(out + i) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+  }
+  for (; i < cnt; ++i) {
+    refill(int32_t(mb));
+    out[i] = uint8_t(literal());
   }
   return P == B0;
 }
@@ -1619,7 +1630,12 @@ __global__ __launch_bounds__(1024) void okv_zstd_roff_kernel(const uint64_t* __r
 // tables into HBM.  Raw / RLE / literals-only blocks finish here; a block whose
 // input is one frame holding one compressed block with sequences is deferred to
 // stages 2-3; anything else goes to okv_zstd_kernel (kKindSlow).
-__global__ __launch_bounds__(64) void okv_zstd_pro_kernel(
+// Registers capped for 4 waves per SIMD (128 VGPRs and a few scratch spills; uncapped:
+// 140, 3 waves): prologue 755 -> 715 us at CZ (zstd_seq_chain_ab.log, r6zg).
+#ifndef OKV_ZSTD_PRO_WPE
+#define OKV_ZSTD_PRO_WPE 4
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OKV_ZSTD_PRO_WPE))) void okv_zstd_pro_kernel(
     const uint8_t* __restrict__ seg, uint64_t seg_bytes, const Desc* __restrict__ descs,
     uint32_t nblk, const uint64_t* __restrict__ cap_off, uint8_t* __restrict__ dec,
     uint64_t* __restrict__ dec_len, int32_t* __restrict__ zstatus, uint8_t* __restrict__ lits,

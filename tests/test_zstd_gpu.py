@@ -155,6 +155,32 @@ def test_zstd_staged_equals_general_under_corruption(decoder, one_pass_decoder):
     assert 0 < int((staged.status != 0).sum()) < len(dl)
 
 
+def test_zstd_sequence_section_corruption_wide(decoder, one_pass_decoder):
+    """Bit flips in the back 40 % of 256 frames (the sequences section and its
+    bitstream, whose first bytes are read last): most such streams overflow,
+    so the sequence stage's last stored sequence reads past the stream's start
+    and the executor re-reads its extra bits masked (ZBlk::pfix); corrupt
+    repeat-offset codes go through the executor's repeat-offset scan.
+    Two-sided against libzstd through the oracle (statuses and the rows of the
+    blocks that decode), and the one-pass kernel agrees."""
+    import random
+    from tools.zstd_gen import text_zstd_segment
+    seg, descs, _ = text_zstd_segment(256, 29, 3)
+    b = bytearray(seg.tobytes())
+    rng = random.Random(31)
+    for d in descs:
+        off, csz = int(d[0]), int(d[3])
+        back = max(8, (csz * 2) // 5)
+        for _ in range(1 + rng.randrange(2)):
+            b[off + csz - 1 - rng.randrange(back)] ^= 1 << rng.randrange(8)
+    dl = [tuple(int(x) for x in d) for d in descs]
+    staged = _check(decoder, bytes(b), dl)
+    general = _check(one_pass_decoder, bytes(b), dl)
+    assert np.array_equal(staged.status, general.status)
+    bad = int((staged.status != 0).sum())
+    assert 0 < bad < len(dl)
+
+
 def test_zstd_literal_stream_corruption(decoder, one_pass_decoder):
     """Byte flips in the first KiBs of 48 frames -- the Huffman tree and the
     literal streams, which the staged path decodes in its stream stage

@@ -2508,6 +2508,11 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
     }
     O = 0;
     lp = 0;
+    // (each window's records are loaded as soon as the window before it knows
+    // its length, so the load runs under that window's execution)
+    uint64_t nxr[kSU];
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) nxr[u] = nseq ? S[min(uint32_t(kSU * lane + u), nseq - 1)] : 0;
     for (uint32_t i0 = 0; i0 < nseq;) {
       long long tp0 = prof ? clock64() : 0;
       const uint32_t nrem = nseq - i0;
@@ -2517,8 +2522,7 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
 #pragma unroll
       for (int u = 0; u < kSU; ++u) {
         const uint32_t k = kSU * lane + u;
-        const uint64_t vr = S[i0 + (k < nrem ? k : 0)];
-        const uint64_t v = k < nrem ? vr : 0;
+        const uint64_t v = k < nrem ? nxr[u] : 0;
         ll[u] = uint32_t(v) & 0x3ffff;
         ml[u] = uint32_t(v >> 18) & 0x3ffff;
         of[u] = uint32_t(v >> 36);
@@ -2537,6 +2541,8 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
       }
       if (lane == 63) rec[kSW] = make_uint4(opx, 0, 0, lpx);
       const uint32_t cnt = fit ? fit : 1;  // a single long sequence when none fits
+#pragma unroll
+      for (int u = 0; u < kSU; ++u) nxr[u] = S[min(i0 + cnt + uint32_t(kSU * lane + u), nseq - 1)];
       __syncthreads();
       const uint32_t osum = zst::rfl(rec[cnt].x), lsum = zst::rfl(rec[cnt].w);
       PMARK(0);

@@ -2658,6 +2658,11 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
         // the map: a head byte's wraps, a tail byte's is stale, both ignored),
         // then every byte is loaded from a valid address (an RLE literal or a
         // zero byte reads the block's first output byte) and selected.
+        // the previous chunk's stores visible to this gather's loads (waited
+        // here, not at that chunk's end: they complete under this chunk's
+        // source resolution)
+        __builtin_amdgcn_s_waitcnt(0);
+        __threadfence_block();
         const uint32_t g0 = O >> 2, g1 = (O + osum + 3) >> 2;
         const uint64_t out_a = reinterpret_cast<uint64_t>(out);
         const uint64_t lit_a = reinterpret_cast<uint64_t>(lits);
@@ -2699,6 +2704,8 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
         // one sequence longer than the map: every match byte lands on this
         // sequence's literals or on output before it; stored as aligned dwords
         const uint4 R = rec[0];
+        __builtin_amdgcn_s_waitcnt(0);  // (the previous chunk's stores, as above)
+        __threadfence_block();
         const uint32_t g0 = O >> 2, g1 = (O + osum + 3) >> 2;
         for (uint32_t gb = g0 + lane; gb < g1; gb += 64 * kGQ) {
           const uint8_t* ptr[4 * kGQ];
@@ -2740,8 +2747,6 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
         }
       }
       PMARK(4);
-      __builtin_amdgcn_s_waitcnt(0);  // this chunk's stores visible to the next chunk's loads
-      __threadfence_block();
       __syncthreads();
       PMARK(5);
       pacc[9] += 1;
@@ -2751,6 +2756,8 @@ __global__ __launch_bounds__(64) OKV_ZSTD_EXEC_ATTR void okv_zstd_exec_kernel(
     }
     // literals after the last sequence
     {
+      __builtin_amdgcn_s_waitcnt(0);  // (the last chunk's stores)
+      __threadfence_block();
       const uint32_t tl = lit_total - lp;
       const uint32_t g0 = O >> 2, g1 = (O + tl + 3) >> 2;
       for (uint32_t gb = g0 + lane; gb < g1; gb += 64 * kGQ) {

@@ -14,7 +14,7 @@ step() {
 }
 OKV_LIB=tools/ab/r5/lib_${VAR:-zstmod}.so step tests_var 400 python -u -m pytest tests/test_zstd_gpu.py -m gpu -x -v --timeout 300 --timeout-method thread
 for r in 1 2; do
-  for L in zstd5 ${VAR:-zstmod}; do
+  for L in ${BASE:-zstd5} ${VAR:-zstmod}; do
     OKV_LIB=tools/ab/r5/lib_$L.so step trace_${L}_$r 300 rocprofv3 --kernel-trace --stats -d $O/trace_${L}_$r -o run --output-format csv -- python3 bench.py --config cz --steps 10 --warmup 2 --no-cpu --no-verify
   done
 done

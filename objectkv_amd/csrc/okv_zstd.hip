@@ -1995,9 +1995,10 @@ __device__ __forceinline__ uint64_t seq_pack(uint32_t llc, uint32_t llx, uint32_
 
 // ---- stage 2: sequences, one lane per segment block --------------------------------
 // RFC 8878 3.1.1.3.2 / libzstd ZSTD_decodeSequence for every deferred block at
-// once: each lane owns a block's FSE states and bitstream, checks each
-// sequence exactly as the general kernel does and writes it packed.  64 blocks
-// advance per wave instruction.  The lane chain is one table lookup per state
+// once: each lane owns a block's FSE states and bitstream, checks the stream
+// as the general kernel does and writes each sequence's codes, extra bits and
+// raw offset value (seq_pack; the repeat offsets are the executor's scan).
+// 64 blocks advance per wave instruction.  The lane chain is one table lookup per state
 // per sequence: the 64 blocks' tables live in LDS (16-bit states, 160 KiB: one
 // workgroup per CU), so a step costs its instructions plus an LDS trip, not an
 // HBM / L2 trip (the round-2/3 form gathered 32-bit states from HBM:

@@ -530,7 +530,10 @@ def run_decode(args, torch, okv, D):
         roof_ms = ms["copy"]
     achieved = alg / (roof_ms * 1e-3) / 1e9
     pass3 = tuple(w for w in roof_kernel.replace("(", " ").split() if w.startswith("okv_"))
-    traffic, traffic_src = (None, None) if comp else pmc_traffic(args.config, args.mode, pass3)
+    if comp:  # the zstd stage: its kernels' bytes per decode, summed (zstd sources)
+        traffic, traffic_src = pmc_traffic(args.config, args.mode, ("okv_zstd_",), ZSTD_SOURCES)
+    else:
+        traffic, traffic_src = pmc_traffic(args.config, args.mode, pass3)
 
     # ---- CPU baseline (rank 0, after every rank's timing has finished) ------------
     cpu = None
